@@ -1,0 +1,41 @@
+# Build of the MI355X-native WeightedLD hot path.
+#   make            -> weightedld_amd/libweightedld.so, weightedld_amd/bin/weighted_ld, oracle
+# Everything is compiled for gfx950 only.  -ffp-contract=off: the LdStats
+# epilogue must not be FMA-contracted (Rust never contracts); the pair kernels
+# use explicit fmaf where a fused multiply-add is exact by construction.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := weightedld_amd
+CSRC := $(PKG)/csrc
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Iinclude -I$(CSRC)
+HIP_SRCS := $(CSRC)/encode.hip $(CSRC)/pair_valu.hip $(CSRC)/pair_mfma.hip $(CSRC)/order.hip $(CSRC)/capi.hip
+CXX_SRCS := $(CSRC)/host.cpp
+HDRS := include/weightedld.h $(CSRC)/common.hpp $(CSRC)/kernels.hpp $(CSRC)/pair_common.hpp
+OBJDIR := build/obj
+OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(CXX_SRCS))
+
+all: $(PKG)/libweightedld.so $(PKG)/bin/weighted_ld oracle
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) -x c++ -O3 -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC) -D__HIP_PLATFORM_AMD__ -c $< -o $@
+
+$(PKG)/libweightedld.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS) -lpthread
+
+$(PKG)/bin/weighted_ld: $(CSRC)/cli.cpp $(PKG)/libweightedld.so include/weightedld.h
+	@mkdir -p $(PKG)/bin
+	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $(CSRC)/cli.cpp -L$(PKG) -lweightedld -Wl,-rpath,'$$ORIGIN/..' -lpthread
+
+oracle:
+	$(MAKE) -s -C oracle
+
+clean:
+	rm -rf build $(PKG)/libweightedld.so $(PKG)/bin
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all clean oracle

@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""Headline benchmark: LD site-pairs/s at N=2000 sequences x L=20000 sites (BASELINE config 4).
+
+A "step" is one all_weighted_ld_pairs pass (lib.rs:578-684) over the whole
+synthetic alignment: the pair kernel over this rank's row-block shard, the
+reference-order assembly of the rows with r2 > 0.05 and, for N>1, their RCCL
+gather to rank 0.  Inputs (site codes + weights) are resident in HBM before
+the timed region.  Total work is fixed as N grows (strong scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c5]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU)
+
+Rank 0 prints ONE JSON line.  The CPU baseline (rank 0, N=1 only) is the C
+restatement of the lib.rs simd path (oracle/wld_oracle.c, "port"), threaded
+like rayon over 256x256 chunks, timed on a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+METRIC = "LD site-pairs/sec at N=2000 seq × L=20000 var sites; 1/2/4/8 GPU; %HBM roofline"
+CONFIGS = {
+    # name: (n_seqs, n_sites, r2_threshold, description)
+    "c2": (500, 2000, 0.0, "BASELINE config 2: synthetic 500 seq x 2000 sites, r2_threshold=0.0"),
+    "c4": (2000, 20000, 0.05, "BASELINE config 4: synthetic 2000 seq x 20000 sites, r2_threshold=0.05"),
+    "c5": (5000, 50000, 0.05, "BASELINE config 5: synthetic 5000 seq x 50000 sites, r2_threshold=0.05"),
+}
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+I8_MFMA_PEAK_TOPS = 5000.0  # dense i8 MFMA = 2x bf16 dense 2.5 PF (MI355X_MICROARCH.md Matrix cores)
+F32_VALU_PEAK_TFLOPS = 157.3  # FP32 vector peak (spec)
+
+
+def synth(L, N, seed=0x5EED, block=4096):
+    """bench_weighted_pair_ld.rs:8-28 distribution, seeded: per site a major !=
+    minor from ACGT; each sequence '-' w.p. 0.10, major 0.60, else minor."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    maj = rng.integers(0, 4, size=L)
+    mnr = (maj + rng.integers(1, 4, size=L)) % 4
+    out = np.empty((L, N), dtype=np.uint8)
+    for s0 in range(0, L, block):
+        s1 = min(L, s0 + block)
+        u = rng.random((s1 - s0, N), dtype=np.float32)
+        out[s0:s1] = np.where(u < 0.1, 4, np.where(u < 0.7, maj[s0:s1, None], mnr[s0:s1, None]))
+    return out
+
+
+def pairs_in_rows(L, rb, re_):
+    a0, a1 = min(L, rb * 256), min(L, re_ * 256)
+    return (a1 - a0) * (L - 1) - (a1 - 1 + a0) * (a1 - a0) // 2 if a1 > a0 else 0
+
+
+def chunk_pairs(L, i):
+    n = (L + 255) // 256
+    rf = int(((8 * i + 1) ** 0.5 - 1) / 2)
+    while (rf + 1) * (rf + 2) // 2 <= i:
+        rf += 1
+    while rf * (rf + 1) // 2 > i:
+        rf -= 1
+    row = n - rf - 1
+    col = row + i - rf * (rf + 1) // 2
+    sa = min(L, row * 256 + 256) - row * 256
+    sb = min(L, col * 256 + 256) - col * 256
+    return sa * (sa - 1) // 2 if row == col else sa * sb
+
+
+def cpu_baseline(buf, w, thr, target_s=15.0):
+    """Times the oracle (C restatement of the lib.rs simd path) on the first
+    chunks of the same workload in triu order, sized to ~target_s seconds."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _oracle as O  # checker / baseline only
+
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    L = buf.shape[0]
+    n = (L + 255) // 256
+    nchunks = n * (n + 1) // 2
+
+    def run(k):
+        t0 = time.perf_counter()
+        r = O.all_pairs(buf, w, thr, n_threads=threads, chunk_lo=0, chunk_hi=k)
+        return r["pairs"], time.perf_counter() - t0
+
+    k = min(nchunks, max(threads, 4))
+    p, t = run(k)
+    rate = p / max(t, 1e-9)
+    want = rate * target_s
+    k2, acc = 0, 0
+    while k2 < nchunks and acc < want:
+        acc += chunk_pairs(L, k2)
+        k2 += 1
+    p, t = run(max(k2, 1))
+    return {"value": p / t, "unit": "site-pairs/s", "cores": threads, "kind": "port",
+            "sample": "first %d of %d reference chunks (256x256, triu order) of the same workload = %d pairs in "
+                      "%.1f s; C restatement of the lib.rs simd path (8-lane f32, rayon-style chunk scheduling), "
+                      "gcc -O3 -march=x86-64-v3" % (max(k2, 1), nchunks, p, t)}
+
+
+def load_traffic(config, kernel):
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return t.get("%s/%s" % (config, kernel))
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--kernel", default="auto", choices=["auto", "valu", "mfma"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    sys.path.insert(0, REPO)
+    import weightedld_amd as W
+
+    N, L, thr, desc = CONFIGS[args.config]
+    buf = synth(L, N)
+    weights = W.henikoff_weights(W.SiteSet.from_buffer(buf))  # host pre-pass (lib.rs:340-380)
+    d_buf = torch.from_numpy(buf).to(device)
+    d_w = torch.from_numpy(weights).to(device)
+    torch.cuda.synchronize()
+
+    kernel = {"auto": W.KERNEL_AUTO, "valu": W.KERNEL_VALU, "mfma": W.KERNEL_MFMA}[args.kernel]
+    ctx = W.Context(local_rank, kernel)
+    ctx.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
+    rb, re_ = ctx.shard_chunk_rows(L, world, rank)
+
+    def gather(n):
+        if world == 1:
+            return n
+        cnt = torch.tensor([n], dtype=torch.int64, device=device)
+        cnts = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(cnts, cnt)
+        counts = [int(c.item()) for c in cnts]
+        m = max(counts)
+        if m == 0:
+            return 0
+        packed = torch.zeros((5, m), dtype=torch.int32, device=device)
+        if n:
+            ctx.rows_copy_device(*(packed[i].data_ptr() for i in range(5)))
+        gl = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
+        dist.gather(packed, gl, dst=0)
+        if rank == 0:
+            # shards concatenate in descending rank order (chunk rows descend)
+            rows = torch.cat([gl[g][:, :counts[g]] for g in reversed(range(world))], dim=1)
+            return int(rows.shape[1])
+        return sum(counts)
+
+    def step():
+        n = ctx.run(thr, rb, re_)
+        return gather(n)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kms, oms, rows = [], [], 0
+    for _ in range(args.steps):
+        rows = step()
+        st = ctx.stats()
+        kms.append(st["pair_kernel_ms"])
+        oms.append(st["order_ms"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        km = torch.tensor([float(np.mean(kms))], dtype=torch.float64, device=device)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        kernel_ms = float(km.item())
+    else:
+        kernel_ms = float(np.mean(kms))
+    st = ctx.stats()
+    kern_name = "mfma" if st["kernel"] == W.KERNEL_MFMA else "valu"
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    total_pairs = L * (L - 1) // 2
+    value = total_pairs * args.steps / elapsed
+    shard_pairs = pairs_in_rows(L, rb, re_)
+    # dominant kernel roofline (DESIGN.md "Roofline"): per-launch algorithmic work / HIP-event time
+    if kern_name == "mfma":
+        ops = shard_pairs * 24.0 * N  # 3 weight planes x 4 masked products x N seqs x 2 ops/MAC
+        achieved = ops / (kernel_ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": achieved, "peak": I8_MFMA_PEAK_TOPS, "unit": "TFLOP/s",
+                "frac": achieved / I8_MFMA_PEAK_TOPS}
+    else:
+        ops = shard_pairs * 8.0 * N  # 4 masked f32 sums x N seqs x 2 flops/FMA
+        achieved = ops / (kernel_ms * 1e-3) / 1e12
+        roof = {"bound": "valu", "achieved": achieved, "peak": F32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / F32_VALU_PEAK_TFLOPS}
+    roof["kernel"] = "pair_%s_kernel" % kern_name
+    roof["kernel_ms"] = kernel_ms
+    tr = load_traffic(args.config, kern_name)
+    roof["traffic"] = tr.get("hbm_bytes_per_launch") if tr else None
+    hbm_alg = shard_pairs * 2.0 * N / (kernel_ms * 1e-3) / 1e9  # 2N bytes per pair
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "site-pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "i8" if kern_name == "mfma" else "f32",
+        "data": "synthetic (seeded bench_weighted_pair_ld.rs distribution, Henikoff weights)",
+        "config": {"workload": desc, "n_seqs": N, "n_sites": L, "r2_threshold": thr, "pairs": total_pairs,
+                   "rows_passing": rows, "kernel": kern_name,
+                   "parallelism": "row-block shard x%d%s" % (world, " + RCCL gather" if world > 1 else "")},
+        "roofline": roof,
+        "north_star_hbm_view": {"algorithmic_bytes_per_pair": 2 * N, "achieved_GBps": hbm_alg,
+                                "peak_GBps": HBM_PEAK_GBPS, "frac": hbm_alg / HBM_PEAK_GBPS},
+        "order_ms": float(np.mean(oms)),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(buf, weights, thr, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,216 @@
+/*
+ * weightedld.h — C ABI of the MI355X-native WeightedLD all-pairs LD hot path.
+ *
+ * The reference (ojcharles/WeightedLD, Rust crate rust/weighted_ld) has no FFI;
+ * its hot path is the generic Rust fn
+ *     pub fn all_weighted_ld_pairs(site_set: &SiteSet, weights: &[f32],
+ *                                  r2_threshold: f32,
+ *                                  progress_report: impl FnMut(usize) + Send)
+ *         -> PairStore<LdStats>                               (lib.rs:578-684)
+ * called once from main.rs:180-190.  The entry points below are what a Rust
+ * `extern "C"` binding of that seam needs: plain pointers
+ * and sizes, no Rust/C++/torch types, no exceptions across the boundary, every
+ * call returns a status code (WLD_OK or a negative WLD_E_*), and
+ * wld_last_error() gives the message for the calling thread.
+ *
+ * Symbol codes are the reference's #[repr(u8)] Symbol (lib.rs:20-29):
+ *     A=0 C=1 G=2 T=3 Missing('-')=4 Unknown=5
+ * A "site-major" buffer is SiteSet.buffer (lib.rs:163): buffer[site*n_seqs+seq].
+ */
+#ifndef WEIGHTEDLD_H
+#define WEIGHTEDLD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ status */
+#define WLD_OK 0
+#define WLD_E_ARG (-1)    /* bad argument (the reference would panic)           */
+#define WLD_E_HIP (-2)    /* HIP runtime error                                   */
+#define WLD_E_OOM (-3)    /* device or host allocation failed                    */
+#define WLD_E_NODEV (-4)  /* no usable gfx950 device                             */
+#define WLD_E_IO (-5)     /* file could not be read / written                    */
+#define WLD_E_FORMAT (-6) /* input violates the reference's format (it panics)  */
+#define WLD_E_STATE (-7)  /* call order violated (e.g. run before load)          */
+
+#define WLD_SYM_A 0
+#define WLD_SYM_C 1
+#define WLD_SYM_G 2
+#define WLD_SYM_T 3
+#define WLD_SYM_MISSING 4
+#define WLD_SYM_UNKNOWN 5
+#define WLD_NONE (-1) /* Option<Symbol>::None */
+
+const char *wld_status_string(int status);
+/* Message of the last failed call on this thread ("" if none). */
+const char *wld_last_error(void);
+/* Library version string, e.g. "weightedld-amd 0.1.0 (gfx950)". */
+const char *wld_version(void);
+
+/* ========================================================================
+ * Host pre-pass — stays on the host per north_star.  Mirrors lib.rs:20-380.
+ * ======================================================================== */
+
+/* Opaque SiteSet (lib.rs:158-173): site-major symbol buffer, optional
+ * site_map (filtered index -> parent index, lib.rs:165-169) and per-site
+ * histograms (lib.rs:171-172). */
+typedef struct wld_siteset wld_siteset;
+
+/* read_fasta + SiteSet::from_multiseq (lib.rs:277-307, 176-206), including the
+ * reader's quirks: every non-'>' line is one sequence and its '\n' becomes a
+ * trailing Unknown site.  WLD_E_FORMAT where the reference panics (sequences
+ * of unequal length, lib.rs:180-182; no sequence at all, lib.rs:178). */
+int wld_read_fasta(const char *path, wld_siteset **out);
+
+/* VCF reader following the Python reference's handle_vcf
+ * (WeightedLD.py:311-379): phased diploid calls split into two haplotypes,
+ * '.' -> 4 (Missing), allele digits used as symbol codes, the last data line
+ * dropped (:365), haplotypes in reversed order (np.rot90, :375) and
+ * site_map = POS.  The Rust crate has no VCF input; this serves BASELINE
+ * config 3.  WLD_E_FORMAT where the Python code exits. */
+int wld_read_vcf(const char *path, wld_siteset **out);
+
+/* Builds a SiteSet from a caller buffer (copied); histograms computed as in
+ * from_multiseq (lib.rs:194-196). site_map may be NULL (identity). */
+int wld_siteset_from_buffer(const uint8_t *site_major, size_t n_sites, size_t n_seqs,
+                            const uint64_t *site_map, wld_siteset **out);
+void wld_siteset_free(wld_siteset *s);
+size_t wld_siteset_n_sites(const wld_siteset *s);                        /* lib.rs:254-256 */
+size_t wld_siteset_n_seqs(const wld_siteset *s);                         /* lib.rs:259-261 */
+const uint8_t *wld_siteset_buffer(const wld_siteset *s);                 /* SiteSet.buffer */
+const uint64_t *wld_siteset_site_map(const wld_siteset *s);              /* NULL = identity */
+uint64_t wld_siteset_parent_site_index(const wld_siteset *s, size_t i);  /* lib.rs:263-265 */
+int wld_siteset_histogram(const wld_siteset *s, size_t site, uint64_t out[6]); /* lib.rs:272 */
+
+/* SymbolHistogram::from_slice (lib.rs:98-104) and major_minor_symbols
+ * (lib.rs:126-140): ties keep the earlier of A,C,G,T,-; Unknown never
+ * eligible; WLD_NONE for None. */
+int wld_histogram(const uint8_t *symbols, size_t n, uint64_t out[6]);
+int wld_major_minor(const uint64_t hist[6], int *major, int *minor);
+
+/* is_site_of_interest (lib.rs:309-338); min_acgt is the COUNT
+ * ceil(min_acgt_frac * n_seqs) of main.rs:139.  Returns 1/0. */
+int wld_is_site_of_interest(const uint8_t *site, size_t n, size_t min_acgt, float min_minor,
+                            float max_minor);
+
+/* main.rs:139-143: siteset.filter_by(is_site_of_interest) with
+ * min_acgt = ceil(min_acgt_frac * n_seqs) (f32 arithmetic), i.e.
+ * SiteSet::filter_by (lib.rs:230-251). */
+int wld_siteset_filter_sites_of_interest(const wld_siteset *s, float min_acgt_frac,
+                                         float min_minor, float max_minor, wld_siteset **out);
+
+/* henikoff_weights (lib.rs:340-380), out has n_seqs floats. */
+int wld_henikoff_weights(const wld_siteset *s, float *out);
+
+/* ========================================================================
+ * Device hot path — replaces all_weighted_ld_pairs / single_weighted_ld_pair.
+ * ======================================================================== */
+
+typedef struct wld_ctx wld_ctx;
+
+/* One context per device; owns its HIP stream, device buffers and results.
+ * Not thread-safe; separate contexts are independent.  device = HIP ordinal. */
+int wld_create(int device, wld_ctx **out);
+void wld_destroy(wld_ctx *ctx);
+
+/* Kernel selection.  AUTO (default): the exact-integer MFMA kernel when the
+ * weights are finite and their dynamic range fits its fixed-point weight
+ * planes, else the f32 VALU kernel.  Both run on the GPU; there is no CPU path. */
+#define WLD_KERNEL_AUTO 0
+#define WLD_KERNEL_VALU 1
+#define WLD_KERNEL_MFMA 2
+int wld_set_kernel(wld_ctx *ctx, int kernel);
+
+/* Rows of PairStore<LdStats> (lib.rs:523-576) as structure-of-arrays, in the
+ * reference's order: 256x256 chunks in triu_index order (lib.rs:623-635:
+ * chunk rows descending, columns ascending), then site_a, then site_b
+ * ascending.  Site indices are PARENT indices (lib.rs:662-663).  Only rows
+ * with r2 > r2_threshold (strict, lib.rs:660; NaN never passes). */
+typedef struct {
+    uint64_t n;
+    uint32_t *site_a;
+    uint32_t *site_b;
+    float *d;
+    float *d_prime;
+    float *r2;
+} wld_pairs;
+void wld_pairs_free(wld_pairs *p); /* only for host results made by this library */
+
+/* progress_report (lib.rs:582, main.rs:184-188).  Called on the calling
+ * thread (never from a worker) with the running number of evaluated pairs. */
+typedef void (*wld_progress_fn)(uint64_t pairs_done, void *user);
+
+/* Drop-in for all_weighted_ld_pairs (lib.rs:578-684).  Blocking.  sites is
+ * SiteSet.buffer (n_sites*n_seqs bytes, host memory), site_map the SiteSet's
+ * site_map (NULL = identity), weights n_seqs floats.  Allocates out's host
+ * arrays (release with wld_pairs_free). */
+int wld_all_weighted_ld_pairs(wld_ctx *ctx, const uint8_t *sites, size_t n_sites, size_t n_seqs,
+                              const uint64_t *site_map, const float *weights, float r2_threshold,
+                              wld_progress_fn progress, void *user, wld_pairs *out);
+
+/* Drop-in for single_weighted_ld_pair (lib.rs:390-521) with the histograms of
+ * a and b taken from the slices themselves (as SiteSet does).  Returns 1 and
+ * fills out[3] = {d, d_prime, r2} for Some, 0 for None, <0 on error. */
+int wld_single_weighted_ld_pair(wld_ctx *ctx, const uint8_t *a, const uint8_t *b,
+                                const float *weights, size_t n_seqs, float out[3]);
+
+/* ---- staged API: inputs resident in HBM, shardable, results on device ---- */
+
+/* Uploads a SiteSet (host pointers) and encodes it on the device: per-site
+ * histogram -> major/minor (lib.rs:126-140, hoisted out of the pair loop)
+ * -> per-sequence codes and weight planes.  Replaces any previous load. */
+int wld_load(wld_ctx *ctx, const uint8_t *sites, size_t n_sites, size_t n_seqs,
+             const uint64_t *site_map, const float *weights);
+/* Same, from device pointers already resident in HBM (d_sites: n_sites*n_seqs
+ * bytes site-major; d_weights: n_seqs floats; site_map host, may be NULL). */
+int wld_load_device(wld_ctx *ctx, const void *d_sites, size_t n_sites, size_t n_seqs,
+                    const uint64_t *site_map, const void *d_weights);
+
+/* Number of 256-site chunk rows n = ceil(n_sites/256) (lib.rs:615-619), and a
+ * balanced contiguous partition of chunk rows [begin,end) for shard `shard` of
+ * `n_shards` (equal pair counts up to chunk granularity).  Each shard's rows
+ * are a contiguous run of the reference order; shards concatenate in
+ * DESCENDING shard order (chunk rows descend in triu_index order). */
+uint32_t wld_chunk_rows(size_t n_sites);
+int wld_shard_chunk_rows(size_t n_sites, int n_shards, int shard, uint32_t *begin, uint32_t *end);
+
+/* Evaluates every pair (a<b) whose a lies in chunk rows [row_begin,row_end)
+ * (pass 0, wld_chunk_rows() for all), filters r2 > r2_threshold and leaves
+ * the rows on the device in reference order.  *n_rows receives the count. */
+int wld_run(wld_ctx *ctx, float r2_threshold, uint32_t row_begin, uint32_t row_end,
+            uint64_t *n_rows);
+/* Device pointers of the last run's rows (valid until the next run/load or
+ * destroy; do not free). */
+int wld_rows_device(wld_ctx *ctx, wld_pairs *view);
+/* Copies the last run's rows to caller host arrays of at least n_rows each
+ * (any pointer may be NULL to skip that column). */
+int wld_rows_copy(wld_ctx *ctx, uint32_t *site_a, uint32_t *site_b, float *d, float *d_prime,
+                  float *r2);
+/* Device-to-device copy of the last run's rows into caller device buffers
+ * (e.g. tensors handed to an RCCL gather); NULL skips a column.  Completes
+ * before returning. */
+int wld_rows_copy_device(wld_ctx *ctx, void *site_a, void *site_b, void *d, void *d_prime, void *r2);
+/* Dense stats of every pair a<b of the loaded set into host n_sites*n_sites
+ * row-major matrices (valid[a*L+b] = 1 for Some); for tests. */
+int wld_dense(wld_ctx *ctx, float *d, float *d_prime, float *r2, uint8_t *valid);
+
+typedef struct {
+    int kernel;              /* WLD_KERNEL_VALU or WLD_KERNEL_MFMA actually used   */
+    uint64_t pairs;          /* pairs evaluated (a<b) in the last run              */
+    uint64_t rows;           /* rows that passed the threshold                     */
+    double pair_kernel_ms;   /* HIP-event time of the pair kernel (last run)       */
+    double order_ms;         /* HIP-event time of the ordering kernels (last run)  */
+    double load_ms;          /* HIP-event time of the encode kernel (last load)    */
+    uint64_t pair_kernel_launches;
+    int weight_shift;        /* fixed-point exponent of the MFMA weight planes     */
+} wld_run_stats;
+int wld_last_stats(wld_ctx *ctx, wld_run_stats *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WEIGHTEDLD_H */

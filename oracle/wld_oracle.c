@@ -41,6 +41,9 @@
 
 enum { SYM_A = 0, SYM_C, SYM_G, SYM_T, SYM_MISSING, SYM_UNKNOWN };
 
+typedef float f32x8 __attribute__((vector_size(32)));
+typedef int32_t i32x8 __attribute__((vector_size(32)));
+
 /* lib.rs:53-64 */
 uint8_t wldo_symbol_from_char(uint32_t c) {
     switch (c) {
@@ -202,19 +205,28 @@ int wldo_single_pair_mm(const uint8_t *a, int a_maj, int a_min, const uint8_t *b
     const uint8_t bm = (uint8_t)b_maj, bn = (uint8_t)b_min;
     size_t simd_end = (n / 8) * 8;
 
-    /* :416-445 — 8 independent lanes */
-    float tw[8] = {0}, pa[8] = {0}, pb[8] = {0}, l3[8] = {0};
+    /* :416-445 — 8 lanes, op for op like packed_simd's u8x8 eq / f32x8 select
+     * (GCC vector types; with -march=x86-64-v3 this is AVX2 like the reference's
+     * RUSTFLAGS=-C target-cpu=native build, README.md:88-97). */
+    f32x8 tw = {0}, pa = {0}, pb = {0}, l3 = {0};
     for (size_t seq = 0; seq < simd_end; seq += 8) {
+        i32x8 av, bv;
         for (int j = 0; j < 8; ++j) {
-            int a_mj = a[seq + j] == am, a_mn = a[seq + j] == an;
-            int b_mj = b[seq + j] == bm, b_mn = b[seq + j] == bn;
-            int mask = (a_mj | a_mn) & (b_mj | b_mn);
-            float wt = mask ? w[seq + j] : 0.0f;
-            tw[j] += wt;
-            pa[j] += a_mj ? wt : 0.0f;
-            pb[j] += b_mj ? wt : 0.0f;
-            l3[j] += (a_mj & b_mj) ? wt : 0.0f;
+            av[j] = a[seq + j];
+            bv[j] = b[seq + j];
         }
+        const i32x8 a_maj = av == (i32x8){am, am, am, am, am, am, am, am};
+        const i32x8 a_min = av == (i32x8){an, an, an, an, an, an, an, an};
+        const i32x8 b_maj = bv == (i32x8){bm, bm, bm, bm, bm, bm, bm, bm};
+        const i32x8 b_min = bv == (i32x8){bn, bn, bn, bn, bn, bn, bn, bn};
+        const i32x8 mask = (a_maj | a_min) & (b_maj | b_min);
+        f32x8 wv;
+        memcpy(&wv, w + seq, sizeof wv);
+        const i32x8 wbits = (i32x8)wv & mask; /* mask.select(weight, zero) */
+        tw += (f32x8)wbits;
+        pa += (f32x8)(wbits & a_maj);
+        pb += (f32x8)(wbits & b_maj);
+        l3 += (f32x8)(wbits & (a_maj & b_maj));
     }
     /* :447-452 — horizontal sums (ordered; see header) */
     float total_weight = 0.0f, PA = 0.0f, PB = 0.0f, ld3 = 0.0f;

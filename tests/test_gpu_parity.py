@@ -1,0 +1,314 @@
+"""GPU parity tests: the HIP path through the C ABI against the CPU oracle.
+
+Tolerance: north_star — D, D' and r2 within 1e-5 (f32).  Row sets must match
+exactly except for rows whose r2 lies within 1e-5 of the threshold (a strict
+'>' on floating point sums computed in a different order), and the rows must
+come in the reference order (triu chunk order, then a, then b).
+"""
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from conftest import FIXTURES, REPO, SYNTH
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+KERNELS = ["valu", "mfma"]
+
+
+@pytest.fixture(scope="module")
+def W():
+    import weightedld_amd as W
+    return W
+
+
+@pytest.fixture(scope="module")
+def ctxs(W):
+    out = {"valu": W.Context(0, W.KERNEL_VALU)}
+    if W.lib().wld_set_kernel(out["valu"]._h, W.KERNEL_MFMA) == 0:
+        out["mfma"] = W.Context(0, W.KERNEL_MFMA)
+    out["valu"].set_kernel(W.KERNEL_VALU)
+    return out
+
+
+def _ctx(ctxs, kern):
+    if kern not in ctxs:
+        pytest.skip("%s kernel not built" % kern)
+    return ctxs[kern]
+
+
+def synth(L, N, seed, p_missing=0.1, p_major=0.6, unknown=0.0):
+    """bench_weighted_pair_ld.rs:8-28 distribution, seeded."""
+    rng = np.random.default_rng(seed)
+    maj = rng.integers(0, 4, size=L)
+    mnr = (maj + rng.integers(1, 4, size=L)) % 4
+    u = rng.random((L, N))
+    codes = np.where(u < p_missing, 4, np.where(u < p_missing + p_major, maj[:, None], mnr[:, None]))
+    if unknown:
+        codes = np.where(rng.random((L, N)) < unknown, 5, codes)
+    return codes.astype(np.uint8)
+
+
+def close(x, y, tol=TOL):
+    x = np.asarray(x, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64)
+    both_nan = np.isnan(x) & np.isnan(y)
+    same_inf = np.isinf(x) & np.isinf(y) & (np.sign(x) == np.sign(y))
+    ok = both_nan | same_inf | (np.abs(x - y) <= tol)
+    return ok
+
+
+def compare_dense(gpu, ref, tol=TOL):
+    d, dp, r2, valid = gpu
+    rd, rdp, rr2, rvalid = ref
+    L = d.shape[0]
+    iu = np.triu_indices(L, 1)
+    assert np.array_equal(valid[iu], rvalid[iu])
+    m = rvalid[iu] == 1
+    for g, r in ((d, rd), (dp, rdp), (r2, rr2)):
+        ok = close(g[iu][m], r[iu][m], tol)
+        # D' = D / den is ill-conditioned when den ~ 0: compare relative there
+        assert ok.mean() == 1.0 or np.all(ok | (np.abs(g[iu][m] - r[iu][m]) <= tol * np.maximum(1, np.abs(r[iu][m])))), \
+            (np.argwhere(~ok)[:5], g[iu][m][~ok][:5], r[iu][m][~ok][:5])
+
+
+def compare_rows(store, ref, thr, tol=TOL):
+    ka = list(zip(store.site_a.tolist(), store.site_b.tolist()))
+    kb = list(zip(ref["site_a"].tolist(), ref["site_b"].tolist()))
+    ga = {k: i for i, k in enumerate(ka)}
+    gb = {k: i for i, k in enumerate(kb)}
+    assert len(ga) == len(ka), "duplicate rows"
+    only_gpu = [k for k in ka if k not in gb]
+    only_ref = [k for k in kb if k not in ga]
+    for k in only_gpu:
+        assert abs(store.r2[ga[k]] - thr) <= tol, ("extra row", k, store.r2[ga[k]])
+    for k in only_ref:
+        assert abs(ref["r2"][gb[k]] - thr) <= tol, ("missing row", k, ref["r2"][gb[k]])
+    common = [k for k in ka if k in gb]
+    # same relative order
+    assert [k for k in kb if k in ga] == common
+    ia = np.array([ga[k] for k in common], dtype=np.int64)
+    ib = np.array([gb[k] for k in common], dtype=np.int64)
+    if len(common):
+        assert close(store.d[ia], ref["d"][ib], tol).all()
+        assert close(store.r2[ia], ref["r2"][ib], tol).all()
+        okp = close(store.d_prime[ia], ref["d_prime"][ib], tol)
+        rel = np.abs(store.d_prime[ia] - ref["d_prime"][ib]) <= tol * np.maximum(1.0, np.abs(ref["d_prime"][ib]))
+        assert (okp | rel).all()
+    return len(common), len(only_gpu), len(only_ref)
+
+
+# ------------------------------------------------------------------ known answers
+def test_librs_known_answers_on_gpu(W, librs_ka):
+    for c in librs_ka["ld_pair"]["cases"]:
+        r = W.single_weighted_ld_pair(W.api.symbols_from_str(c["a"]), None, W.api.symbols_from_str(c["b"]), None,
+                                      np.array(c["w"], dtype=np.float32))
+        assert r is not None
+        assert abs(r.d - c["d"]) <= c["tol"] and abs(r.d_prime - c["d_prime"]) <= c["tol"] and abs(r.r2 - c["r2"]) <= c["tol"], (c["ref"], r)
+    assert W.single_weighted_ld_pair(W.api.symbols_from_str("AAAAAAAA"), None, W.api.symbols_from_str("ACACACAC"),
+                                     None, np.ones(8, dtype=np.float32)) is None
+
+
+# ------------------------------------------------------------------ dense parity
+@pytest.mark.parametrize("kern", KERNELS)
+@pytest.mark.parametrize("L,N,seed", [(2, 7, 0), (37, 50, 1), (64, 64, 2), (130, 129, 3), (300, 500, 4), (257, 1000, 5)])
+def test_dense_vs_oracle_synthetic(ctxs, kern, L, N, seed):
+    ctx = _ctx(ctxs, kern)
+    buf = synth(L, N, seed)
+    w = np.random.default_rng(seed + 100).random(N).astype(np.float32)
+    for weights in (w, np.ones(N, dtype=np.float32)):
+        ctx.load(buf, weights)
+        compare_dense(ctx.dense(L), O.all_pairs_dense(buf, weights))
+
+
+@pytest.mark.parametrize("kern", KERNELS)
+def test_dense_vs_oracle_awkward_sites(ctxs, kern):
+    # monomorphic (None), all-Unknown, Missing as minor, ties, Unknown sprinkled
+    ctx = _ctx(ctxs, kern)
+    rng = np.random.default_rng(9)
+    L, N = 90, 77
+    buf = rng.choice(6, size=(L, N), p=[0.3, 0.3, 0.1, 0.1, 0.1, 0.1]).astype(np.uint8)
+    buf[0] = 0
+    buf[1] = 5
+    buf[2] = np.where(np.arange(N) % 2, 0, 4)
+    buf[3] = np.where(np.arange(N) % 3 == 0, 1, 2)
+    w = rng.random(N).astype(np.float32)
+    w[::5] = 0.0
+    ctx.load(buf, w)
+    compare_dense(ctx.dense(L), O.all_pairs_dense(buf, w))
+
+
+def test_dense_nonfinite_weights_valu(ctxs):
+    # non-finite weights force the SAFE select variant (0*inf must not appear)
+    ctx = ctxs["valu"]
+    buf = synth(70, 40, 11)
+    w = np.random.default_rng(3).random(40).astype(np.float32)
+    w[5] = np.inf
+    w[9] = np.nan
+    ctx.load(buf, w)
+    compare_dense(ctx.dense(70), O.all_pairs_dense(buf, w))
+
+
+# ------------------------------------------------------------------ ordered rows
+@pytest.mark.parametrize("kern", KERNELS)
+@pytest.mark.parametrize("L,N,thr", [(1, 10, 0.0), (2, 10, 0.0), (255, 64, 0.0), (256, 100, 0.05), (257, 100, 0.0),
+                                     (700, 300, 0.0), (700, 300, 0.01), (1100, 200, -1.0), (900, 2000, 0.001)])
+def test_rows_vs_oracle(ctxs, kern, L, N, thr):
+    ctx = _ctx(ctxs, kern)
+    buf = synth(L, N, L * 7 + N)
+    w = np.random.default_rng(L).random(N).astype(np.float32) + 0.05
+    site_map = np.arange(L, dtype=np.uint64) * 3 + 11
+    ctx.load(buf, w, site_map)
+    n = ctx.run(thr)
+    store = ctx.rows()
+    assert len(store) == n
+    ref = O.all_pairs(buf, w, thr, site_map=site_map)
+    compare_rows(store, ref, thr)
+    st = ctx.stats()
+    assert st["pairs"] == L * (L - 1) // 2
+
+
+@pytest.mark.parametrize("kern", KERNELS)
+@pytest.mark.parametrize("G", [2, 3, 4])
+def test_sharded_runs_concatenate_to_reference_order(ctxs, kern, G):
+    ctx = _ctx(ctxs, kern)
+    L, N = 1500, 200
+    buf = synth(L, N, 77)
+    w = np.random.default_rng(1).random(N).astype(np.float32)
+    ctx.load(buf, w)
+    ctx.run(0.0)
+    full = ctx.rows()
+    parts = []
+    for g in range(G):
+        b, e = ctx.shard_chunk_rows(L, G, g)
+        ctx.run(0.0, b, e)
+        parts.append(ctx.rows())
+    # chunk rows descend in reference order: shard G-1 comes first
+    cat = lambda f: np.concatenate([getattr(p, f) for p in reversed(parts)])  # noqa: E731
+    for f in ("site_a", "site_b", "d", "d_prime", "r2"):
+        assert np.array_equal(cat(f), getattr(full, f)), f
+
+
+# ------------------------------------------------------------------ API + CLI
+def test_all_weighted_ld_pairs_api_on_fixture(W):
+    ss = W.read_fasta(os.path.join(FIXTURES, "example.fasta"))
+    f = ss.filter_sites_of_interest(0.8, 0.02, 0.5)
+    w = W.henikoff_weights(f)
+    seen = []
+    store = W.all_weighted_ld_pairs(f, w, 0.1, progress_report=seen.append)
+    rows = list(store)
+    assert len(rows) == 1 and rows[0][:2] == (0, 1)
+    assert "%.3f %.3f %.3f" % (rows[0][2].d, rows[0][2].d_prime, rows[0][2].r2) == "0.107 0.345 0.237"
+    assert seen[0] == 0 and seen[-1] == 1
+
+
+@pytest.mark.parametrize("name", ["synth_n200_l24.fasta", "synth_n500_l40.fasta", "synth_n2000_l30.fasta"])
+def test_gpu_vs_python_reference_goldens(W, python_ref, name):
+    g = python_ref[name]
+    ss = W.read_fasta(os.path.join(SYNTH, name))
+    f = ss.filter_sites_of_interest()
+    w = W.henikoff_weights(f)
+    for weights, key in ((w, "pairs_weighted"), (np.ones_like(w), "pairs_unweighted")):
+        store = W.all_weighted_ld_pairs(f, weights, float("-inf"))
+        got = {(a, b): (s.d, s.d_prime, s.r2) for a, b, s in store}
+        for a, b, D, Dp, R2 in g[key]:
+            d, dp, r2 = got[(a, b)]
+            assert abs(d - D) <= TOL and abs(dp - Dp) <= TOL and abs(r2 - R2) <= TOL
+
+
+def test_gpu_vcf_config3_vs_python(W, python_ref):
+    g = python_ref["t7_1000genome.vcf"]
+    ss = W.read_vcf(os.path.join(FIXTURES, "t7_1000genome.vcf"))
+    w = W.henikoff_weights(ss)
+    store = W.all_weighted_ld_pairs(ss, w, float("-inf"))
+    got = {(a, b): (s.d, s.d_prime, s.r2) for a, b, s in store}
+    assert len(g["pairs_weighted"]) == 10
+    for a, b, D, Dp, R2 in g["pairs_weighted"]:
+        d, dp, r2 = got[(a, b)]
+        assert abs(d - D) <= TOL and abs(dp - Dp) <= TOL and abs(r2 - R2) <= TOL
+
+
+CLI = os.path.join(REPO, "weightedld_amd", "bin", "weighted_ld")
+
+# expected Rust CLI output derived from lib.rs semantics
+CLI_EXPECT = {
+    ("example.fasta", False): ["0\t1\t0.107\t0.345\t0.237"],
+    ("example.fasta", True): [],
+    ("t2_henikoff_complex1.fasta", False): ["1\t2\t0.107\t0.357\t0.238"],
+    ("t3_henikoff_complex2.fasta", False): ["1\t2\t0.107\t0.357\t0.238"],
+    ("t4_weights1_ld0.fasta", False): ["0\t3\t0.088\t0.422\t0.192", "1\t3\t0.088\t0.422\t0.192"],
+    ("t5_weights1_ld0.25.fasta", False): ["0\t1\t-0.250\t0.500\t1.000"],
+    ("t5_weights1_ld0.25.fasta", True): ["0\t1\t-0.250\t0.500\t1.000"],
+    ("t6_varsites_hk_ld.fasta", False): ["0\t1\t-0.148\t0.444\t0.400"],
+    ("t6_varsites_hk_ld.fasta", True): ["0\t1\t-0.070\t0.700\t0.259"],
+}
+
+
+@pytest.mark.parametrize("case", sorted(CLI_EXPECT))
+def test_cli_tsv(tmp_path, case):
+    name, unweighted = case
+    out = tmp_path / "pairs.tsv"
+    cmd = [CLI, "--fasta-input", os.path.join(FIXTURES, name), "--pair-output", str(out)]
+    if unweighted:
+        cmd.append("--unweighted")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = out.read_text().splitlines()
+    assert lines[0] == "site_a\tsite_b\td\td'\tr2"
+    assert lines[1:] == CLI_EXPECT[case]
+    assert "pairs computed at" in r.stderr
+
+
+def test_cli_t1_panics_like_reference(tmp_path):
+    r = subprocess.run([CLI, "--fasta-input", os.path.join(FIXTURES, "t1_henikoff_paper.fasta"), "--pair-output",
+                        str(tmp_path / "p.tsv")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 101 and "panicked" in r.stderr
+
+
+def test_cli_vcf_threshold_zero(tmp_path, python_ref):
+    out = tmp_path / "pairs.tsv"
+    r = subprocess.run([CLI, "--vcf-input", os.path.join(FIXTURES, "t7_1000genome.vcf"), "--pair-output", str(out),
+                        "--r2-threshold", "0"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = out.read_text().splitlines()[1:]
+    exp = ["%d\t%d\t%.3f\t%.3f\t%.3f" % (a, b, d, dp, r2) for a, b, d, dp, r2 in
+           python_ref["t7_1000genome.vcf"]["pairs_weighted"]]
+    assert sorted(lines) == sorted(exp)
+
+
+# ------------------------------------------------------------------ full size (BASELINE config 4)
+@pytest.mark.parametrize("kern", KERNELS)
+def test_config4_full_size_properties(ctxs, kern):
+    """N=2000 x L=20000, thr 0.05: size-independent properties plus a sampled
+    oracle check (the oracle at full size takes minutes, a sample seconds)."""
+    ctx = _ctx(ctxs, kern)
+    L, N = 20000, 2000
+    buf = synth(L, N, 2024)
+    import weightedld_amd as W
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ctx.load(buf, w)
+    n = ctx.run(0.05)
+    store = ctx.rows()
+    st = ctx.stats()
+    assert st["pairs"] == L * (L - 1) // 2 == 199990000
+    assert len(store) == n
+    if n:
+        assert np.all(store.r2 > 0.05)
+        assert np.all(store.site_a < store.site_b)
+    # reference order of the emitted rows
+    nchunk = (L + 255) // 256
+    ca, cb = store.site_a.astype(np.int64) // 256, store.site_b.astype(np.int64) // 256
+    rf = nchunk - 1 - ca
+    lin = rf * (rf + 1) // 2 + (cb - ca)
+    key = lin * (L * L) + store.site_a.astype(np.int64) * L + store.site_b
+    assert np.all(np.diff(key) > 0)
+    # sampled exact check against the oracle: a 600-site window at thr -inf
+    sub = buf[9000:9600]
+    ctx.load(sub, w)
+    ctx.run(float("-inf"))
+    compare_rows(ctx.rows(), O.all_pairs(sub, w, float("-inf")), float("-inf"))

@@ -1,0 +1,142 @@
+"""ctypes binding of libweightedld.so (include/weightedld.h).
+
+The shared library is built in-tree by `make` (or __graft_entry__.build()).
+There is no Python or CPU fallback for the hot path: if the library is missing
+every call raises, and device entry points fail loudly without a gfx950 GPU.
+"""
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libweightedld.so")
+
+WLD_OK = 0
+STATUS = {
+    -1: "WLD_E_ARG",
+    -2: "WLD_E_HIP",
+    -3: "WLD_E_OOM",
+    -4: "WLD_E_NODEV",
+    -5: "WLD_E_IO",
+    -6: "WLD_E_FORMAT",
+    -7: "WLD_E_STATE",
+}
+KERNEL_AUTO, KERNEL_VALU, KERNEL_MFMA = 0, 1, 2
+
+
+class WldError(RuntimeError):
+    def __init__(self, status, where, message):
+        self.status = status
+        self.name = STATUS.get(status, str(status))
+        super().__init__("%s: %s (%s)" % (where, message, self.name))
+
+
+class Pairs(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint64),
+        ("site_a", ctypes.POINTER(ctypes.c_uint32)),
+        ("site_b", ctypes.POINTER(ctypes.c_uint32)),
+        ("d", ctypes.POINTER(ctypes.c_float)),
+        ("d_prime", ctypes.POINTER(ctypes.c_float)),
+        ("r2", ctypes.POINTER(ctypes.c_float)),
+    ]
+
+
+class RunStats(ctypes.Structure):
+    _fields_ = [
+        ("kernel", ctypes.c_int),
+        ("pairs", ctypes.c_uint64),
+        ("rows", ctypes.c_uint64),
+        ("pair_kernel_ms", ctypes.c_double),
+        ("order_ms", ctypes.c_double),
+        ("load_ms", ctypes.c_double),
+        ("pair_kernel_launches", ctypes.c_uint64),
+        ("weight_shift", ctypes.c_int),
+    ]
+
+
+PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_uint64, ctypes.c_void_p)
+
+# name -> (restype, argtypes); every symbol include/weightedld.h declares.
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_int = ctypes.c_int
+SIGNATURES = {
+    "wld_status_string": (ctypes.c_char_p, [_int]),
+    "wld_last_error": (ctypes.c_char_p, []),
+    "wld_version": (ctypes.c_char_p, []),
+    "wld_read_fasta": (_int, [ctypes.c_char_p, ctypes.POINTER(_vp)]),
+    "wld_read_vcf": (_int, [ctypes.c_char_p, ctypes.POINTER(_vp)]),
+    "wld_siteset_from_buffer": (_int, [_u8p, _sz, _sz, _u64p, ctypes.POINTER(_vp)]),
+    "wld_siteset_free": (None, [_vp]),
+    "wld_siteset_n_sites": (_sz, [_vp]),
+    "wld_siteset_n_seqs": (_sz, [_vp]),
+    "wld_siteset_buffer": (_u8p, [_vp]),
+    "wld_siteset_site_map": (_u64p, [_vp]),
+    "wld_siteset_parent_site_index": (ctypes.c_uint64, [_vp, _sz]),
+    "wld_siteset_histogram": (_int, [_vp, _sz, _u64p]),
+    "wld_histogram": (_int, [_u8p, _sz, _u64p]),
+    "wld_major_minor": (_int, [_u64p, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "wld_is_site_of_interest": (_int, [_u8p, _sz, _sz, ctypes.c_float, ctypes.c_float]),
+    "wld_siteset_filter_sites_of_interest": (_int, [_vp, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                                    ctypes.POINTER(_vp)]),
+    "wld_henikoff_weights": (_int, [_vp, _f32p]),
+    "wld_create": (_int, [_int, ctypes.POINTER(_vp)]),
+    "wld_destroy": (None, [_vp]),
+    "wld_set_kernel": (_int, [_vp, _int]),
+    "wld_pairs_free": (None, [ctypes.POINTER(Pairs)]),
+    "wld_all_weighted_ld_pairs": (_int, [_vp, _u8p, _sz, _sz, _u64p, _f32p, ctypes.c_float, PROGRESS_FN, _vp,
+                                         ctypes.POINTER(Pairs)]),
+    "wld_single_weighted_ld_pair": (_int, [_vp, _u8p, _u8p, _f32p, _sz, _f32p]),
+    "wld_load": (_int, [_vp, _u8p, _sz, _sz, _u64p, _f32p]),
+    "wld_load_device": (_int, [_vp, _vp, _sz, _sz, _u64p, _vp]),
+    "wld_chunk_rows": (ctypes.c_uint32, [_sz]),
+    "wld_shard_chunk_rows": (_int, [_sz, _int, _int, _u32p, _u32p]),
+    "wld_run": (_int, [_vp, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint32, _u64p]),
+    "wld_rows_device": (_int, [_vp, ctypes.POINTER(Pairs)]),
+    "wld_rows_copy": (_int, [_vp, _u32p, _u32p, _f32p, _f32p, _f32p]),
+    "wld_rows_copy_device": (_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "wld_dense": (_int, [_vp, _f32p, _f32p, _f32p, _u8p]),
+    "wld_last_stats": (_int, [_vp, ctypes.POINTER(RunStats)]),
+}
+
+_lib = None
+
+
+def _preload_torch():
+    # torch ships its own libamdhip64.so.7; load it first so this process has
+    # exactly one HIP runtime whichever of torch / this library comes first.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
+def lib():
+    """Loads libweightedld.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise WldError(-2, "load", "%s is missing: run `make` (or __graft_entry__.build())" % LIB_PATH)
+    _preload_torch()
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def last_error():
+    return lib().wld_last_error().decode(errors="replace")
+
+
+def check(status, where):
+    if status < 0:
+        raise WldError(status, where, last_error())
+    return status

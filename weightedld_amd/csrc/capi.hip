@@ -1,0 +1,576 @@
+// C ABI of the device hot path (include/weightedld.h).
+//
+// wld_all_weighted_ld_pairs is the drop-in for all_weighted_ld_pairs
+// (lib.rs:578-684).  It is built from the staged calls:
+//   wld_load  : H2D of SiteSet.buffer + weights, encode on device
+//   wld_run   : pair kernel over the shard's tiles -> staging + segment counts,
+//               chunk scan, reference-order gather (order.hip)
+//   wld_rows_copy : D2H of the ordered rows
+// There is no CPU compute path: without a gfx950 device every device entry
+// point fails with WLD_E_NODEV.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "kernels.hpp"
+
+using namespace wld;
+
+#define HIP_TRY(expr)                                                                               \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess)                                                                       \
+            return fail(e_ == hipErrorOutOfMemory ? WLD_E_OOM : WLD_E_HIP, "%s failed: %s (%s:%d)", \
+                        #expr, hipGetErrorString(e_), __FILE__, __LINE__);                          \
+    } while (0)
+
+#define WLD_TRY(expr)          \
+    do {                       \
+        int st_ = (expr);      \
+        if (st_ != WLD_OK)     \
+            return st_;        \
+    } while (0)
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+int ensure(DevBuf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.p && b.bytes >= bytes) return WLD_OK;
+    if (b.p) {
+        (void)hipFree(b.p);
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) {
+        b.p = nullptr;
+        (void)hipGetLastError();
+        return fail(WLD_E_OOM, "hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
+    }
+    b.bytes = bytes;
+    return WLD_OK;
+}
+
+void release(DevBuf &b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+template <class T>
+T *ptr(DevBuf &b) {
+    return reinterpret_cast<T *>(b.p);
+}
+
+size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+struct wld_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[6] = {};
+    int kernel_pref = WLD_KERNEL_AUTO;
+
+    // loaded SiteSet
+    bool loaded = false;
+    size_t L = 0, N = 0, LP = 0, NP = 0;
+    DevBuf raw, wraw, codes, w_pad, wstats, site_ok, site_map, planes;
+    bool has_map = false;
+    int kernel = WLD_KERNEL_VALU;
+    bool safe = false;
+    int shift = 0;
+
+    // run state
+    DevBuf tiles, seg_cnt, seg_off, chunk_total, chunk_base, counters;
+    DevBuf st_a, st_b, st_d, st_dp, st_r2;
+    DevBuf out_a, out_b, out_d, out_dp, out_r2;
+    uint64_t st_capacity = 0;
+    uint32_t tiles_rb = ~0u, tiles_re = ~0u;
+    uint32_t n_tiles = 0;
+    bool have_rows = false;
+    uint64_t rows = 0;
+    wld_run_stats stats{};
+
+    ~wld_ctx() {
+        (void)hipSetDevice(device);
+        DevBuf *all[] = {&raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &tiles,
+                         &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &st_a, &st_b, &st_d,
+                         &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
+        for (DevBuf *b : all) release(*b);
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+int set_dev(wld_ctx *c) {
+    if (!c) return fail(WLD_E_ARG, "null context");
+    HIP_TRY(hipSetDevice(c->device));
+    return WLD_OK;
+}
+
+float event_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1.0f;
+    }
+    return ms;
+}
+
+// fixed-point exponent for the MFMA weight planes: max|w| * 2^shift must fit
+// three balanced base-256 digits (|q| <= 127 * 65793 = 8,355,711 + 256).
+int weight_shift(float maxabs) {
+    const double lim = 127.0 * (1.0 + 256.0 + 65536.0);
+    int e = 0;
+    std::frexp((double)maxabs, &e);  // maxabs = m * 2^e, m in [0.5, 1)
+    int shift = 22 - e;              // maxabs * 2^shift < 2^22 < lim
+    while (std::ldexp((double)maxabs, shift + 1) <= lim) ++shift;
+    while (std::ldexp((double)maxabs, shift) > lim) --shift;
+    return shift;
+}
+
+int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint64_t *site_map) {
+    const size_t L = c->L, N = c->N;
+    c->LP = round_up(std::max<size_t>(L, 1), kChunk);
+    c->NP = round_up(std::max<size_t>(N, 1), kSeqPad);
+    WLD_TRY(ensure(c->codes, c->LP * c->NP));
+    WLD_TRY(ensure(c->site_ok, c->LP));
+    WLD_TRY(ensure(c->w_pad, c->NP * sizeof(float)));
+    WLD_TRY(ensure(c->wstats, 4 * sizeof(float)));
+    HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+    launch_encode(d_sites, L, N, c->LP, c->NP, ptr<uint8_t>(c->codes), ptr<uint8_t>(c->site_ok), c->stream);
+    HIP_TRY(hipGetLastError());
+    launch_weight_prep(d_w, N, c->NP, ptr<float>(c->w_pad), ptr<float>(c->wstats), c->stream);
+    HIP_TRY(hipGetLastError());
+    float ws[3] = {0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(ws, c->wstats.p, 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+
+    const bool finite = ws[2] == 0.0f;
+    const float maxabs = ws[0], minabs = ws[1];
+    // MFMA planes hold w * 2^shift in 24-bit fixed point; AUTO keeps the f32
+    // VALU kernel when that could lose precision ("Kernel choice").
+    const bool mfma_ok = mfma_supported() && finite && maxabs > 0.0f && minabs >= maxabs * 0x1p-10f;
+    int k = c->kernel_pref;
+    if (k == WLD_KERNEL_AUTO) k = mfma_ok ? WLD_KERNEL_MFMA : WLD_KERNEL_VALU;
+    if (k == WLD_KERNEL_MFMA && !(mfma_supported() && finite && maxabs > 0.0f))
+        return fail(WLD_E_ARG, "MFMA kernel requested but weights are not finite/nonzero");
+    c->kernel = k;
+    c->safe = !finite;
+    c->shift = 0;
+    if (k == WLD_KERNEL_MFMA) {
+        c->shift = weight_shift(maxabs);
+        WLD_TRY(ensure(c->planes, 3 * c->NP));
+        launch_mfma_prep(ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), c->LP, c->NP, c->shift,
+                         ptr<int8_t>(c->planes), c->stream);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+
+    c->has_map = site_map != nullptr;
+    if (site_map) {
+        std::vector<uint32_t> m(L);
+        for (size_t i = 0; i < L; ++i) {
+            if (site_map[i] > 0xFFFFFFFFull) return fail(WLD_E_ARG, "site_map[%zu] exceeds 32 bits", i);
+            m[i] = (uint32_t)site_map[i];
+        }
+        WLD_TRY(ensure(c->site_map, std::max<size_t>(L, 1) * sizeof(uint32_t)));
+        if (L) HIP_TRY(hipMemcpyAsync(c->site_map.p, m.data(), L * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->stats.load_ms = event_ms(c->ev[0], c->ev[1]);
+    c->stats.kernel = c->kernel;
+    c->stats.weight_shift = c->shift;
+    c->loaded = true;
+    c->have_rows = false;
+    c->tiles_rb = c->tiles_re = ~0u;
+    return WLD_OK;
+}
+
+uint32_t chunk_rows_of(size_t L) { return (uint32_t)((L + kChunk - 1) / kChunk); }
+
+uint64_t pairs_in_rows(size_t L, uint32_t rb, uint32_t re) {
+    // pairs (a<b) with a in [rb*256, re*256) ∩ [0, L)
+    uint64_t a0 = std::min<uint64_t>(L, (uint64_t)rb * kChunk), a1 = std::min<uint64_t>(L, (uint64_t)re * kChunk);
+    uint64_t s = 0;
+    // sum_{a=a0}^{a1-1} (L-1-a)
+    if (a1 > a0) s = (a1 - a0) * (uint64_t)(L - 1) - (a1 - 1 + a0) * (a1 - a0) / 2;
+    return s;
+}
+
+int build_tiles(wld_ctx *c, uint32_t rb, uint32_t re) {
+    if (c->tiles_rb == rb && c->tiles_re == re && c->n_tiles) return WLD_OK;
+    const uint32_t T_used = (uint32_t)((c->L + kTile - 1) / kTile);
+    std::vector<uint32_t> t;
+    for (uint32_t ta = rb * kTilesPerChunk; ta < std::min<uint32_t>(re * kTilesPerChunk, T_used); ++ta)
+        for (uint32_t tb = ta; tb < T_used; ++tb) t.push_back((ta << 16) | tb);
+    c->n_tiles = (uint32_t)t.size();
+    WLD_TRY(ensure(c->tiles, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));
+    if (!t.empty())
+        HIP_TRY(hipMemcpyAsync(c->tiles.p, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->tiles_rb = rb;
+    c->tiles_re = re;
+    return WLD_OK;
+}
+
+OrderArgs order_args(wld_ctx *c) {
+    OrderArgs o;
+    o.st_a = ptr<uint32_t>(c->st_a);
+    o.st_b = ptr<uint32_t>(c->st_b);
+    o.st_d = ptr<float>(c->st_d);
+    o.st_dp = ptr<float>(c->st_dp);
+    o.st_r2 = ptr<float>(c->st_r2);
+    o.st_capacity = c->st_capacity;
+    o.seg_cnt = ptr<uint8_t>(c->seg_cnt);
+    o.seg_off = ptr<uint32_t>(c->seg_off);
+    o.T = (uint32_t)(c->LP / kTile);
+    o.chunk_total = ptr<uint32_t>(c->chunk_total);
+    o.cursor = ptr<unsigned long long>(c->counters);
+    return o;
+}
+
+int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *dense) {
+    const uint32_t n = chunk_rows_of(c->L);
+    if (c->kernel == WLD_KERNEL_MFMA)
+        launch_pair_mfma(ptr<uint8_t>(c->codes), ptr<int8_t>(c->planes), ptr<uint8_t>(c->site_ok),
+                         ptr<uint32_t>(c->tiles), c->n_tiles, (uint32_t)c->L, (uint32_t)c->NP, n, thr, c->shift, o,
+                         dense, c->stream);
+    else
+        launch_pair_valu(ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), ptr<uint8_t>(c->site_ok),
+                         ptr<uint32_t>(c->tiles), c->n_tiles, (uint32_t)c->L, (uint32_t)c->NP, n, thr, c->safe, o,
+                         dense, c->stream);
+    HIP_TRY(hipGetLastError());
+    return WLD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *wld_version(void) { return "weightedld-amd 0.1.0 (gfx950)"; }
+
+int wld_create(int device, wld_ctx **out) {
+    if (!out) return fail(WLD_E_ARG, "wld_create: null out");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) {
+        (void)hipGetLastError();
+        return fail(WLD_E_NODEV, "no HIP device visible (%s); the weightedld hot path runs only on a gfx950 GPU",
+                    e == hipSuccess ? "0 devices" : hipGetErrorString(e));
+    }
+    if (device < 0 || device >= n) return fail(WLD_E_ARG, "device %d out of range (%d visible)", device, n);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        return fail(WLD_E_NODEV, "device %d is %s, not gfx950 (MI355X)", device, prop.gcnArchName);
+    HIP_TRY(hipSetDevice(device));
+    auto *c = new wld_ctx;
+    c->device = device;
+    hipError_t es = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (es != hipSuccess) {
+        delete c;
+        return fail(WLD_E_HIP, "hipStreamCreate: %s", hipGetErrorString(es));
+    }
+    for (auto &ev : c->ev)
+        if (hipEventCreate(&ev) != hipSuccess) {
+            delete c;
+            return fail(WLD_E_HIP, "hipEventCreate failed");
+        }
+    *out = c;
+    return WLD_OK;
+}
+
+void wld_destroy(wld_ctx *ctx) { delete ctx; }
+
+int wld_set_kernel(wld_ctx *ctx, int kernel) {
+    if (!ctx) return fail(WLD_E_ARG, "null context");
+    if (kernel < WLD_KERNEL_AUTO || kernel > WLD_KERNEL_MFMA) return fail(WLD_E_ARG, "bad kernel id %d", kernel);
+    if (kernel == WLD_KERNEL_MFMA && !mfma_supported()) return fail(WLD_E_ARG, "MFMA kernel not built");
+    ctx->kernel_pref = kernel;
+    return WLD_OK;
+}
+
+int wld_load(wld_ctx *c, const uint8_t *sites, size_t n_sites, size_t n_seqs, const uint64_t *site_map,
+             const float *weights) {
+    WLD_TRY(set_dev(c));
+    if ((!sites && n_sites * n_seqs) || (!weights && n_seqs)) return fail(WLD_E_ARG, "wld_load: null input");
+    if (n_sites >= (1u << 16) * (size_t)kTile) return fail(WLD_E_ARG, "n_sites %zu too large", n_sites);
+    c->loaded = false;
+    c->L = n_sites;
+    c->N = n_seqs;
+    WLD_TRY(ensure(c->raw, n_sites * n_seqs));
+    WLD_TRY(ensure(c->wraw, n_seqs * sizeof(float)));
+    if (n_sites * n_seqs)
+        HIP_TRY(hipMemcpyAsync(c->raw.p, sites, n_sites * n_seqs, hipMemcpyHostToDevice, c->stream));
+    if (n_seqs) HIP_TRY(hipMemcpyAsync(c->wraw.p, weights, n_seqs * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    return common_load(c, ptr<uint8_t>(c->raw), ptr<float>(c->wraw), site_map);
+}
+
+int wld_load_device(wld_ctx *c, const void *d_sites, size_t n_sites, size_t n_seqs, const uint64_t *site_map,
+                    const void *d_weights) {
+    WLD_TRY(set_dev(c));
+    if ((!d_sites && n_sites * n_seqs) || (!d_weights && n_seqs)) return fail(WLD_E_ARG, "wld_load_device: null input");
+    if (n_sites >= (1u << 16) * (size_t)kTile) return fail(WLD_E_ARG, "n_sites %zu too large", n_sites);
+    c->loaded = false;
+    c->L = n_sites;
+    c->N = n_seqs;
+    return common_load(c, (const uint8_t *)d_sites, (const float *)d_weights, site_map);
+}
+
+uint32_t wld_chunk_rows(size_t n_sites) { return chunk_rows_of(n_sites); }
+
+int wld_shard_chunk_rows(size_t n_sites, int n_shards, int shard, uint32_t *begin, uint32_t *end) {
+    if (n_shards < 1 || shard < 0 || shard >= n_shards || !begin || !end)
+        return fail(WLD_E_ARG, "bad shard %d/%d", shard, n_shards);
+    const uint32_t n = chunk_rows_of(n_sites);
+    const uint64_t total = pairs_in_rows(n_sites, 0, n);
+    // boundaries: first chunk row where the cumulative pair count reaches k/n_shards
+    auto boundary = [&](int k) -> uint32_t {
+        if (k <= 0) return 0;
+        if (k >= n_shards) return n;
+        const long double target = (long double)total * k / n_shards;
+        uint32_t r = 0;
+        while (r < n && (long double)pairs_in_rows(n_sites, 0, r + 1) <= target) ++r;
+        // pick the closer of r and r+1
+        if (r < n) {
+            long double lo = (long double)pairs_in_rows(n_sites, 0, r), hi = (long double)pairs_in_rows(n_sites, 0, r + 1);
+            if (hi - target < target - lo) ++r;
+        }
+        return r;
+    };
+    *begin = boundary(shard);
+    *end = boundary(shard + 1);
+    if (*end < *begin) *end = *begin;
+    return WLD_OK;
+}
+
+int wld_run(wld_ctx *c, float thr, uint32_t rb, uint32_t re, uint64_t *n_rows) {
+    WLD_TRY(set_dev(c));
+    if (!c->loaded) return fail(WLD_E_STATE, "wld_run before wld_load");
+    const uint32_t n = chunk_rows_of(c->L);
+    if (re == 0 || re > n) re = n;
+    if (rb > re) return fail(WLD_E_ARG, "row range [%u,%u) invalid", rb, re);
+    c->have_rows = false;
+    WLD_TRY(build_tiles(c, rb, re));
+    const uint64_t pairs = pairs_in_rows(c->L, rb, re);
+    const uint32_t T = (uint32_t)(c->LP / kTile);
+    const uint32_t n_chunks = n * (n + 1) / 2;
+    // chunks of rows [rb, re): linear range [lin(re-1, re-1), lin(rb, rb) + (n-rb))
+    const uint32_t lin_begin = re > rb ? chunk_linear(n, re - 1, re - 1) : 0;
+    const uint32_t lin_end = re > rb ? chunk_linear(n, rb, rb) + (n - rb) : 0;
+    const uint32_t lin_count = lin_end - lin_begin;
+
+    // staging: worst case every pair of the shard passes (+ slack for the tile overshoot guard)
+    const uint64_t cap = std::max<uint64_t>(pairs, 1);
+    if (cap > 0xFFFFFFFFull) return fail(WLD_E_ARG, "shard has %llu pairs; > 2^32 per device not supported", (unsigned long long)cap);
+    if (c->st_capacity < cap) {
+        WLD_TRY(ensure(c->st_a, cap * 4));
+        WLD_TRY(ensure(c->st_b, cap * 4));
+        WLD_TRY(ensure(c->st_d, cap * 4));
+        WLD_TRY(ensure(c->st_dp, cap * 4));
+        WLD_TRY(ensure(c->st_r2, cap * 4));
+        c->st_capacity = cap;
+    }
+    WLD_TRY(ensure(c->seg_cnt, c->LP * T));
+    WLD_TRY(ensure(c->seg_off, c->LP * T * sizeof(uint32_t)));
+    WLD_TRY(ensure(c->chunk_total, std::max<size_t>(n_chunks, 1) * sizeof(uint32_t)));
+    WLD_TRY(ensure(c->chunk_base, std::max<size_t>(n_chunks, 1) * sizeof(uint32_t)));
+    WLD_TRY(ensure(c->counters, 4 * sizeof(unsigned long long)));
+
+    HIP_TRY(hipMemsetAsync(c->counters.p, 0, 4 * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(c->seg_cnt.p, 0, c->LP * T, c->stream));
+    if (lin_count)
+        HIP_TRY(hipMemsetAsync(ptr<uint32_t>(c->chunk_total) + lin_begin, 0, lin_count * sizeof(uint32_t), c->stream));
+    OrderArgs o = order_args(c);
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    if (c->n_tiles) WLD_TRY(launch_pairs(c, thr, o, nullptr));
+    HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+    unsigned long long *d_total = ptr<unsigned long long>(c->counters) + 1;
+    if (lin_count) {
+        launch_chunk_scan(ptr<uint32_t>(c->chunk_total), lin_begin, lin_count, ptr<uint32_t>(c->chunk_base), d_total,
+                          c->stream);
+        HIP_TRY(hipGetLastError());
+    }
+    unsigned long long h[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(h, c->counters.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const uint64_t rows = h[1];
+    if (h[0] != h[1]) return fail(WLD_E_HIP, "internal: staging cursor %llu != chunk total %llu", h[0], h[1]);
+    WLD_TRY(ensure(c->out_a, std::max<uint64_t>(rows, 1) * 4));
+    WLD_TRY(ensure(c->out_b, std::max<uint64_t>(rows, 1) * 4));
+    WLD_TRY(ensure(c->out_d, std::max<uint64_t>(rows, 1) * 4));
+    WLD_TRY(ensure(c->out_dp, std::max<uint64_t>(rows, 1) * 4));
+    WLD_TRY(ensure(c->out_r2, std::max<uint64_t>(rows, 1) * 4));
+    HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+    if (rows && lin_count) {
+        launch_gather(o, ptr<uint32_t>(c->chunk_base), lin_begin, lin_count, n, (uint32_t)c->L,
+                      c->has_map ? ptr<uint32_t>(c->site_map) : nullptr, ptr<uint32_t>(c->out_a),
+                      ptr<uint32_t>(c->out_b), ptr<float>(c->out_d), ptr<float>(c->out_dp), ptr<float>(c->out_r2),
+                      c->stream);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(c->ev[5], c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->rows = rows;
+    c->have_rows = true;
+    c->stats.kernel = c->kernel;
+    c->stats.pairs = pairs;
+    c->stats.rows = rows;
+    c->stats.pair_kernel_ms = event_ms(c->ev[2], c->ev[3]);
+    c->stats.order_ms = event_ms(c->ev[3], c->ev[5]);
+    c->stats.pair_kernel_launches = c->n_tiles ? 1 : 0;
+    if (n_rows) *n_rows = rows;
+    return WLD_OK;
+}
+
+int wld_rows_device(wld_ctx *c, wld_pairs *v) {
+    if (!c || !v) return fail(WLD_E_ARG, "null argument");
+    if (!c->have_rows) return fail(WLD_E_STATE, "no rows: call wld_run first");
+    v->n = c->rows;
+    v->site_a = ptr<uint32_t>(c->out_a);
+    v->site_b = ptr<uint32_t>(c->out_b);
+    v->d = ptr<float>(c->out_d);
+    v->d_prime = ptr<float>(c->out_dp);
+    v->r2 = ptr<float>(c->out_r2);
+    return WLD_OK;
+}
+
+int wld_rows_copy(wld_ctx *c, uint32_t *site_a, uint32_t *site_b, float *d, float *d_prime, float *r2) {
+    WLD_TRY(set_dev(c));
+    if (!c->have_rows) return fail(WLD_E_STATE, "no rows: call wld_run first");
+    const size_t n = c->rows;
+    if (n) {
+        if (site_a) HIP_TRY(hipMemcpyAsync(site_a, c->out_a.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+        if (site_b) HIP_TRY(hipMemcpyAsync(site_b, c->out_b.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+        if (d) HIP_TRY(hipMemcpyAsync(d, c->out_d.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+        if (d_prime) HIP_TRY(hipMemcpyAsync(d_prime, c->out_dp.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+        if (r2) HIP_TRY(hipMemcpyAsync(r2, c->out_r2.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return WLD_OK;
+}
+
+int wld_rows_copy_device(wld_ctx *c, void *site_a, void *site_b, void *d, void *d_prime, void *r2) {
+    WLD_TRY(set_dev(c));
+    if (!c->have_rows) return fail(WLD_E_STATE, "no rows: call wld_run first");
+    const size_t n = c->rows;
+    if (n) {
+        if (site_a) HIP_TRY(hipMemcpyAsync(site_a, c->out_a.p, n * 4, hipMemcpyDeviceToDevice, c->stream));
+        if (site_b) HIP_TRY(hipMemcpyAsync(site_b, c->out_b.p, n * 4, hipMemcpyDeviceToDevice, c->stream));
+        if (d) HIP_TRY(hipMemcpyAsync(d, c->out_d.p, n * 4, hipMemcpyDeviceToDevice, c->stream));
+        if (d_prime) HIP_TRY(hipMemcpyAsync(d_prime, c->out_dp.p, n * 4, hipMemcpyDeviceToDevice, c->stream));
+        if (r2) HIP_TRY(hipMemcpyAsync(r2, c->out_r2.p, n * 4, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return WLD_OK;
+}
+
+int wld_dense(wld_ctx *c, float *d, float *d_prime, float *r2, uint8_t *valid) {
+    WLD_TRY(set_dev(c));
+    if (!c->loaded) return fail(WLD_E_STATE, "wld_dense before wld_load");
+    if (!d || !d_prime || !r2 || !valid) return fail(WLD_E_ARG, "wld_dense: null output");
+    const size_t L = c->L, LL = L * L;
+    if (LL == 0) return WLD_OK;
+    if (L > 8192) return fail(WLD_E_ARG, "wld_dense is for tests (n_sites <= 8192)");
+    const uint32_t n = chunk_rows_of(L);
+    WLD_TRY(build_tiles(c, 0, n));
+    DevBuf dd, ddp, dr2, dv;
+    int st = WLD_OK;
+    if ((st = ensure(dd, LL * 4)) || (st = ensure(ddp, LL * 4)) || (st = ensure(dr2, LL * 4)) || (st = ensure(dv, LL))) {
+        release(dd); release(ddp); release(dr2); release(dv);
+        return st;
+    }
+    DenseArgs da{ptr<float>(dd), ptr<float>(ddp), ptr<float>(dr2), ptr<uint8_t>(dv)};
+    (void)hipMemsetAsync(dv.p, 0, LL, c->stream);
+    OrderArgs o = order_args(c);
+    st = launch_pairs(c, 0.0f, o, &da);
+    if (st == WLD_OK) {
+        hipError_t e = hipSuccess;
+        if (e == hipSuccess) e = hipMemcpyAsync(d, dd.p, LL * 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_prime, ddp.p, LL * 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(r2, dr2.p, LL * 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(valid, dv.p, LL, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) st = fail(WLD_E_HIP, "wld_dense copy: %s", hipGetErrorString(e));
+    }
+    release(dd); release(ddp); release(dr2); release(dv);
+    return st;
+}
+
+int wld_last_stats(wld_ctx *c, wld_run_stats *out) {
+    if (!c || !out) return fail(WLD_E_ARG, "null argument");
+    *out = c->stats;
+    return WLD_OK;
+}
+
+void wld_pairs_free(wld_pairs *p) {
+    if (!p) return;
+    free(p->site_a);
+    free(p->site_b);
+    free(p->d);
+    free(p->d_prime);
+    free(p->r2);
+    memset(p, 0, sizeof(*p));
+}
+
+int wld_all_weighted_ld_pairs(wld_ctx *c, const uint8_t *sites, size_t n_sites, size_t n_seqs,
+                              const uint64_t *site_map, const float *weights, float r2_threshold,
+                              wld_progress_fn progress, void *user, wld_pairs *out) {
+    if (!out) return fail(WLD_E_ARG, "null out");
+    memset(out, 0, sizeof(*out));
+    if (progress) progress(0, user);  // lib.rs:584
+    WLD_TRY(wld_load(c, sites, n_sites, n_seqs, site_map, weights));
+    uint64_t rows = 0;
+    WLD_TRY(wld_run(c, r2_threshold, 0, 0, &rows));
+    const size_t k = std::max<uint64_t>(rows, 1);
+    out->site_a = (uint32_t *)malloc(k * 4);
+    out->site_b = (uint32_t *)malloc(k * 4);
+    out->d = (float *)malloc(k * 4);
+    out->d_prime = (float *)malloc(k * 4);
+    out->r2 = (float *)malloc(k * 4);
+    if (!out->site_a || !out->site_b || !out->d || !out->d_prime || !out->r2) {
+        wld_pairs_free(out);
+        return fail(WLD_E_OOM, "host allocation of %llu rows failed", (unsigned long long)rows);
+    }
+    int st = wld_rows_copy(c, out->site_a, out->site_b, out->d, out->d_prime, out->r2);
+    if (st != WLD_OK) {
+        wld_pairs_free(out);
+        return st;
+    }
+    out->n = rows;
+    if (progress) progress(c->stats.pairs, user);
+    return WLD_OK;
+}
+
+int wld_single_weighted_ld_pair(wld_ctx *c, const uint8_t *a, const uint8_t *b, const float *weights, size_t n_seqs,
+                                float out[3]) {
+    if (!a || !b || !weights || !out) return fail(WLD_E_ARG, "null argument");
+    std::vector<uint8_t> buf(2 * n_seqs);
+    memcpy(buf.data(), a, n_seqs);
+    memcpy(buf.data() + n_seqs, b, n_seqs);
+    WLD_TRY(wld_load(c, buf.data(), 2, n_seqs, nullptr, weights));
+    float d[4], dp[4], r2[4];
+    uint8_t v[4];
+    WLD_TRY(wld_dense(c, d, dp, r2, v));
+    if (!v[1]) return 0;
+    out[0] = d[1];
+    out[1] = dp[1];
+    out[2] = r2[1];
+    return 1;
+}
+
+}  // extern "C"

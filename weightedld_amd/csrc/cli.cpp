@@ -1,0 +1,369 @@
+// weighted_ld — the reference CLI (rust/weighted_ld/src/main.rs) rebuilt on the
+// C ABI of libweightedld.so.  Same flags (main.rs:14-68), same pipeline
+// (main.rs:121-213), same TSV files (main.rs:70-119) and the same env_logger
+// style log lines on stderr; the all-pairs step runs on the GPU.
+//
+// Additions (do not change the reference flags' meaning):
+//   --vcf-input PATH   VCF input following WeightedLD.py's handle_vcf (no site
+//                      filter, site index = POS), for BASELINE config 3
+//   --device N         HIP device ordinal (default 0)
+//   --kernel K         auto | valu | mfma (default auto)
+#include <chrono>
+#include <cinttypes>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <string>
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+#include "weightedld.h"
+
+namespace {
+
+int g_level = 3;  // 0 off, 1 error, 2 warn, 3 info, 4 debug, 5 trace
+
+void init_logger() {
+    const char *e = getenv("RUST_LOG");  // env_logger, default_filter_or("info") (main.rs:122)
+    if (!e || !*e) return;
+    std::string s(e);
+    for (auto &c : s) c = (char)tolower(c);
+    if (s.find("trace") != std::string::npos) g_level = 5;
+    else if (s.find("debug") != std::string::npos) g_level = 4;
+    else if (s.find("info") != std::string::npos) g_level = 3;
+    else if (s.find("warn") != std::string::npos) g_level = 2;
+    else if (s.find("error") != std::string::npos) g_level = 1;
+    else if (s.find("off") != std::string::npos) g_level = 0;
+}
+
+void log_at(int level, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+void log_at(int level, const char *fmt, ...) {
+    if (level > g_level) return;
+    static const char *names[] = {"", "ERROR", "WARN ", "INFO ", "DEBUG", "TRACE"};
+    char ts[32];
+    time_t t = time(nullptr);
+    struct tm g;
+    gmtime_r(&t, &g);
+    strftime(ts, sizeof ts, "%Y-%m-%dT%H:%M:%SZ", &g);
+    char msg[2048];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(msg, sizeof msg, fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "[%s %s weighted_ld] %s\n", ts, names[level], msg);
+}
+#define INFO(...) log_at(3, __VA_ARGS__)
+
+// Rust's Debug for std::time::Duration
+std::string fmt_duration(std::chrono::nanoseconds d) {
+    uint64_t ns = (uint64_t)d.count();
+    auto frac = [](uint64_t whole, uint64_t rem, int digits, const char *unit) {
+        char buf[64];
+        if (rem == 0) {
+            snprintf(buf, sizeof buf, "%" PRIu64 "%s", whole, unit);
+        } else {
+            char f[16];
+            snprintf(f, sizeof f, "%0*" PRIu64, digits, rem);
+            int n = (int)strlen(f);
+            while (n > 0 && f[n - 1] == '0') f[--n] = 0;
+            snprintf(buf, sizeof buf, "%" PRIu64 ".%s%s", whole, f, unit);
+        }
+        return std::string(buf);
+    };
+    if (ns >= 1000000000ull) return frac(ns / 1000000000ull, ns % 1000000000ull, 9, "s");
+    if (ns >= 1000000ull) return frac(ns / 1000000ull, ns % 1000000ull, 6, "ms");
+    if (ns >= 1000ull) return frac(ns / 1000ull, ns % 1000ull, 3, "\xC2\xB5s");
+    return frac(ns, 0, 0, "ns");
+}
+
+// human_format::Formatter::new() (2 decimals, SI prefixes)
+std::string human(double v, const char *units = "") {
+    static const char *pre[] = {"", "K", "M", "G", "T", "P", "E", "Z", "Y"};
+    int k = 0;
+    double x = v;
+    while (std::fabs(x) >= 1000.0 && k < 8) {
+        x /= 1000.0;
+        ++k;
+    }
+    char buf[64];
+    snprintf(buf, sizeof buf, "%.2f %s%s", x, pre[k], units);
+    return buf;
+}
+
+// Rust `{:.3}` of an f32 (main.rs:76,106).  Finite values print like C's %.3f
+// on the exact binary value; NaN and infinities use Rust's spelling.
+inline int fmt3(char *out, float v) {
+    if (std::isnan(v)) return sprintf(out, "NaN");
+    if (std::isinf(v)) return sprintf(out, v > 0 ? "inf" : "-inf");
+    return sprintf(out, "%.3f", (double)v);
+}
+
+struct Opt {
+    std::string fasta_input, vcf_input, weights_output, pair_output;
+    float min_acgt = 0.8f, min_minor = 0.02f, max_minor = 0.5f, r2_threshold = 0.1f;
+    bool unweighted = false;
+    int device = 0;
+    int kernel = WLD_KERNEL_AUTO;
+};
+
+void usage(FILE *f) {
+    fprintf(f,
+            "weighted_ld 0.1.0\n"
+            "A tool for computing sequence weighted linkage disequilibrium\n\n"
+            "USAGE:\n    weighted_ld [FLAGS] [OPTIONS] --fasta-input <fasta-input> --pair-output <pair-output>\n\n"
+            "FLAGS:\n"
+            "    -h, --help          Prints help information\n"
+            "        --unweighted    Use unit weights instead of Henikoff weights\n"
+            "    -V, --version       Prints version information\n\n"
+            "OPTIONS:\n"
+            "        --fasta-input <fasta-input>          The source file to load\n"
+            "        --max-minor <max-minor>              Maximum fraction of minor symbols for a site to be considered "
+            "[default: 0.5]\n"
+            "        --min-acgt <min-acgt>                Minimum fractions of ACTG for a site to be considered "
+            "[default: 0.8]\n"
+            "        --min-minor <min-minor>              Minimum fraction of minor symbols for a site to be considered "
+            "[default: 0.02]\n"
+            "        --pair-output <pair-output>          Filename to write the per-pair weighted LD figures to, in Tab "
+            "Separated Value format\n"
+            "        --r2-threshold <r2-threshold>        Minimum value of R2 to be included in the output [default: "
+            "0.1]\n"
+            "        --weights-output <weights-output>    Filename to write the per-sequence weights to, in Tab "
+            "Separated Value format\n"
+            "        --vcf-input <vcf-input>              (addition) VCF input, WeightedLD.py handle_vcf semantics\n"
+            "        --device <device>                    (addition) HIP device ordinal [default: 0]\n"
+            "        --kernel <kernel>                    (addition) auto | valu | mfma [default: auto]\n");
+}
+
+[[noreturn]] void arg_error(const char *msg, const char *arg) {
+    fprintf(stderr, "error: %s '%s'\n\nUSAGE:\n    weighted_ld [FLAGS] [OPTIONS] --fasta-input <fasta-input> "
+                    "--pair-output <pair-output>\n\nFor more information try --help\n", msg, arg);
+    exit(1);
+}
+
+float parse_f32(const char *s, const char *name) {
+    char *end = nullptr;
+    float v = strtof(s, &end);
+    if (!end || *end || !*s) {
+        fprintf(stderr, "error: Invalid value for '--%s <%s>': invalid float literal\n", name, name);
+        exit(1);
+    }
+    return v;
+}
+
+Opt parse(int argc, char **argv) {
+    Opt o;
+    bool have_pair = false;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i], val;
+        bool has_eq = false;
+        if (a.rfind("--", 0) == 0) {
+            size_t eq = a.find('=');
+            if (eq != std::string::npos) {
+                val = a.substr(eq + 1);
+                a = a.substr(0, eq);
+                has_eq = true;
+            }
+        }
+        auto need = [&](const char *name) -> std::string {
+            if (has_eq) return val;
+            if (i + 1 >= argc) arg_error("The argument requires a value but none was supplied:", name);
+            return argv[++i];
+        };
+        if (a == "-h" || a == "--help") {
+            usage(stdout);
+            exit(0);
+        } else if (a == "-V" || a == "--version") {
+            printf("weighted_ld 0.1.0 (%s)\n", wld_version());
+            exit(0);
+        } else if (a == "--fasta-input") {
+            o.fasta_input = need("--fasta-input");
+        } else if (a == "--vcf-input") {
+            o.vcf_input = need("--vcf-input");
+        } else if (a == "--min-acgt") {
+            o.min_acgt = parse_f32(need("--min-acgt").c_str(), "min-acgt");
+        } else if (a == "--min-minor") {
+            o.min_minor = parse_f32(need("--min-minor").c_str(), "min-minor");
+        } else if (a == "--max-minor") {
+            o.max_minor = parse_f32(need("--max-minor").c_str(), "max-minor");
+        } else if (a == "--r2-threshold") {
+            o.r2_threshold = parse_f32(need("--r2-threshold").c_str(), "r2-threshold");
+        } else if (a == "--weights-output") {
+            o.weights_output = need("--weights-output");
+        } else if (a == "--pair-output") {
+            o.pair_output = need("--pair-output");
+            have_pair = true;
+        } else if (a == "--unweighted") {
+            o.unweighted = true;
+        } else if (a == "--device") {
+            o.device = atoi(need("--device").c_str());
+        } else if (a == "--kernel") {
+            std::string k = need("--kernel");
+            o.kernel = k == "valu" ? WLD_KERNEL_VALU : k == "mfma" ? WLD_KERNEL_MFMA : WLD_KERNEL_AUTO;
+            if (k != "valu" && k != "mfma" && k != "auto") arg_error("Invalid value for '--kernel':", k.c_str());
+        } else {
+            arg_error("Found argument which wasn't expected, or isn't valid in this context:", argv[i]);
+        }
+    }
+    if (o.fasta_input.empty() && o.vcf_input.empty())
+        arg_error("The following required arguments were not provided:", "--fasta-input <fasta-input>");
+    if (!have_pair) arg_error("The following required arguments were not provided:", "--pair-output <pair-output>");
+    return o;
+}
+
+// Rust's `main() -> Result<(), io::Error>` prints "Error: ..." and exits 1;
+// a panic prints the panic message and exits 101.
+[[noreturn]] void die(int st, const char *what) {
+    if (st == WLD_E_FORMAT || st == WLD_E_ARG) {
+        fprintf(stderr, "thread 'main' panicked at '%s: %s'\n", what, wld_last_error());
+        exit(101);
+    }
+    fprintf(stderr, "Error: %s: %s (%s)\n", what, wld_status_string(st), wld_last_error());
+    exit(1);
+}
+
+std::string debug_path(const std::string &p) { return "\"" + p + "\""; }
+
+// main.rs:70-80
+int write_henikoff_weights(const std::string &path, const std::vector<float> &w) {
+    FILE *f = fopen(path.c_str(), "wb");
+    if (!f) return WLD_E_IO;
+    std::string out = "Sequence_index\thk_weight\n";
+    char buf[64];
+    for (size_t i = 0; i < w.size(); ++i) {
+        int n = snprintf(buf, sizeof buf, "%zu\t", i);
+        n += fmt3(buf + n, w[i]);
+        buf[n++] = '\n';
+        out.append(buf, n);
+    }
+    size_t ok = fwrite(out.data(), 1, out.size(), f);
+    int rc = fclose(f);
+    return (ok == out.size() && rc == 0) ? WLD_OK : WLD_E_IO;
+}
+
+// main.rs:82-119: header, then "{}\t{}\t{:.3}\t{:.3}\t{:.3}" per row in PairStore order.
+// Rows are formatted in parallel blocks and written in order.
+int write_pair_stats(const std::string &path, const wld_pairs &p) {
+    FILE *f = fopen(path.c_str(), "wb");
+    if (!f) return WLD_E_IO;
+    const char *hdr = "site_a\tsite_b\td\td'\tr2\n";
+    bool ok = fwrite(hdr, 1, strlen(hdr), f) == strlen(hdr);
+    const uint64_t n = p.n;
+    const uint64_t block = 1 << 18;
+    unsigned nt = std::max(1u, std::min(std::thread::hardware_concurrency(), 32u));
+    for (uint64_t base = 0; base < n && ok; base += block * nt) {
+        std::vector<std::string> parts(nt);
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; ++t) {
+            uint64_t lo = base + t * block, hi = std::min(n, lo + block);
+            if (lo >= hi) break;
+            th.emplace_back([&, lo, hi, t] {
+                std::string &s = parts[t];
+                s.reserve((hi - lo) * 40);
+                char buf[128];
+                for (uint64_t i = lo; i < hi; ++i) {
+                    int k = snprintf(buf, sizeof buf, "%u\t%u\t", p.site_a[i], p.site_b[i]);
+                    k += fmt3(buf + k, p.d[i]);
+                    buf[k++] = '\t';
+                    k += fmt3(buf + k, p.d_prime[i]);
+                    buf[k++] = '\t';
+                    k += fmt3(buf + k, p.r2[i]);
+                    buf[k++] = '\n';
+                    s.append(buf, k);
+                }
+            });
+        }
+        for (auto &x : th) x.join();
+        for (auto &s : parts)
+            if (!s.empty() && fwrite(s.data(), 1, s.size(), f) != s.size()) ok = false;
+    }
+    if (fclose(f) != 0) ok = false;
+    return ok ? WLD_OK : WLD_E_IO;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    init_logger();
+    Opt opt = parse(argc, argv);
+    using clk = std::chrono::steady_clock;
+
+    auto sw = clk::now();
+    wld_siteset *siteset = nullptr;
+    int st;
+    const bool vcf = !opt.vcf_input.empty();
+    if (vcf)
+        st = wld_read_vcf(opt.vcf_input.c_str(), &siteset);
+    else
+        st = wld_read_fasta(opt.fasta_input.c_str(), &siteset);
+    if (st != WLD_OK) die(st, vcf ? "read_vcf" : "read_fasta");
+    INFO("Loaded %s file in %s", vcf ? "vcf" : "fasta", fmt_duration(clk::now() - sw).c_str());
+    INFO("    %zu sequences, %zu sites", wld_siteset_n_seqs(siteset), wld_siteset_n_sites(siteset));
+
+    sw = clk::now();
+    wld_siteset *filtered = nullptr;
+    if (vcf) {
+        // handle_vcf has no variable-site filter (WeightedLD.py:382-402)
+        filtered = siteset;
+        siteset = nullptr;
+        INFO("VCF input: no site filter (WeightedLD.py handle_vcf semantics)");
+    } else {
+        st = wld_siteset_filter_sites_of_interest(siteset, opt.min_acgt, opt.min_minor, opt.max_minor, &filtered);
+        if (st != WLD_OK) die(st, "filter_by");
+        INFO("Computed + filtered sites of interest in %s", fmt_duration(clk::now() - sw).c_str());
+    }
+    const size_t L = wld_siteset_n_sites(filtered), N = wld_siteset_n_seqs(filtered);
+    INFO("    Found %zu sites of interest", L);
+
+    std::vector<float> weights(N, 1.0f);
+    if (!opt.unweighted) {
+        sw = clk::now();
+        st = wld_henikoff_weights(filtered, weights.data());
+        if (st != WLD_OK) die(st, "henikoff_weights");
+        INFO("Computed Henikoff weights in %s", fmt_duration(clk::now() - sw).c_str());
+    }
+    if (!opt.weights_output.empty()) {
+        INFO("Writing weights to %s", debug_path(opt.weights_output).c_str());
+        if (write_henikoff_weights(opt.weights_output, weights) != WLD_OK) {
+            fprintf(stderr, "Error: cannot write %s\n", opt.weights_output.c_str());
+            return 1;
+        }
+    }
+
+    INFO("Beginning pairwise weighted LD computation");
+    sw = clk::now();
+    const uint64_t total_pairs = ((uint64_t)L - 1) * ((uint64_t)L - 2) / 2;  // main.rs:168 (sic, wraps)
+    wld_ctx *ctx = nullptr;
+    st = wld_create(opt.device, &ctx);
+    if (st != WLD_OK) die(st, "wld_create");
+    if (opt.kernel != WLD_KERNEL_AUTO && (st = wld_set_kernel(ctx, opt.kernel)) != WLD_OK) die(st, "wld_set_kernel");
+    wld_pairs pairs;
+    st = wld_all_weighted_ld_pairs(ctx, wld_siteset_buffer(filtered), L, N, wld_siteset_site_map(filtered),
+                                   weights.data(), opt.r2_threshold, nullptr, nullptr, &pairs);
+    if (st != WLD_OK) die(st, "all_weighted_ld_pairs");
+    const auto dur = clk::now() - sw;
+    INFO("Finished computing pairwise weighted LD stats in %s", fmt_duration(dur).c_str());
+    const double secs = std::chrono::duration<double>(dur).count();
+    INFO("    %s pairs computed at ~%s, %s passed threshold", human((double)total_pairs).c_str(),
+         human((double)total_pairs / secs, "pairs/s").c_str(), human((double)pairs.n).c_str());
+    wld_run_stats rs;
+    if (wld_last_stats(ctx, &rs) == WLD_OK)
+        log_at(4, "device: kernel=%s pairs=%" PRIu64 " pair_kernel=%.3fms order=%.3fms",
+               rs.kernel == WLD_KERNEL_MFMA ? "mfma" : "valu", rs.pairs, rs.pair_kernel_ms, rs.order_ms);
+
+    INFO("Writing output to %s", debug_path(opt.pair_output).c_str());
+    sw = clk::now();
+    if (write_pair_stats(opt.pair_output, pairs) != WLD_OK) {
+        fprintf(stderr, "Error: cannot write %s\n", opt.pair_output.c_str());
+        return 1;
+    }
+    INFO("Finshed writing output in %s", fmt_duration(clk::now() - sw).c_str());  // (sic) main.rs:210
+    wld_pairs_free(&pairs);
+    wld_destroy(ctx);
+    wld_siteset_free(filtered);
+    wld_siteset_free(siteset);
+    return 0;
+}

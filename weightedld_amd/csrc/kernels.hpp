@@ -1,0 +1,71 @@
+// Device-side layout and launchers shared by capi.hip and the kernel files.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace wld {
+
+// ---- layout constants (see DESIGN.md "Data layout in HBM") ----
+constexpr int kChunk = 256;      // reference chunk side, lib.rs:615
+constexpr int kTile = 64;        // pair-kernel tile side (sites); 4 tiles per chunk side
+constexpr int kSeqPad = 64;      // sequences padded to a multiple of this
+constexpr int kTilesPerChunk = kChunk / kTile;
+
+// Code byte per (site, sequence): bit0 = sequence is major or minor at the site
+// ("in" the pair mask, lib.rs:435), bit1 = sequence is major (lib.rs:430,432).
+constexpr uint8_t kCodeIn = 1;
+constexpr uint8_t kCodeMaj = 2;
+
+struct OrderArgs {
+    // staging written by the pair kernels (filtered indices, unordered tiles)
+    uint32_t *st_a, *st_b;
+    float *st_d, *st_dp, *st_r2;
+    uint64_t st_capacity;
+    // per (site a, 64-wide b tile) segment: count (<= 64) and staging offset
+    uint8_t *seg_cnt;   // [LP][T]
+    uint32_t *seg_off;  // [LP][T]
+    uint32_t T;         // number of 64-wide tiles (LP / 64)
+    uint32_t *chunk_total;  // [n_chunks_total] rows per reference chunk (linear triu index)
+    unsigned long long *cursor;  // staging allocation cursor
+};
+
+struct DenseArgs {
+    float *d, *dp, *r2;
+    uint8_t *valid;
+};
+
+// encode.hip
+void launch_encode(const uint8_t *d_sites, size_t L, size_t N, size_t LP, size_t NP, uint8_t *codes,
+                   uint8_t *site_ok, hipStream_t s);
+void launch_weight_prep(const float *d_w, size_t N, size_t NP, float *w_pad, float *wstats, hipStream_t s);
+
+// pair_valu.hip
+void launch_pair_valu(const uint8_t *codes, const float *w, const uint8_t *site_ok, const uint32_t *tiles,
+                      uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, bool safe,
+                      const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
+
+// pair_mfma.hip
+bool mfma_supported();
+void launch_mfma_prep(const uint8_t *codes, const float *w_pad, size_t LP, size_t NP, int shift, int8_t *planes,
+                      hipStream_t s);
+void launch_pair_mfma(const uint8_t *codes, const int8_t *wplanes, const uint8_t *site_ok, const uint32_t *tiles,
+                      uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
+                      const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
+
+// order.hip
+void launch_chunk_scan(const uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
+                       unsigned long long *total, hipStream_t s);
+void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,
+                   uint32_t n_chunk_rows, uint32_t L, const uint32_t *site_map, uint32_t *out_a, uint32_t *out_b,
+                   float *out_d, float *out_dp, float *out_r2, hipStream_t s);
+
+// Linear index of chunk (row, col) in the reference's triu_index order
+// (lib.rs:623-632): rows descend, so row r starts at (n-1-r)(n-r)/2.
+__host__ __device__ inline uint32_t chunk_linear(uint32_t n, uint32_t row, uint32_t col) {
+    uint32_t rf = n - 1 - row;
+    return rf * (rf + 1) / 2 + (col - row);
+}
+
+}  // namespace wld

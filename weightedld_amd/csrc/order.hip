@@ -1,0 +1,129 @@
+// Reference-order assembly of the passing rows.
+//
+// The pair kernels write each 64x64 tile's passing rows to a staging slice
+// taken with one atomic per tile, and record per (site a, 64-wide b tile)
+// segment its row count and staging offset, plus per reference chunk
+// (256x256, lib.rs:615) its total.  These two kernels turn that into the
+// reference's PairStore order (lib.rs:623-683): chunks in triu_index order
+// (rows descending, columns ascending), inside a chunk a ascending, then b.
+//   chunk_scan: exclusive scan of the shard's chunk totals in linear order
+//   gather:     one workgroup per chunk; scans its 256 rows x 4 segments and
+//               copies the rows, mapping filtered site indices to parent
+//               indices through site_map (lib.rs:662-663).
+#include "pair_common.hpp"
+
+namespace wld {
+
+__global__ __launch_bounds__(1024) void chunk_scan_kernel(const uint32_t *__restrict__ chunk_total, uint32_t lin_begin,
+                                                           uint32_t count, uint32_t *__restrict__ chunk_base,
+                                                           unsigned long long *__restrict__ total) {
+    __shared__ unsigned long long sw[16];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t per = (count + 1023) / 1024;
+    const uint32_t lo = min(count, tid * per), hi = min(count, lo + per);
+    unsigned long long s = 0;
+    for (uint32_t i = lo; i < hi; ++i) s += chunk_total[lin_begin + i];
+    // block exclusive scan of s (64-bit)
+    const int lane = tid & 63, wv = tid >> 6;
+    unsigned long long v = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        unsigned long long t = __shfl_up(v, off, 64);
+        if (lane >= off) v += t;
+    }
+    if (lane == 63) sw[wv] = v;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long run = 0;
+        for (int k = 0; k < 16; ++k) {
+            unsigned long long t = sw[k];
+            sw[k] = run;
+            run += t;
+        }
+        *total = run;
+    }
+    __syncthreads();
+    unsigned long long base = sw[wv] + v - s;
+    for (uint32_t i = lo; i < hi; ++i) {
+        chunk_base[i] = (uint32_t)base;
+        base += chunk_total[lin_begin + i];
+    }
+}
+
+// inverse of chunk_linear: exact integer version of triu_index (lib.rs:623-632)
+__device__ inline void chunk_of_linear(uint32_t n, uint32_t i, uint32_t &row, uint32_t &col) {
+    uint32_t rf = (uint32_t)((sqrt(8.0 * (double)i + 1.0) - 1.0) * 0.5);
+    while ((uint64_t)(rf + 1) * (rf + 2) / 2 <= i) ++rf;
+    while ((uint64_t)rf * (rf + 1) / 2 > i) --rf;
+    row = n - rf - 1;
+    col = row + i - rf * (rf + 1) / 2;
+}
+
+__global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t *__restrict__ chunk_base,
+                                                      uint32_t lin_begin, uint32_t n_chunk_rows, uint32_t L,
+                                                      const uint32_t *__restrict__ site_map,
+                                                      uint32_t *__restrict__ out_a, uint32_t *__restrict__ out_b,
+                                                      float *__restrict__ out_d, float *__restrict__ out_dp,
+                                                      float *__restrict__ out_r2) {
+    __shared__ uint8_t sCnt[kChunk][kTilesPerChunk];
+    __shared__ uint32_t sOff[kChunk][kTilesPerChunk];
+    __shared__ uint32_t sPre[kChunk][kTilesPerChunk];
+    __shared__ uint32_t sWave[4];
+    const uint32_t lin = lin_begin + blockIdx.x;
+    uint32_t row, col;
+    chunk_of_linear(n_chunk_rows, lin, row, col);
+    const uint32_t base = chunk_base[blockIdx.x];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t a = row * kChunk + tid;
+    uint32_t rowtot = 0;
+#pragma unroll
+    for (int s = 0; s < kTilesPerChunk; ++s) {
+        const uint32_t tb = col * kTilesPerChunk + s;
+        uint32_t c = 0, off = 0;
+        if (a < L && tb < o.T) {
+            c = o.seg_cnt[(size_t)a * o.T + tb];
+            off = o.seg_off[(size_t)a * o.T + tb];
+        }
+        sCnt[tid][s] = (uint8_t)c;
+        sOff[tid][s] = off;
+        sPre[tid][s] = rowtot;
+        rowtot += c;
+    }
+    const uint32_t incl = wave_inclusive_scan(rowtot);
+    if ((tid & 63) == 63) sWave[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (uint32_t k = 0; k < (tid >> 6); ++k) wbase += sWave[k];
+    const uint32_t rowbase = base + wbase + incl - rowtot;
+#pragma unroll
+    for (int s = 0; s < kTilesPerChunk; ++s) sPre[tid][s] += rowbase;
+    __syncthreads();
+    const uint32_t s = tid >> 6, e = tid & 63;
+    for (uint32_t r = 0; r < kChunk; ++r) {
+        if (e < sCnt[r][s]) {
+            const uint64_t src = (uint64_t)sOff[r][s] + e;
+            const uint64_t dst = (uint64_t)sPre[r][s] + e;
+            const uint32_t fa = o.st_a[src], fb = o.st_b[src];
+            out_a[dst] = site_map ? site_map[fa] : fa;
+            out_b[dst] = site_map ? site_map[fb] : fb;
+            out_d[dst] = o.st_d[src];
+            out_dp[dst] = o.st_dp[src];
+            out_r2[dst] = o.st_r2[src];
+        }
+    }
+}
+
+void launch_chunk_scan(const uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
+                       unsigned long long *total, hipStream_t s) {
+    hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(1024), 0, s, chunk_total, lin_begin, count, chunk_base, total);
+}
+
+void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,
+                   uint32_t n_chunk_rows, uint32_t L, const uint32_t *site_map, uint32_t *out_a, uint32_t *out_b,
+                   float *out_d, float *out_dp, float *out_r2, hipStream_t s) {
+    if (!count) return;
+    hipLaunchKernelGGL(gather_kernel, dim3(count), dim3(256), 0, s, o, chunk_base, lin_begin, n_chunk_rows, L,
+                       site_map, out_a, out_b, out_d, out_dp, out_r2);
+}
+
+}  // namespace wld
