@@ -450,6 +450,60 @@ void wldo_rows_free(wldo_rows *r) {
     memset(r, 0, sizeof(*r));
 }
 
+/* f64 "truth" for diagnostics: the same masked sums accumulated in double and
+ * the lib.rs:482-520 epilogue evaluated in double (what the f32 results
+ * approximate).  Used by the tests to tell a GPU result that is closer to the
+ * exact value than the f32 reference from a wrong one. */
+int wldo_single_pair_f64(const uint8_t *a, int am, int an, const uint8_t *b, int bm, int bn, const float *w,
+                         size_t n, double out[3]) {
+    if (am < 0 || an < 0 || bm < 0 || bn < 0) return 0;
+    double T = 0, PA = 0, PB = 0, l3 = 0;
+    for (size_t k = 0; k < n; ++k) {
+        int ain = a[k] == am || a[k] == an, bin = b[k] == bm || b[k] == bn;
+        if (!(ain && bin)) continue;
+        T += w[k];
+        if (a[k] == am) PA += w[k];
+        if (b[k] == bm) PB += w[k];
+        if (a[k] == am && b[k] == bm) l3 += w[k];
+    }
+    double o3 = l3, o2 = PA - o3, o1 = PB - o3, Pa = T - PA, Pb = T - PB, o0 = Pa - o1;
+    PA /= T; PB /= T; Pa /= T; Pb /= T; o0 /= T; o1 /= T; o2 /= T; o3 /= T;
+    double d = ((PA * PB - o3) + (Pa * Pb - o0) + (o2 - PA * Pb) + (o1 - Pa * PB)) / 4.0;
+    double den;
+    if (d < 0) {
+        den = fmax(-o0, -o3);
+        if (den == 0) den = fmin(-o0, -o3);
+    } else {
+        den = fmin(o1, o2);
+        if (den == 0) den = fmax(o1, o2);
+    }
+    out[0] = d;
+    out[1] = d / den;
+    out[2] = d * d / (PA * Pa * PB * Pb);
+    return 1;
+}
+
+void wldo_all_pairs_dense_f64(const uint8_t *buf, size_t n_sites, size_t n_seqs, const float *w, double *d,
+                              double *dp, double *r2, uint8_t *valid) {
+    int *mm = (int *)malloc(2 * (n_sites ? n_sites : 1) * sizeof(int));
+    for (size_t s = 0; s < n_sites; ++s) {
+        uint64_t h[6];
+        wldo_histogram(buf + s * n_seqs, n_seqs, h);
+        wldo_major_minor(h, &mm[2 * s], &mm[2 * s + 1]);
+    }
+    for (size_t a = 0; a < n_sites; ++a)
+        for (size_t b = a + 1; b < n_sites; ++b) {
+            double v[3] = {0, 0, 0};
+            size_t k = a * n_sites + b;
+            valid[k] = (uint8_t)wldo_single_pair_f64(buf + a * n_seqs, mm[2 * a], mm[2 * a + 1], buf + b * n_seqs,
+                                                     mm[2 * b], mm[2 * b + 1], w, n_seqs, v);
+            d[k] = v[0];
+            dp[k] = v[1];
+            r2[k] = v[2];
+        }
+    free(mm);
+}
+
 /* Dense variant for tests: stats for every a<b written to row-major
  * n_sites x n_sites matrices; valid[a*L+b] = 1 for Some, 0 for None. */
 void wldo_all_pairs_dense(const uint8_t *buf, size_t n_sites, size_t n_seqs, const float *w,

@@ -58,6 +58,8 @@ def lib():
     L.wldo_rows_free.argtypes = [ctypes.POINTER(_Rows)]
     L.wldo_all_pairs_dense.argtypes = [u8p, sz, sz, f32p, f32p, f32p, f32p, u8p]
     L.wldo_triu_index.argtypes = [sz, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
+    f64p = ctypes.POINTER(ctypes.c_double)
+    L.wldo_all_pairs_dense_f64.argtypes = [u8p, sz, sz, f32p, f64p, f64p, f64p, u8p]
     _lib = L
     return L
 
@@ -169,6 +171,23 @@ def all_pairs_dense(buf, weights):
     L.wldo_all_pairs_dense(_p(buf, ctypes.c_uint8), n_sites, n_seqs, _p(w, ctypes.c_float),
                            _p(d, ctypes.c_float), _p(dp, ctypes.c_float), _p(r2, ctypes.c_float),
                            _p(valid, ctypes.c_uint8))
+    return d, dp, r2, valid
+
+
+def all_pairs_dense_f64(buf, weights):
+    """Same sums in double + the epilogue in double: the exact value the f32
+    results approximate (diagnostics / accuracy criterion)."""
+    L = lib()
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    n_sites, n_seqs = buf.shape
+    w = np.ascontiguousarray(weights, dtype=np.float32)
+    d = np.zeros((n_sites, n_sites), dtype=np.float64)
+    dp = np.zeros_like(d)
+    r2 = np.zeros_like(d)
+    valid = np.zeros((n_sites, n_sites), dtype=np.uint8)
+    L.wldo_all_pairs_dense_f64(_p(buf, ctypes.c_uint8), n_sites, n_seqs, _p(w, ctypes.c_float),
+                               _p(d, ctypes.c_double), _p(dp, ctypes.c_double), _p(r2, ctypes.c_double),
+                               _p(valid, ctypes.c_uint8))
     return d, dp, r2, valid
 
 

@@ -54,30 +54,49 @@ def synth(L, N, seed, p_missing=0.1, p_major=0.6, unknown=0.0):
     return codes.astype(np.uint8)
 
 
-def close(x, y, tol=TOL):
-    x = np.asarray(x, dtype=np.float64)
-    y = np.asarray(y, dtype=np.float64)
-    both_nan = np.isnan(x) & np.isnan(y)
-    same_inf = np.isinf(x) & np.isinf(y) & (np.sign(x) == np.sign(y))
-    ok = both_nan | same_inf | (np.abs(x - y) <= tol)
+def agree(g, r, t=None, tol=TOL):
+    """Per-value parity criterion.  g: GPU f32, r: oracle f32 (lib.rs
+    semantics), t: f64 value of the same sums/epilogue (or None).  A value
+    passes if it is within tol of the reference (relative for |r| > 1, where
+    f32 itself has no 1e-5 absolute resolution), or if it is at least as close
+    to the exact value as the f32 reference is (the reference's 8-lane f32
+    sums carry their own rounding error, up to ~N/8 * 2^-24 relative, which
+    D' = D/den amplifies when den is small)."""
+    g = np.asarray(g, dtype=np.float64)
+    r = np.asarray(r, dtype=np.float64)
+    with np.errstate(invalid="ignore"):
+        ok = (np.isnan(g) & np.isnan(r)) | (np.isinf(g) & np.isinf(r) & (np.sign(g) == np.sign(r)))
+        ok |= np.abs(g - r) <= tol * np.maximum(1.0, np.abs(r))
+        if t is not None:
+            t = np.asarray(t, dtype=np.float64)
+            ok |= np.isfinite(t) & (np.abs(g - t) <= np.abs(r - t) + 1e-6 * np.maximum(1.0, np.abs(t)))
     return ok
 
 
-def compare_dense(gpu, ref, tol=TOL):
+def close(x, y, tol=TOL):
+    return agree(x, y, None, tol)
+
+
+def compare_dense(gpu, ref, truth=None, tol=TOL):
     d, dp, r2, valid = gpu
     rd, rdp, rr2, rvalid = ref
     L = d.shape[0]
     iu = np.triu_indices(L, 1)
     assert np.array_equal(valid[iu], rvalid[iu])
     m = rvalid[iu] == 1
-    for g, r in ((d, rd), (dp, rdp), (r2, rr2)):
-        ok = close(g[iu][m], r[iu][m], tol)
-        # D' = D / den is ill-conditioned when den ~ 0: compare relative there
-        assert ok.mean() == 1.0 or np.all(ok | (np.abs(g[iu][m] - r[iu][m]) <= tol * np.maximum(1, np.abs(r[iu][m])))), \
-            (np.argwhere(~ok)[:5], g[iu][m][~ok][:5], r[iu][m][~ok][:5])
+    for k, (g, r) in enumerate(((d, rd), (dp, rdp), (r2, rr2))):
+        t = truth[k][iu][m] if truth is not None else None
+        ok = agree(g[iu][m], r[iu][m], t, tol)
+        assert ok.all(), ("dsr"[k], np.count_nonzero(~ok), g[iu][m][~ok][:5], r[iu][m][~ok][:5],
+                          None if t is None else t[~ok][:5])
 
 
-def compare_rows(store, ref, thr, tol=TOL):
+def dense_check(ctx, buf, w):
+    L = buf.shape[0]
+    compare_dense(ctx.dense(L), O.all_pairs_dense(buf, w), O.all_pairs_dense_f64(buf, w)[:3])
+
+
+def compare_rows(store, ref, thr, tol=TOL, buf=None, w=None, site_map=None):
     ka = list(zip(store.site_a.tolist(), store.site_b.tolist()))
     kb = list(zip(ref["site_a"].tolist(), ref["site_b"].tolist()))
     ga = {k: i for i, k in enumerate(ka)}
@@ -95,11 +114,17 @@ def compare_rows(store, ref, thr, tol=TOL):
     ia = np.array([ga[k] for k in common], dtype=np.int64)
     ib = np.array([gb[k] for k in common], dtype=np.int64)
     if len(common):
-        assert close(store.d[ia], ref["d"][ib], tol).all()
-        assert close(store.r2[ia], ref["r2"][ib], tol).all()
-        okp = close(store.d_prime[ia], ref["d_prime"][ib], tol)
-        rel = np.abs(store.d_prime[ia] - ref["d_prime"][ib]) <= tol * np.maximum(1.0, np.abs(ref["d_prime"][ib]))
-        assert (okp | rel).all()
+        truth = [None, None, None]
+        if buf is not None:
+            td, tdp, tr2, _ = O.all_pairs_dense_f64(buf, w)
+            inv = {int(p): i for i, p in enumerate(site_map)} if site_map is not None else None
+            fa = np.array([inv[a] if inv else a for a, _ in common])
+            fb = np.array([inv[b] if inv else b for _, b in common])
+            truth = [td[fa, fb], tdp[fa, fb], tr2[fa, fb]]
+        for k, f in enumerate(("d", "d_prime", "r2")):
+            ok = agree(getattr(store, f)[ia], ref[f][ib], truth[k], tol)
+            assert ok.all(), (f, np.count_nonzero(~ok), getattr(store, f)[ia][~ok][:5], ref[f][ib][~ok][:5],
+                              None if truth[k] is None else truth[k][~ok][:5])
     return len(common), len(only_gpu), len(only_ref)
 
 
@@ -123,7 +148,7 @@ def test_dense_vs_oracle_synthetic(ctxs, kern, L, N, seed):
     w = np.random.default_rng(seed + 100).random(N).astype(np.float32)
     for weights in (w, np.ones(N, dtype=np.float32)):
         ctx.load(buf, weights)
-        compare_dense(ctx.dense(L), O.all_pairs_dense(buf, weights))
+        dense_check(ctx, buf, weights)
 
 
 @pytest.mark.parametrize("kern", KERNELS)
@@ -140,7 +165,7 @@ def test_dense_vs_oracle_awkward_sites(ctxs, kern):
     w = rng.random(N).astype(np.float32)
     w[::5] = 0.0
     ctx.load(buf, w)
-    compare_dense(ctx.dense(L), O.all_pairs_dense(buf, w))
+    dense_check(ctx, buf, w)
 
 
 def test_dense_nonfinite_weights_valu(ctxs):
@@ -151,7 +176,7 @@ def test_dense_nonfinite_weights_valu(ctxs):
     w[5] = np.inf
     w[9] = np.nan
     ctx.load(buf, w)
-    compare_dense(ctx.dense(70), O.all_pairs_dense(buf, w))
+    dense_check(ctx, buf, w)
 
 
 # ------------------------------------------------------------------ ordered rows
@@ -168,7 +193,7 @@ def test_rows_vs_oracle(ctxs, kern, L, N, thr):
     store = ctx.rows()
     assert len(store) == n
     ref = O.all_pairs(buf, w, thr, site_map=site_map)
-    compare_rows(store, ref, thr)
+    compare_rows(store, ref, thr, buf=buf, w=w, site_map=site_map)
     st = ctx.stats()
     assert st["pairs"] == L * (L - 1) // 2
 
@@ -311,4 +336,4 @@ def test_config4_full_size_properties(ctxs, kern):
     sub = buf[9000:9600]
     ctx.load(sub, w)
     ctx.run(float("-inf"))
-    compare_rows(ctx.rows(), O.all_pairs(sub, w, float("-inf")), float("-inf"))
+    compare_rows(ctx.rows(), O.all_pairs(sub, w, float("-inf")), float("-inf"), buf=sub, w=w)

@@ -10,8 +10,10 @@
 //     SB  += w  where additionally b == maj
 //     SAB += w  where a == maj and b == maj
 // as fmaf(u, f, acc) with u = w or 0 (a side) and f = 1.0 or 0.0 (b side):
-// w*1 and w*0 are exact, so each sum is the plain f32 running sum over
-// sequences in order.  (The SAFE variant uses selects, for non-finite weights
+// w*1 and w*0 are exact, so each sum is an f32 sum over sequences in order
+// (64-sequence stage sums added into a running total; the same terms in the
+// same order for all four sums, so SA == T still implies SAB == SB exactly and
+// degenerate pairs stay NaN as in the reference).  (The SAFE variant uses selects, for non-finite weights
 // where 0*inf would differ from the reference's select.)  Codes of both 64-site
 // panels and the weights are staged through LDS 64 sequences at a time.
 #include "pair_common.hpp"
@@ -23,7 +25,7 @@ constexpr int kStride = 68;  // LDS row stride in bytes (17 dwords: conflict-fre
 }
 
 template <bool DENSE, bool SAFE>
-__global__ __launch_bounds__(256) void pair_valu_kernel(const uint8_t *__restrict__ codes,
+__global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__restrict__ codes,
                                                          const float *__restrict__ w,
                                                          const uint8_t *__restrict__ site_ok,
                                                          const uint32_t *__restrict__ tiles, uint32_t L, uint32_t NP,
@@ -38,13 +40,18 @@ __global__ __launch_bounds__(256) void pair_valu_kernel(const uint8_t *__restric
     const uint32_t tid = threadIdx.x;
     const uint32_t tx = tid & 15, ty = tid >> 4;
 
-    float acc[4][4][4];
+    // Two-level summation: acc holds the current 64-sequence stage, tot the
+    // running total (tot += acc after every stage).  A plain running sum over
+    // thousands of sequences loses ~N*2^-24 relative (e.g. 5008 Henikoff
+    // weights of ~0.002 into a total of ~10); the reference's 8 lane sums
+    // (lib.rs:418-445) lose N/8*2^-24; 64-term stages lose far less than both.
+    float acc[4][4][4], tot[4][4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) acc[i][j][q] = 0.0f;
+            for (int q = 0; q < 4; ++q) tot[i][j][q] = 0.0f;
 
     const uint32_t lr = tid >> 2, part = tid & 3;  // loader: site row, 16-byte part
     const uint8_t *gA = codes + (size_t)(a0 + lr) * NP + part * 16;
@@ -61,6 +68,12 @@ __global__ __launch_bounds__(256) void pair_valu_kernel(const uint8_t *__restric
         pb[0] = vb.x; pb[1] = vb.y; pb[2] = vb.z; pb[3] = vb.w;
         if (tid < 64) sW[tid] = wv;
         __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[i][j][q] = 0.0f;
 
 #pragma unroll 2
         for (int kk = 0; kk < 64; kk += 4) {
@@ -114,6 +127,12 @@ __global__ __launch_bounds__(256) void pair_valu_kernel(const uint8_t *__restric
                 }
             }
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) tot[i][j][q] += acc[i][j][q];
     }
 
     // ---- epilogue ------------------------------------------------------
@@ -127,7 +146,7 @@ __global__ __launch_bounds__(256) void pair_valu_kernel(const uint8_t *__restric
         for (int j = 0; j < 4; ++j) {
             const uint32_t b = b0 + tx + 16 * j;
             float d, dp, r2;
-            ld_epilogue(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3], d, dp, r2);
+            ld_epilogue(tot[i][j][0], tot[i][j][1], tot[i][j][2], tot[i][j][3], d, dp, r2);
             res[i][j][0] = d;
             res[i][j][1] = dp;
             res[i][j][2] = r2;
