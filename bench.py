@@ -147,28 +147,17 @@ def main():
     kernel = {"auto": W.KERNEL_AUTO, "valu": W.KERNEL_VALU, "mfma": W.KERNEL_MFMA}[args.kernel]
     ctx = W.Context(local_rank, kernel)
     ctx.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
-    rb, re_ = ctx.shard_chunk_rows(L, world, rank)
+    rb, re_ = ctx.shard_chunk_rows(L, world, rank)  # row-block shard (weightedld_amd/dist.py)
+
+    from weightedld_amd import dist as wdist
 
     def gather(n):
         if world == 1:
             return n
-        cnt = torch.tensor([n], dtype=torch.int64, device=device)
-        cnts = [torch.zeros_like(cnt) for _ in range(world)]
-        dist.all_gather(cnts, cnt)
-        counts = [int(c.item()) for c in cnts]
-        m = max(counts)
-        if m == 0:
-            return 0
-        packed = torch.zeros((5, m), dtype=torch.int32, device=device)
-        if n:
-            ctx.rows_copy_device(*(packed[i].data_ptr() for i in range(5)))
-        gl = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
-        dist.gather(packed, gl, dst=0)
-        if rank == 0:
-            # shards concatenate in descending rank order (chunk rows descend)
-            rows = torch.cat([gl[g][:, :counts[g]] for g in reversed(range(world))], dim=1)
-            return int(rows.shape[1])
-        return sum(counts)
+        # RCCL gather of this rank's reference-ordered rows to rank 0 (shards
+        # concatenate in descending rank order: chunk rows descend)
+        rows = wdist.gather_rows(wdist.pack_rows_device(ctx, n, device), rank, world)
+        return int(rows.shape[1]) if rows is not None else 0
 
     def step():
         n = ctx.run(thr, rb, re_)

@@ -199,6 +199,21 @@ def test_rows_vs_oracle(ctxs, kern, L, N, thr):
 
 
 @pytest.mark.parametrize("kern", KERNELS)
+def test_staging_overflow_regrows(W, ctxs, kern, monkeypatch):
+    # staging starts tiny, the run detects the overflow from the cursor and re-runs
+    _ctx(ctxs, kern)
+    ctx = W.Context(0, W.KERNEL_MFMA if kern == "mfma" else W.KERNEL_VALU)  # fresh: no grown staging
+    monkeypatch.setenv("WLD_INITIAL_STAGING_ROWS", "100")
+    L, N = 700, 150
+    buf = synth(L, N, 5)
+    w = np.random.default_rng(2).random(N).astype(np.float32)
+    ctx.load(buf, w)
+    n = ctx.run(0.0)
+    assert n > 1000
+    compare_rows(ctx.rows(), O.all_pairs(buf, w, 0.0), 0.0, buf=buf, w=w)
+
+
+@pytest.mark.parametrize("kern", KERNELS)
 @pytest.mark.parametrize("G", [2, 3, 4])
 def test_sharded_runs_concatenate_to_reference_order(ctxs, kern, G):
     ctx = _ctx(ctxs, kern)

@@ -10,6 +10,7 @@
 // point fails with WLD_E_NODEV.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -374,40 +375,56 @@ int wld_run(wld_ctx *c, float thr, uint32_t rb, uint32_t re, uint64_t *n_rows) {
     const uint32_t lin_end = re > rb ? chunk_linear(n, rb, rb) + (n - rb) : 0;
     const uint32_t lin_count = lin_end - lin_begin;
 
-    // staging: worst case every pair of the shard passes (+ slack for the tile overshoot guard)
-    const uint64_t cap = std::max<uint64_t>(pairs, 1);
-    if (cap > 0xFFFFFFFFull) return fail(WLD_E_ARG, "shard has %llu pairs; > 2^32 per device not supported", (unsigned long long)cap);
-    if (c->st_capacity < cap) {
+    // Staging starts at min(pairs, 32M rows) and grows to the exact need: the
+    // pair kernels count every passing row but store only below capacity, so
+    // an overflow is detected from the cursor and the pass is re-run once.
+    if (pairs > 0xFFFFFFFFull)
+        return fail(WLD_E_ARG, "shard has %llu pairs; > 2^32 per device not supported (shard over more devices)",
+                    (unsigned long long)pairs);
+    auto grow_staging = [&](uint64_t cap) -> int {
+        cap = std::max<uint64_t>(cap, 1);
+        if (c->st_capacity >= cap) return WLD_OK;
         WLD_TRY(ensure(c->st_a, cap * 4));
         WLD_TRY(ensure(c->st_b, cap * 4));
         WLD_TRY(ensure(c->st_d, cap * 4));
         WLD_TRY(ensure(c->st_dp, cap * 4));
         WLD_TRY(ensure(c->st_r2, cap * 4));
         c->st_capacity = cap;
-    }
+        return WLD_OK;
+    };
+    uint64_t init_rows = 1ull << 25;
+    if (const char *e = getenv("WLD_INITIAL_STAGING_ROWS")) init_rows = strtoull(e, nullptr, 10);  // tests
+    WLD_TRY(grow_staging(std::min<uint64_t>(pairs, init_rows)));
     WLD_TRY(ensure(c->seg_cnt, c->LP * T));
     WLD_TRY(ensure(c->seg_off, c->LP * T * sizeof(uint32_t)));
     WLD_TRY(ensure(c->chunk_total, std::max<size_t>(n_chunks, 1) * sizeof(uint32_t)));
     WLD_TRY(ensure(c->chunk_base, std::max<size_t>(n_chunks, 1) * sizeof(uint32_t)));
     WLD_TRY(ensure(c->counters, 4 * sizeof(unsigned long long)));
 
-    HIP_TRY(hipMemsetAsync(c->counters.p, 0, 4 * sizeof(unsigned long long), c->stream));
-    HIP_TRY(hipMemsetAsync(c->seg_cnt.p, 0, c->LP * T, c->stream));
-    if (lin_count)
-        HIP_TRY(hipMemsetAsync(ptr<uint32_t>(c->chunk_total) + lin_begin, 0, lin_count * sizeof(uint32_t), c->stream));
-    OrderArgs o = order_args(c);
-    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-    if (c->n_tiles) WLD_TRY(launch_pairs(c, thr, o, nullptr));
-    HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-    unsigned long long *d_total = ptr<unsigned long long>(c->counters) + 1;
-    if (lin_count) {
-        launch_chunk_scan(ptr<uint32_t>(c->chunk_total), lin_begin, lin_count, ptr<uint32_t>(c->chunk_base), d_total,
-                          c->stream);
-        HIP_TRY(hipGetLastError());
-    }
     unsigned long long h[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(h, c->counters.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    OrderArgs o;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        HIP_TRY(hipMemsetAsync(c->counters.p, 0, 4 * sizeof(unsigned long long), c->stream));
+        HIP_TRY(hipMemsetAsync(c->seg_cnt.p, 0, c->LP * T, c->stream));
+        if (lin_count)
+            HIP_TRY(hipMemsetAsync(ptr<uint32_t>(c->chunk_total) + lin_begin, 0, lin_count * sizeof(uint32_t),
+                                   c->stream));
+        o = order_args(c);
+        HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+        if (c->n_tiles) WLD_TRY(launch_pairs(c, thr, o, nullptr));
+        HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+        unsigned long long *d_total = ptr<unsigned long long>(c->counters) + 1;
+        if (lin_count) {
+            launch_chunk_scan(ptr<uint32_t>(c->chunk_total), lin_begin, lin_count, ptr<uint32_t>(c->chunk_base),
+                              d_total, c->stream);
+            HIP_TRY(hipGetLastError());
+        }
+        HIP_TRY(hipMemcpyAsync(h, c->counters.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (h[0] <= c->st_capacity) break;
+        if (attempt == 1) return fail(WLD_E_HIP, "internal: staging overflow after resize");
+        WLD_TRY(grow_staging(h[0]));
+    }
     const uint64_t rows = h[1];
     if (h[0] != h[1]) return fail(WLD_E_HIP, "internal: staging cursor %llu != chunk total %llu", h[0], h[1]);
     WLD_TRY(ensure(c->out_a, std::max<uint64_t>(rows, 1) * 4));

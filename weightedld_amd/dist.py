@@ -1,0 +1,75 @@
+"""Multi-GPU sharding of the pair space and the gather of passing rows.
+
+The L^2 pair space is split by contiguous 256-site chunk rows (the reference's
+chunking, lib.rs:615-634) into balanced row blocks, one per rank (one process
+per GPU).  Pairs are independent, so ranks exchange nothing while computing.
+Each rank leaves its rows on its GPU in reference order; the only collective is
+the final gather of those rows to rank 0 (RCCL over xGMI with the "nccl"
+backend; gloo in the CPU tests).  Because chunk rows DESCEND in the reference's
+triu_index order (lib.rs:623-632), rank 0 concatenates the shards in
+descending rank order.
+"""
+import numpy as np
+
+from .api import Context
+
+ROW_FIELDS = ("site_a", "site_b", "d", "d_prime", "r2")
+
+
+def shard_rows(n_sites, world, rank):
+    """Chunk rows [begin, end) of this rank (balanced pair counts)."""
+    return Context.shard_chunk_rows(n_sites, world, rank)
+
+
+def pack_rows_device(ctx, n, device):
+    """The last run's rows as one [5, n] int32 tensor on `device` (floats bit-cast)."""
+    import torch
+
+    packed = torch.zeros((5, max(n, 0)), dtype=torch.int32, device=device)
+    if n:
+        ctx.rows_copy_device(*(packed[i].data_ptr() for i in range(5)))
+    return packed
+
+
+def pack_rows_host(store):
+    """A PairStore (host numpy) as a [5, n] int32 tensor (floats bit-cast)."""
+    import torch
+
+    cols = [np.ascontiguousarray(getattr(store, f)) for f in ROW_FIELDS] if not isinstance(store, dict) else \
+        [np.ascontiguousarray(store[f]) for f in ROW_FIELDS]
+    arr = np.stack([c.astype(np.uint32).view(np.int32) if c.dtype.kind == "u" else c.view(np.int32)
+                    for c in cols]) if len(cols[0]) else np.zeros((5, 0), dtype=np.int32)
+    return torch.from_numpy(np.ascontiguousarray(arr))
+
+
+def unpack_rows(packed):
+    """[5, n] int32 tensor -> dict of numpy columns."""
+    a = packed.cpu().numpy()
+    return {"site_a": a[0].view(np.uint32), "site_b": a[1].view(np.uint32), "d": a[2].view(np.float32),
+            "d_prime": a[3].view(np.float32), "r2": a[4].view(np.float32)}
+
+
+def gather_rows(packed, rank, world, group=None):
+    """Gathers every rank's [5, n_r] rows to rank 0.  Returns the [5, sum n_r]
+    concatenation in reference order on rank 0 (shards in descending rank
+    order), None elsewhere.  One count all_gather + one padded gather."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return packed
+    cnt = torch.tensor([packed.shape[1]], dtype=torch.int64, device=packed.device)
+    cnts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt, group=group)
+    counts = [int(c.item()) for c in cnts]
+    m = max(counts)
+    if m == 0:
+        return torch.zeros((5, 0), dtype=torch.int32, device=packed.device) if rank == 0 else None
+    if packed.shape[1] < m:
+        pad = torch.zeros((5, m - packed.shape[1]), dtype=torch.int32, device=packed.device)
+        packed = torch.cat([packed, pad], dim=1)
+    gl = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
+    dist.gather(packed.contiguous(), gl, dst=0, group=group)
+    if rank != 0:
+        return None
+    return torch.cat([gl[g][:, :counts[g]] for g in reversed(range(world))], dim=1)
