@@ -84,8 +84,9 @@ struct wld_ctx {
     // loaded SiteSet
     bool loaded = false;
     size_t L = 0, N = 0, LP = 0, NP = 0;
-    DevBuf raw, wraw, codes, w_pad, wstats, site_ok, site_map, planes;
+    DevBuf raw, wraw, codes, w_pad, wstats, site_ok, site_map, planes, frag;
     bool has_map = false;
+    bool use_frag = false;
     int kernel = WLD_KERNEL_VALU;
     bool safe = false;
     int shift = 0;
@@ -103,7 +104,7 @@ struct wld_ctx {
 
     ~wld_ctx() {
         (void)hipSetDevice(device);
-        DevBuf *all[] = {&raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &tiles,
+        DevBuf *all[] = {&raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &tiles,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
@@ -173,10 +174,19 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     c->shift = 0;
     if (k == WLD_KERNEL_MFMA) {
         c->shift = weight_shift(maxabs);
-        WLD_TRY(ensure(c->planes, 3 * c->NP));
+        WLD_TRY(ensure(c->planes, mfma_planes_bytes(c->NP)));
         launch_mfma_prep(ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), c->LP, c->NP, c->shift,
                          ptr<int8_t>(c->planes), c->stream);
         HIP_TRY(hipGetLastError());
+        // fragment-major copy of the codes (1 KB contiguous per wave operand load);
+        // WLD_MFMA_LAYOUT=rows keeps the site-major reads (A/B experiments)
+        const char *lay = getenv("WLD_MFMA_LAYOUT");
+        c->use_frag = !(lay && std::string(lay) == "rows");
+        if (c->use_frag) {
+            WLD_TRY(ensure(c->frag, c->LP * c->NP));
+            launch_frag(ptr<uint8_t>(c->codes), c->LP, c->NP, ptr<uint8_t>(c->frag), c->stream);
+            HIP_TRY(hipGetLastError());
+        }
     }
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
 
@@ -245,11 +255,14 @@ OrderArgs order_args(wld_ctx *c) {
 
 int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *dense) {
     const uint32_t n = chunk_rows_of(c->L);
-    if (c->kernel == WLD_KERNEL_MFMA)
-        launch_pair_mfma(ptr<uint8_t>(c->codes), ptr<int8_t>(c->planes), ptr<uint8_t>(c->site_ok),
-                         ptr<uint32_t>(c->tiles), c->n_tiles, (uint32_t)c->L, (uint32_t)c->NP, n, thr, c->shift, o,
-                         dense, c->stream);
-    else
+    if (c->kernel == WLD_KERNEL_MFMA) {
+        // the exact-integer r2 prefilter needs a positive threshold to reject
+        // anything; WLD_NO_PREFILTER=1 disables it (A/B experiments)
+        const bool prefilter = thr > 0.0f && !getenv("WLD_NO_PREFILTER");
+        launch_pair_mfma(ptr<uint8_t>(c->codes), c->use_frag ? ptr<uint8_t>(c->frag) : nullptr,
+                         ptr<int8_t>(c->planes), ptr<uint8_t>(c->site_ok), ptr<uint32_t>(c->tiles), c->n_tiles,
+                         (uint32_t)c->L, (uint32_t)c->NP, n, thr, c->shift, prefilter, o, dense, c->stream);
+    } else
         launch_pair_valu(ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), ptr<uint8_t>(c->site_ok),
                          ptr<uint32_t>(c->tiles), c->n_tiles, (uint32_t)c->L, (uint32_t)c->NP, n, thr, c->safe, o,
                          dense, c->stream);

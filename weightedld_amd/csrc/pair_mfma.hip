@@ -10,7 +10,7 @@
 //   * weights become fixed point q_k = rint(w_k * 2^shift), |q_k| < 2^23, split
 //     into three balanced base-256 digits d_p in [-128,127]
 //     (q = d0 + 256 d1 + 65536 d2; built once per load by mfma_prep_kernel);
-//   * A operand (a sites): indicator byte & digit byte  (in & d_p, maj & d_p);
+//   * A operand (a sites): indicator byte mask & digit byte (in & d_p, maj & d_p);
 //     B operand (b sites): indicator bytes 0/1;
 //   * 12 v_mfma_i32_32x32x32_i8 per 32 sequences accumulate the 2x3x2
 //     (channel_a, plane, channel_b) partial sums in int32, exactly;
@@ -23,59 +23,126 @@
 //
 // Tiling: a 256-thread workgroup owns a 64x64 tile of site pairs (the tile
 // list is the triangular set of (a-tile, b-tile) with b-tile >= a-tile of the
-// shard's chunk rows); each wave owns a 32x32 sub-tile and streams its 32 a-
-// and 32 b-site code rows (16 bytes per lane per 32 sequences) straight from
-// HBM/L2 into registers.  Passing rows are compacted per 64x64 tile in LDS
-// exactly like the VALU kernel (order.hip assembles the reference order).
+// shard's chunk rows); wave w owns the 32x32 sub-tile (w>>1, w&1).  Operands
+// stream through an LDS ring of kRing 32-sequence stages filled with
+// global_load_lds (async, no VGPRs): per stage each wave copies one 1 KB code
+// fragment block (A0, A1, B0, B1 of the fragment-major layout) and wave 0 the
+// 96 bytes of weight digits; waves then read their A/B fragments with
+// ds_read_b128.  Passing rows are compacted per 64x64 tile in LDS
+// (order.hip assembles the reference order).
 #include "pair_common.hpp"
 
 namespace wld {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void;
 
 bool mfma_supported() { return true; }
 
-// digit planes [3][NP] int8 of q = rint(w * 2^shift)
+namespace {
+constexpr int kRing = 4;            // LDS ring depth (stages of 32 sequences)
+constexpr int kSlot = 4096 + 128;   // A0 A1 B0 B1 (1 KB each) + 96 B digits, 16-B aligned
+constexpr int kDigBlock = 96;       // digit bytes per 32 sequences: [plane 0..2][half 0..1][16]
+}  // namespace
+
+// Weight digits of q = rint(w * 2^shift) in two layouts:
+//   planes[p*NP + k]                      (plane-major, site-major kernel path)
+//   digf[kb*96 + (2p + h)*16 + j]         (per 32-sequence block, ring path;
+//                                          k = 32kb + 16h + j)
 __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict__ w_pad, uint32_t NP, int shift,
-                                                         int8_t *__restrict__ planes) {
+                                                         int8_t *__restrict__ planes, int8_t *__restrict__ digf) {
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
     if (k >= NP) return;
     long long q = llrint(ldexp((double)w_pad[k], shift));
-    int d[3];
+    const uint32_t kb = k >> 5, h = (k >> 4) & 1, j = k & 15;
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
-        long long r = ((q + 128) & 255) - 128;  // balanced digit in [-128, 127]
-        d[p] = (int)r;
+        const long long r = ((q + 128) & 255) - 128;  // balanced digit in [-128, 127]
         q = (q - r) / 256;
+        planes[p * NP + k] = (int8_t)r;
+        digf[kb * kDigBlock + (2 * p + h) * 16 + j] = (int8_t)r;
     }
-    planes[k] = (int8_t)d[0];
-    planes[NP + k] = (int8_t)d[1];
-    planes[2 * NP + k] = (int8_t)d[2];
+}
+
+// codes_frag: the (site, sequence) code bytes in "fragment-major" order, so a
+// wave's A or B operand for 32 sites x 32 sequences is one contiguous 1 KB
+// block (lane l = 32h + r gets site r, sequences 16h..16h+15 — the MFMA
+// operand layout):
+//   frag[((g * NKB + kb) * 64 + l) * 16 + j] = codes[(32g + (l&31)) * NP + 32kb + 16(l>>5) + j]
+__global__ __launch_bounds__(256) void frag_kernel(const uint8_t *__restrict__ codes, uint32_t LP, uint32_t NP,
+                                                    uint8_t *__restrict__ frag) {
+    const uint32_t NKB = NP / 32;
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;  // one 16-byte chunk
+    if (idx >= (size_t)LP * NP / 16) return;
+    const uint32_t l = idx & 63;
+    const size_t t = idx >> 6;
+    const uint32_t kb = t % NKB;
+    const size_t g = t / NKB;
+    const uint4 v = *reinterpret_cast<const uint4 *>(codes + (g * 32 + (l & 31)) * NP + kb * 32 + (l >> 5) * 16);
+    *reinterpret_cast<uint4 *>(frag + idx * 16) = v;
 }
 
 __device__ __forceinline__ v16i mfma_i8(v4i a, v4i b, v16i c) {
     return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
 }
 
-template <bool DENSE>
+// Byte-wise masks from code bytes c in {0 (out), 1 (minor), 3 (major)}:
+// v_perm_b32 with zero sources returns, per selector byte, 0xFF for >= 13 and
+// 0x00 for 8..12 — a byte compare without a multiply.
+__device__ __forceinline__ v4i mask_in(v4i c) {  // c+12 in {12,13,15}: 00 FF FF
+    v4i m;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e] = (int)__builtin_amdgcn_perm(0u, 0u, (unsigned)c[e] | 0x0C0C0C0Cu);
+    return m;
+}
+__device__ __forceinline__ v4i mask_maj(v4i c) {  // c+10 in {10,11,13}: 00 00 FF
+    v4i m;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e] = (int)__builtin_amdgcn_perm(0u, 0u, (unsigned)c[e] + 0x0A0A0A0Au);
+    return m;
+}
+
+// 12 MFMAs of one 32-sequence block for this wave's 32x32 sub-tile
+__device__ __forceinline__ void mfma_block(v16i (&acc)[2][3][2], v4i ca, v4i cb, v4i d0, v4i d1, v4i d2) {
+    const v4i one = {0x01010101, 0x01010101, 0x01010101, 0x01010101};
+    const v4i b_in = cb & one;
+    const v4i b_maj = (cb >> 1) & one;
+    const v4i a_in = mask_in(ca);
+    const v4i a_maj = mask_maj(ca);
+    const v4i dp[3] = {d0, d1, d2};
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const v4i ai = a_in & dp[p];
+        const v4i am = a_maj & dp[p];
+        acc[0][p][0] = mfma_i8(ai, b_in, acc[0][p][0]);
+        acc[0][p][1] = mfma_i8(ai, b_maj, acc[0][p][1]);
+        acc[1][p][0] = mfma_i8(am, b_in, acc[1][p][0]);
+        acc[1][p][1] = mfma_i8(am, b_maj, acc[1][p][1]);
+    }
+}
+
+// DENSE: write every pair's stats (tests).  RING: fragment-major codes through
+// the LDS ring (else site-major codes read straight into registers).
+// PREFILTER (threshold > 0): skip the f32 epilogue for pairs whose exact r2,
+// evaluated in f64 from the exact integer sums, lies clearly below the threshold.
+template <bool DENSE, bool RING, bool PREFILTER>
 __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__restrict__ codes,
                                                             const int8_t *__restrict__ planes,
                                                             const uint8_t *__restrict__ site_ok,
                                                             const uint32_t *__restrict__ tiles, uint32_t L,
                                                             uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
                                                             OrderArgs o, DenseArgs dn) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kRing * kSlot];  // the only LDS object
+
     const uint32_t tile = tiles[blockIdx.x];
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
     const uint32_t a0 = ta * kTile, b0 = tb * kTile;
     const uint32_t tid = threadIdx.x;
-    const uint32_t wave = tid >> 6, lane = tid & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const uint32_t wa = wave >> 1, wb = wave & 1;
     const uint32_t r = lane & 31, h = lane >> 5;
-
-    const uint8_t *pa = codes + (size_t)(a0 + 32 * wa + r) * NP + 16 * h;
-    const uint8_t *pb = codes + (size_t)(b0 + 32 * wb + r) * NP + 16 * h;
-    const int8_t *pd = planes + 16 * h;
+    const uint32_t NKB = NP / 32;
 
     v16i acc[2][3][2];
 #pragma unroll
@@ -87,40 +154,57 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
 #pragma unroll
                 for (int e = 0; e < 16; ++e) acc[x][p][y][e] = 0;
 
-    v4i ca = *reinterpret_cast<const v4i *>(pa);
-    v4i cb = *reinterpret_cast<const v4i *>(pb);
-    v4i d0 = *reinterpret_cast<const v4i *>(pd);
-    v4i d1 = *reinterpret_cast<const v4i *>(pd + NP);
-    v4i d2 = *reinterpret_cast<const v4i *>(pd + 2 * NP);
-    for (uint32_t k0 = 0; k0 < NP; k0 += 32) {
-        // prefetch the next 32 sequences while this block's MFMAs run
-        const uint32_t kn = (k0 + 32 < NP) ? k0 + 32 : k0;
-        const v4i na = *reinterpret_cast<const v4i *>(pa + kn);
-        const v4i nb = *reinterpret_cast<const v4i *>(pb + kn);
-        const v4i n0 = *reinterpret_cast<const v4i *>(pd + kn);
-        const v4i n1 = *reinterpret_cast<const v4i *>(pd + NP + kn);
-        const v4i n2 = *reinterpret_cast<const v4i *>(pd + 2 * NP + kn);
-
-        const v4i one = {0x01010101, 0x01010101, 0x01010101, 0x01010101};
-        const v4i b_in = cb & one;
-        const v4i b_maj = (cb >> 1) & one;
-        const v4i a_in = (ca & one) * 0xFF;         // 0x00 / 0xFF byte masks
-        const v4i a_maj = ((ca >> 1) & one) * 0xFF;
-        const v4i dp[3] = {d0, d1, d2};
+    if constexpr (RING) {
+        // this wave's share of every stage: code block A0/A1/B0/B1, wave 0 also the digits
+        const uint32_t g_src = wave < 2 ? (a0 >> 5) + wave : (b0 >> 5) + (wave - 2);
+        const uint8_t *src = codes + ((size_t)g_src * NKB * 64 + lane) * 16;
+        const int8_t *dsrc = planes + 3 * (size_t)NP + lane * 16;  // digf
+        auto issue = [&](uint32_t kb) {
+            uint8_t *slot = smem + (kb % kRing) * kSlot;
+            __builtin_amdgcn_global_load_lds(src + (size_t)kb * 1024, (lds_void *)(slot + wave * 1024), 16, 0, 0);
+            if (wave == 0 && lane < 6)
+                __builtin_amdgcn_global_load_lds(dsrc + (size_t)kb * kDigBlock, (lds_void *)(slot + 4096), 16, 0, 0);
+        };
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
-            const v4i ai = a_in & dp[p];
-            const v4i am = a_maj & dp[p];
-            acc[0][p][0] = mfma_i8(ai, b_in, acc[0][p][0]);
-            acc[0][p][1] = mfma_i8(ai, b_maj, acc[0][p][1]);
-            acc[1][p][0] = mfma_i8(am, b_in, acc[1][p][0]);
-            acc[1][p][1] = mfma_i8(am, b_maj, acc[1][p][1]);
+        for (int s = 0; s < kRing - 1; ++s)
+            if ((uint32_t)s < NKB) issue(s);
+        for (uint32_t kb = 0; kb < NKB; ++kb) {
+            // block kb has landed once at most `ahead` newer stages of this wave are in flight
+            const uint32_t last = min(NKB - 1, kb + kRing - 2);
+            const uint32_t ahead = last - kb;  // 0 .. kRing-2 (=2)
+            if (wave == 0) {  // two glds per stage
+                if (ahead >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else if (ahead == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
+                if (ahead >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                else if (ahead == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __builtin_amdgcn_s_barrier();  // every wave's part of stage kb is in LDS; stage kb-1 is free
+            asm volatile("" ::: "memory");
+            if (kb + kRing - 1 < NKB) issue(kb + kRing - 1);
+            const uint8_t *slot = smem + (kb % kRing) * kSlot;
+            const v4i ca = *reinterpret_cast<const v4i *>(slot + wa * 1024 + lane * 16);
+            const v4i cb = *reinterpret_cast<const v4i *>(slot + 2048 + wb * 1024 + lane * 16);
+            const v4i d0 = *reinterpret_cast<const v4i *>(slot + 4096 + (0 + h) * 16);
+            const v4i d1 = *reinterpret_cast<const v4i *>(slot + 4096 + (2 + h) * 16);
+            const v4i d2 = *reinterpret_cast<const v4i *>(slot + 4096 + (4 + h) * 16);
+            mfma_block(acc, ca, cb, d0, d1, d2);
         }
-        ca = na;
-        cb = nb;
-        d0 = n0;
-        d1 = n1;
-        d2 = n2;
+        __syncthreads();  // ring reads done before the compaction reuses smem
+    } else {
+        const uint8_t *pa = codes + (size_t)(a0 + 32 * wa + r) * NP + 16 * h;
+        const uint8_t *pb = codes + (size_t)(b0 + 32 * wb + r) * NP + 16 * h;
+        const int8_t *pd = planes + 16 * h;
+        for (uint32_t k0 = 0; k0 < NP; k0 += 32) {
+            const v4i ca = *reinterpret_cast<const v4i *>(pa + k0);
+            const v4i cb = *reinterpret_cast<const v4i *>(pb + k0);
+            const v4i d0 = *reinterpret_cast<const v4i *>(pd + k0);
+            const v4i d1 = *reinterpret_cast<const v4i *>(pd + NP + k0);
+            const v4i d2 = *reinterpret_cast<const v4i *>(pd + 2 * NP + k0);
+            mfma_block(acc, ca, cb, d0, d1, d2);
+        }
     }
 
     // ---- epilogue: lane holds b = b0+32wb+r and 16 a rows -------------------
@@ -134,21 +218,41 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
     for (int i = 0; i < 16; ++i) {
         const uint32_t a_local = 32 * wa + (i & 3) + 8 * (i >> 2) + 4 * h;
         const uint32_t a = a0 + a_local;
+        const bool valid = okb && a < b && site_ok[a];
+        long long S[2][2];
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+                S[x][y] = (long long)acc[x][0][y][i] + ((long long)acc[x][1][y][i] << 8) +
+                          ((long long)acc[x][2][y][i] << 16);
+        if constexpr (!DENSE) {
+            if (!valid) continue;
+            if constexpr (PREFILTER) {
+                // Exact algebra: d = PA*PB - P(AB) and r2 = d^2/(PA Pa PB Pb) become
+                // r2 = (SA*SB - SAB*T)^2 / (SA (T-SA) SB (T-SB)) on the exact sums.
+                // Evaluated in f64 (|err| ~1e-16 relative); pairs more than
+                // 1e-5 + 1e-4|thr| below the threshold cannot pass the f32
+                // epilogue, so they skip it.  Everything else (and den <= 0,
+                // the NaN/inf cases) takes the full reference epilogue.
+                const double T = (double)S[0][0], SA = (double)S[1][0], SB = (double)S[0][1],
+                             SAB = (double)S[1][1];
+                const double num = SA * SB - SAB * T;
+                const double den = SA * (T - SA) * SB * (T - SB);
+                const double cut = (double)thr - (1e-5 + 1e-4 * fabs((double)thr));
+                if (den > 0.0 && num * num < cut * den) continue;
+            }
+        }
         float s[2][2];
 #pragma unroll
         for (int x = 0; x < 2; ++x)
 #pragma unroll
-            for (int y = 0; y < 2; ++y) {
-                const long long v = (long long)acc[x][0][y][i] + ((long long)acc[x][1][y][i] << 8) +
-                                    ((long long)acc[x][2][y][i] << 16);
-                s[x][y] = (float)((double)v * scale);
-            }
+            for (int y = 0; y < 2; ++y) s[x][y] = (float)((double)S[x][y] * scale);
         float d, dp, r2;
         ld_epilogue(s[0][0], s[1][0], s[0][1], s[1][1], d, dp, r2);
         res[i][0] = d;
         res[i][1] = dp;
         res[i][2] = r2;
-        const bool valid = okb && a < b && site_ok[a];
         if constexpr (DENSE) {
             if (a < b && b < L) {
                 const size_t k = (size_t)a * L + b;
@@ -164,8 +268,8 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
     if constexpr (DENSE) return;
 
     // ---- compaction: a 64x64 pass-bit matrix in LDS, rows in b order ----------
-    __shared__ unsigned long long sBits[kTile];
-    __shared__ uint32_t sRowBase[kTile];
+    unsigned long long *sBits = reinterpret_cast<unsigned long long *>(smem);  // [64]
+    uint32_t *sRowBase = reinterpret_cast<uint32_t *>(smem + kTile * 8);      // [64]
     if (tid < kTile) sBits[tid] = 0ull;
     __syncthreads();
     if (pass) {
@@ -212,21 +316,48 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
     }
 }
 
+size_t mfma_planes_bytes(size_t NP) { return 3 * NP + (NP / 32) * kDigBlock; }
+
 void launch_mfma_prep(const uint8_t *, const float *w_pad, size_t, size_t NP, int shift, int8_t *planes,
                       hipStream_t s) {
     hipLaunchKernelGGL(mfma_prep_kernel, dim3((unsigned)((NP + 255) / 256)), dim3(256), 0, s, w_pad, (uint32_t)NP,
-                       shift, planes);
+                       shift, planes, planes + 3 * NP);
 }
 
-void launch_pair_mfma(const uint8_t *codes, const int8_t *wplanes, const uint8_t *site_ok, const uint32_t *tiles,
-                      uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
-                      const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
-    if (dense)
-        hipLaunchKernelGGL((pair_mfma_kernel<true>), dim3(n_tiles), dim3(256), 0, s, codes, wplanes, site_ok, tiles, L,
-                           NP, n_chunk_rows, thr, shift, o, *dense);
-    else
-        hipLaunchKernelGGL((pair_mfma_kernel<false>), dim3(n_tiles), dim3(256), 0, s, codes, wplanes, site_ok, tiles,
-                           L, NP, n_chunk_rows, thr, shift, o, DenseArgs{nullptr, nullptr, nullptr, nullptr});
+void launch_frag(const uint8_t *codes, size_t LP, size_t NP, uint8_t *frag, hipStream_t s) {
+    const size_t chunks = LP * NP / 16;
+    hipLaunchKernelGGL(frag_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, codes, (uint32_t)LP,
+                       (uint32_t)NP, frag);
+}
+
+void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const int8_t *wplanes, const uint8_t *site_ok,
+                      const uint32_t *tiles, uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows,
+                      float thr, int shift, bool prefilter, const OrderArgs &o, const DenseArgs *dense,
+                      hipStream_t s) {
+    const DenseArgs none{nullptr, nullptr, nullptr, nullptr};
+    const dim3 g(n_tiles), b(256);
+    if (dense) {
+        if (frag)
+            hipLaunchKernelGGL((pair_mfma_kernel<true, true, false>), g, b, 0, s, frag, wplanes, site_ok, tiles, L, NP,
+                               n_chunk_rows, thr, shift, o, *dense);
+        else
+            hipLaunchKernelGGL((pair_mfma_kernel<true, false, false>), g, b, 0, s, codes, wplanes, site_ok, tiles, L,
+                               NP, n_chunk_rows, thr, shift, o, *dense);
+    } else if (frag) {
+        if (prefilter)
+            hipLaunchKernelGGL((pair_mfma_kernel<false, true, true>), g, b, 0, s, frag, wplanes, site_ok, tiles, L, NP,
+                               n_chunk_rows, thr, shift, o, none);
+        else
+            hipLaunchKernelGGL((pair_mfma_kernel<false, true, false>), g, b, 0, s, frag, wplanes, site_ok, tiles, L,
+                               NP, n_chunk_rows, thr, shift, o, none);
+    } else {
+        if (prefilter)
+            hipLaunchKernelGGL((pair_mfma_kernel<false, false, true>), g, b, 0, s, codes, wplanes, site_ok, tiles, L,
+                               NP, n_chunk_rows, thr, shift, o, none);
+        else
+            hipLaunchKernelGGL((pair_mfma_kernel<false, false, false>), g, b, 0, s, codes, wplanes, site_ok, tiles, L,
+                               NP, n_chunk_rows, thr, shift, o, none);
+    }
 }
 
 }  // namespace wld
