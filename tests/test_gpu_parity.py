@@ -352,3 +352,33 @@ def test_config4_full_size_properties(ctxs, kern):
     ctx.load(sub, w)
     ctx.run(float("-inf"))
     compare_rows(ctx.rows(), O.all_pairs(sub, w, float("-inf")), float("-inf"), buf=sub, w=w)
+
+
+def test_mfma_lds_pipeline_race_screen(W, monkeypatch):
+    """Race screen for the MFMA kernel's LDS pipeline (global_load_lds groups):
+    the fragment-major LDS path and the site-major register path compute the
+    same exact integer sums and the same f32 epilogue, so at config-4 size and
+    a low threshold (~4e7 rows, 256-workgroup waves over every CU) they must
+    agree bit for bit, run after run."""
+    import torch
+    from weightedld_amd import dist as wdist
+    L, N = 20000, 2000
+    buf = synth(L, N, 77)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    dev = torch.device("cuda", 0)
+    monkeypatch.setenv("WLD_NO_PREFILTER", "1")
+    monkeypatch.setenv("WLD_MFMA_LAYOUT", "rows")
+    ref_ctx = W.Context(0, W.KERNEL_MFMA)
+    ref_ctx.load(buf, w)
+    monkeypatch.delenv("WLD_MFMA_LAYOUT")
+    n_ref = ref_ctx.run(0.001)
+    ref = wdist.pack_rows_device(ref_ctx, n_ref, dev)
+    del ref_ctx
+    ctx = W.Context(0, W.KERNEL_MFMA)
+    ctx.load(buf, w)
+    assert n_ref > 10_000_000
+    for _ in range(4):
+        n = ctx.run(0.001)
+        assert n == n_ref
+        got = wdist.pack_rows_device(ctx, n, dev)
+        assert torch.equal(got, ref)

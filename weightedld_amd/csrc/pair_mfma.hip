@@ -24,12 +24,16 @@
 // Tiling: a 256-thread workgroup owns a 64x64 tile of site pairs (the tile
 // list is the triangular set of (a-tile, b-tile) with b-tile >= a-tile of the
 // shard's chunk rows); wave w owns the 32x32 sub-tile (w>>1, w&1).  Operands
-// stream through an LDS ring of kRing 32-sequence stages filled with
-// global_load_lds (async, no VGPRs): per stage each wave copies one 1 KB code
-// fragment block (A0, A1, B0, B1 of the fragment-major layout) and wave 0 the
-// 96 bytes of weight digits; waves then read their A/B fragments with
-// ds_read_b128.  Passing rows are compacted per 64x64 tile in LDS
-// (order.hip assembles the reference order).
+// stream through LDS in groups of kGroup 32-sequence stages, double-buffered
+// and filled with global_load_lds (async, no VGPRs): per stage each wave copies
+// one 1 KB code-fragment block (A0, A1, B0, B1 of the fragment-major layout),
+// and per group wave 0 copies the group's 1 KB of weight digits (128 B per
+// stage).  Every DMA is a full-wave 1 KB copy, and a group is consumed only
+// after s_waitcnt vmcnt(0) + a barrier — correctness never depends on the
+// completion order of outstanding loads.  The next group's copies are issued
+// right after that barrier, one group (8 stages of MFMA work) ahead of use.
+// Passing rows are compacted per 64x64 tile in LDS (order.hip assembles the
+// reference order).
 #include "pair_common.hpp"
 
 namespace wld {
@@ -41,15 +45,16 @@ typedef __attribute__((address_space(3))) void lds_void;
 bool mfma_supported() { return true; }
 
 namespace {
-constexpr int kRing = 4;            // LDS ring depth (stages of 32 sequences)
-constexpr int kSlot = 4096 + 128;   // A0 A1 B0 B1 (1 KB each) + 96 B digits, 16-B aligned
-constexpr int kDigBlock = 96;       // digit bytes per 32 sequences: [plane 0..2][half 0..1][16]
+constexpr int kGroup = 8;                           // 32-sequence stages per LDS group
+constexpr int kStageCodes = 4096;                   // A0 A1 B0 B1, 1 KB each
+constexpr int kDigStage = 128;                      // digit bytes per stage: [plane][half][16] + 32 pad
+constexpr int kGroupBytes = kGroup * (kStageCodes + kDigStage);  // 33 KB; two groups in LDS
 }  // namespace
 
 // Weight digits of q = rint(w * 2^shift) in two layouts:
 //   planes[p*NP + k]                      (plane-major, site-major kernel path)
-//   digf[kb*96 + (2p + h)*16 + j]         (per 32-sequence block, ring path;
-//                                          k = 32kb + 16h + j)
+//   digf[kb*128 + (2p + h)*16 + j]        (per 32-sequence stage, LDS path;
+//                                          k = 32kb + 16h + j; bytes 96..127 pad)
 __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict__ w_pad, uint32_t NP, int shift,
                                                          int8_t *__restrict__ planes, int8_t *__restrict__ digf) {
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
@@ -61,7 +66,7 @@ __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict_
         const long long r = ((q + 128) & 255) - 128;  // balanced digit in [-128, 127]
         q = (q - r) / 256;
         planes[p * NP + k] = (int8_t)r;
-        digf[kb * kDigBlock + (2 * p + h) * 16 + j] = (int8_t)r;
+        digf[kb * kDigStage + (2 * p + h) * 16 + j] = (int8_t)r;
     }
 }
 
@@ -123,7 +128,7 @@ __device__ __forceinline__ void mfma_block(v16i (&acc)[2][3][2], v4i ca, v4i cb,
 }
 
 // DENSE: write every pair's stats (tests).  RING: fragment-major codes through
-// the LDS ring (else site-major codes read straight into registers).
+// the double-buffered LDS groups (else site-major codes read straight into registers).
 // PREFILTER (threshold > 0): skip the f32 epilogue for pairs whose exact r2,
 // evaluated in f64 from the exact integer sums, lies clearly below the threshold.
 template <bool DENSE, bool RING, bool PREFILTER>
@@ -133,7 +138,7 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
                                                             const uint32_t *__restrict__ tiles, uint32_t L,
                                                             uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
                                                             OrderArgs o, DenseArgs dn) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kRing * kSlot];  // the only LDS object
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kGroupBytes];  // the only LDS object
 
     const uint32_t tile = tiles[blockIdx.x];
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
@@ -155,44 +160,44 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
                 for (int e = 0; e < 16; ++e) acc[x][p][y][e] = 0;
 
     if constexpr (RING) {
-        // this wave's share of every stage: code block A0/A1/B0/B1, wave 0 also the digits
+        // this wave's code block per stage (A0/A1/B0/B1); wave 0 also the digit records
         const uint32_t g_src = wave < 2 ? (a0 >> 5) + wave : (b0 >> 5) + (wave - 2);
         const uint8_t *src = codes + ((size_t)g_src * NKB * 64 + lane) * 16;
         const int8_t *dsrc = planes + 3 * (size_t)NP + lane * 16;  // digf
-        auto issue = [&](uint32_t kb) {
-            uint8_t *slot = smem + (kb % kRing) * kSlot;
-            __builtin_amdgcn_global_load_lds(src + (size_t)kb * 1024, (lds_void *)(slot + wave * 1024), 16, 0, 0);
-            if (wave == 0 && lane < 6)
-                __builtin_amdgcn_global_load_lds(dsrc + (size_t)kb * kDigBlock, (lds_void *)(slot + 4096), 16, 0, 0);
-        };
+        const uint32_t n_groups = (NKB + kGroup - 1) / kGroup;
+        auto issue = [&](uint32_t grp) {
+            uint8_t *gb = smem + (grp & 1) * kGroupBytes;
+            const uint32_t kb0 = grp * kGroup;
 #pragma unroll
-        for (int s = 0; s < kRing - 1; ++s)
-            if ((uint32_t)s < NKB) issue(s);
-        for (uint32_t kb = 0; kb < NKB; ++kb) {
-            // block kb has landed once at most `ahead` newer stages of this wave are in flight
-            const uint32_t last = min(NKB - 1, kb + kRing - 2);
-            const uint32_t ahead = last - kb;  // 0 .. kRing-2 (=2)
-            if (wave == 0) {  // two glds per stage
-                if (ahead >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-                else if (ahead == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            } else {
-                if (ahead >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-                else if (ahead == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __builtin_amdgcn_s_barrier();  // every wave's part of stage kb is in LDS; stage kb-1 is free
+            for (int st = 0; st < kGroup; ++st)
+                if (kb0 + st < NKB)
+                    __builtin_amdgcn_global_load_lds(src + (size_t)(kb0 + st) * 1024,
+                                                     (lds_void *)(gb + st * kStageCodes + wave * 1024), 16, 0, 0);
+            if (wave == 0)  // digits of 8 stages = 1 KB (allocation padded to whole groups)
+                __builtin_amdgcn_global_load_lds(dsrc + (size_t)kb0 * kDigStage,
+                                                 (lds_void *)(gb + kGroup * kStageCodes), 16, 0, 0);
+        };
+        issue(0);
+        for (uint32_t grp = 0; grp < n_groups; ++grp) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of group grp landed
+            __builtin_amdgcn_s_barrier();                     // ... and every other wave's; group grp-1 is free
             asm volatile("" ::: "memory");
-            if (kb + kRing - 1 < NKB) issue(kb + kRing - 1);
-            const uint8_t *slot = smem + (kb % kRing) * kSlot;
-            const v4i ca = *reinterpret_cast<const v4i *>(slot + wa * 1024 + lane * 16);
-            const v4i cb = *reinterpret_cast<const v4i *>(slot + 2048 + wb * 1024 + lane * 16);
-            const v4i d0 = *reinterpret_cast<const v4i *>(slot + 4096 + (0 + h) * 16);
-            const v4i d1 = *reinterpret_cast<const v4i *>(slot + 4096 + (2 + h) * 16);
-            const v4i d2 = *reinterpret_cast<const v4i *>(slot + 4096 + (4 + h) * 16);
-            mfma_block(acc, ca, cb, d0, d1, d2);
+            if (grp + 1 < n_groups) issue(grp + 1);
+            const uint8_t *gb = smem + (grp & 1) * kGroupBytes;
+            const uint32_t n_st = min((uint32_t)kGroup, NKB - grp * kGroup);
+            for (uint32_t st = 0; st < n_st; ++st) {
+                const uint8_t *sc = gb + st * kStageCodes;
+                const uint8_t *sd = gb + kGroup * kStageCodes + st * kDigStage + h * 16;
+                const v4i ca = *reinterpret_cast<const v4i *>(sc + wa * 1024 + lane * 16);
+                const v4i cb = *reinterpret_cast<const v4i *>(sc + 2048 + wb * 1024 + lane * 16);
+                const v4i d0 = *reinterpret_cast<const v4i *>(sd);
+                const v4i d1 = *reinterpret_cast<const v4i *>(sd + 32);
+                const v4i d2 = *reinterpret_cast<const v4i *>(sd + 64);
+                mfma_block(acc, ca, cb, d0, d1, d2);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of group grp done before the barrier
         }
-        __syncthreads();  // ring reads done before the compaction reuses smem
+        __syncthreads();  // LDS reads done before the compaction reuses smem
     } else {
         const uint8_t *pa = codes + (size_t)(a0 + 32 * wa + r) * NP + 16 * h;
         const uint8_t *pb = codes + (size_t)(b0 + 32 * wb + r) * NP + 16 * h;
@@ -316,7 +321,10 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
     }
 }
 
-size_t mfma_planes_bytes(size_t NP) { return 3 * NP + (NP / 32) * kDigBlock; }
+size_t mfma_planes_bytes(size_t NP) {
+    const size_t n_groups = (NP / 32 + kGroup - 1) / kGroup;
+    return 3 * NP + n_groups * kGroup * kDigStage;  // digit records padded to whole groups
+}
 
 void launch_mfma_prep(const uint8_t *, const float *w_pad, size_t, size_t NP, int shift, int8_t *planes,
                       hipStream_t s) {
