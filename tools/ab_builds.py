@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""A/B timing of experimental library builds (tools/build_variant.sh), one
+child process per (round, build), interleaved.  Prints per-build median
+pair-kernel ms (HIP events) at a bench config with the default kernel."""
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(path, config, reps, thr):
+    sys.path.insert(0, REPO)
+    import torch  # noqa: F401
+    import weightedld_amd._lib as L
+    L.LIB_PATH = os.path.abspath(path)
+    import bench
+    import weightedld_amd as W
+    if "," in config:  # custom shape "N,L,thr"
+        N, Ls, thr0 = int(config.split(",")[0]), int(config.split(",")[1]), float(config.split(",")[2])
+    else:
+        N, Ls, thr0, _ = bench.CONFIGS[config]
+    thr = thr0 if thr is None else thr
+    buf = bench.synth(Ls, N)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ctx = W.Context(0, W.KERNEL_MFMA)
+    ctx.load(buf, w)
+    ctx.run(thr)
+    import ctypes
+    lib = W.lib()
+    st = None
+    if hasattr(lib, "wld_debug_stamps"):
+        st = (ctypes.c_ulonglong * 8)()
+        lib.wld_debug_stamps(st, 1)
+    t, rows = [], 0
+    for _ in range(reps):
+        rows = ctx.run(thr)
+        t.append(ctx.stats()["pair_kernel_ms"])
+    out = {"ms": t, "rows": rows}
+    ops = 24.0 * ((N + 63) // 64 * 64) * (Ls * (Ls - 1) / 2)
+    out["tops"] = ops / (sorted(t)[len(t) // 2] * 1e-3) / 1e12
+    if st is not None:
+        lib.wld_debug_stamps(st, 0)
+        n = max(st[5], 1)
+        out["stamps_per_wave"] = {"prologue": st[0] / n, "loop": st[1] / n, "epilogue": (st[2] - st[0] - st[1]) / n,
+                                  "compaction": st[3] / n, "waves": st[5]}
+    print(json.dumps(out))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--child")
+    ap.add_argument("--config", default="c4")
+    ap.add_argument("--thr", type=float)
+    ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("builds", nargs="*", help="name=path/to/libweightedld.so")
+    a = ap.parse_args()
+    if a.child:
+        return child(a.child, a.config, a.reps, a.thr)
+    res = {}
+    for _ in range(a.rounds):
+        for b in a.builds:
+            name, path = b.split("=", 1)
+            cmd = [sys.executable, __file__, "--child", path, "--config", a.config, "--reps", str(a.reps)]
+            if a.thr is not None:
+                cmd += ["--thr", str(a.thr)]
+            out = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            if out.returncode:
+                print(json.dumps({"build": name, "rc": out.returncode, "err": out.stderr[-800:]}), flush=True)
+                if out.returncode < 0 or out.returncode >= 124:
+                    sys.exit(out.returncode if out.returncode > 0 else 1)
+                continue
+            r = json.loads(out.stdout.strip().splitlines()[-1])
+            res.setdefault(name, {"ms": [], "rows": r["rows"]})["ms"] += r["ms"]
+            print(json.dumps({"build": name, "median_ms": statistics.median(r["ms"]), "rows": r["rows"], "tops": r["tops"],
+                              "stamps": r.get("stamps_per_wave")}), flush=True)
+    for name, r in res.items():
+        print(json.dumps({"build": name, "median_ms": statistics.median(r["ms"]), "min_ms": min(r["ms"]),
+                          "rows": r["rows"], "n": len(r["ms"])}))
+
+
+if __name__ == "__main__":
+    main()
