@@ -65,10 +65,16 @@ def main():
     for _ in range(a.rounds):
         for b in a.builds:
             name, path = b.split("=", 1)
+            env = dict(os.environ)
+            if "@" in path:  # name=path@VAR=value[,VAR=value]
+                path, kvs = path.split("@", 1)
+                for kv in kvs.split(","):
+                    k, v = kv.split("=", 1)
+                    env[k] = v
             cmd = [sys.executable, __file__, "--child", path, "--config", a.config, "--reps", str(a.reps)]
             if a.thr is not None:
                 cmd += ["--thr", str(a.thr)]
-            out = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
             if out.returncode:
                 print(json.dumps({"build": name, "rc": out.returncode, "err": out.stderr[-800:]}), flush=True)
                 if out.returncode < 0 or out.returncode >= 124:

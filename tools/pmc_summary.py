@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc CSVs for the pair kernel: per-dispatch averages,
+effective clock (GRBM_GUI_ACTIVE / 8 / duration) and MFMA busy fraction."""
+import collections
+import csv
+import glob
+import sys
+
+for f in sorted(glob.glob(sys.argv[1] + "/**/*_counter_collection.csv", recursive=True)):
+    agg = collections.defaultdict(list)
+    dur = {}
+    for r in csv.DictReader(open(f)):
+        if "pair_mfma" not in r["Kernel_Name"]:
+            continue
+        agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    if not agg:
+        continue
+    m = {k: sum(v) / len(v) for k, v in agg.items()}
+    d = sum(dur.values()) / len(dur)
+    out = {"file": f.split("/")[-1], "ms": round(d * 1e3, 3)}
+    if "GRBM_GUI_ACTIVE" in m:
+        cyc = m["GRBM_GUI_ACTIVE"] / 8
+        out["ghz"] = round(cyc / d / 1e9, 3)
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+            out["mfma_busy"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / cyc, 3)
+    if "SQ_WAVE_CYCLES" in m:
+        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            if k in m:
+                out[k] = round(m[k] / m["SQ_WAVE_CYCLES"], 3)
+    for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"):
+        if k in m:
+            out[k] = m[k]
+    print(out)

@@ -15,6 +15,9 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
+import weightedld_amd._lib as _L  # noqa: E402
+if os.environ.get("WLD_TOOL_LIB"):
+    _L.LIB_PATH = os.path.abspath(os.environ["WLD_TOOL_LIB"])
 import weightedld_amd as W  # noqa: E402
 from weightedld_amd import dist as wdist  # noqa: E402
 

@@ -174,8 +174,8 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     c->shift = 0;
     if (k == WLD_KERNEL_MFMA) {
         c->shift = weight_shift(maxabs);
-        WLD_TRY(ensure(c->planes, mfma_planes_bytes(c->NP)));
-        launch_mfma_prep(ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), c->LP, c->NP, c->shift,
+        WLD_TRY(ensure(c->planes, mfma_planes_bytes(c->LP, c->NP)));
+        launch_mfma_prep(ptr<uint8_t>(c->site_ok), ptr<float>(c->w_pad), L, c->LP, c->NP, c->shift,
                          ptr<int8_t>(c->planes), c->stream);
         HIP_TRY(hipGetLastError());
         // fragment-major copy of the codes (1 KB contiguous per wave operand load);
@@ -260,8 +260,8 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         // anything; WLD_NO_PREFILTER=1 disables it (A/B experiments)
         const bool prefilter = thr > 0.0f && !getenv("WLD_NO_PREFILTER");
         launch_pair_mfma(ptr<uint8_t>(c->codes), c->use_frag ? ptr<uint8_t>(c->frag) : nullptr,
-                         ptr<int8_t>(c->planes), ptr<uint8_t>(c->site_ok), ptr<uint32_t>(c->tiles), c->n_tiles,
-                         (uint32_t)c->L, (uint32_t)c->NP, n, thr, c->shift, prefilter, o, dense, c->stream);
+                         ptr<int8_t>(c->planes), ptr<uint32_t>(c->tiles), c->n_tiles, (uint32_t)c->L,
+                         (uint32_t)c->NP, n, thr, c->shift, prefilter, o, dense, c->stream);
     } else
         launch_pair_valu(ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), ptr<uint8_t>(c->site_ok),
                          ptr<uint32_t>(c->tiles), c->n_tiles, (uint32_t)c->L, (uint32_t)c->NP, n, thr, c->safe, o,

@@ -48,14 +48,16 @@ void launch_pair_valu(const uint8_t *codes, const float *w, const uint8_t *site_
 
 // pair_mfma.hip
 bool mfma_supported();
-size_t mfma_planes_bytes(size_t NP);  // weight digits: plane-major + per-block layouts
-void launch_mfma_prep(const uint8_t *codes, const float *w_pad, size_t LP, size_t NP, int shift, int8_t *planes,
-                      hipStream_t s);
+// weight digits (two layouts) + per-64-site filter bits
+size_t mfma_planes_bytes(size_t LP, size_t NP);
+void launch_mfma_prep(const uint8_t *site_ok, const float *w_pad, size_t L, size_t LP, size_t NP, int shift,
+                      int8_t *planes, hipStream_t s);
 void launch_frag(const uint8_t *codes, size_t LP, size_t NP, uint8_t *frag, hipStream_t s);
-void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const int8_t *wplanes, const uint8_t *site_ok,
-                      const uint32_t *tiles, uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows,
-                      float thr, int shift, bool prefilter, const OrderArgs &o, const DenseArgs *dense,
-                      hipStream_t s);
+// frag != nullptr: LDS-streaming kernel on the fragment-major copy; else the
+// site-major kernel
+void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const int8_t *wplanes, const uint32_t *tiles,
+                      uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
+                      bool prefilter, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
 
 // order.hip
 void launch_chunk_scan(const uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,

@@ -10,66 +10,67 @@
 //   * weights become fixed point q_k = rint(w_k * 2^shift), |q_k| < 2^23, split
 //     into three balanced base-256 digits d_p in [-128,127]
 //     (q = d0 + 256 d1 + 65536 d2; built once per load by mfma_prep_kernel);
-//   * A operand (a sites): indicator byte mask & digit byte (in & d_p, maj & d_p);
-//     B operand (b sites): indicator bytes 0/1;
+//   * A operand (a sites): the digit where the indicator is set (in & d_p,
+//     maj & d_p); B operand (b sites): indicator bytes 0/1;
 //   * 12 v_mfma_i32_32x32x32_i8 per 32 sequences accumulate the 2x3x2
 //     (channel_a, plane, channel_b) partial sums in int32, exactly;
-//   * epilogue: S = sum_p 2^(8p) acc_p in int64 (exact), converted once to f32
+//   * epilogue: S = sum_p 2^(8p) acc_p, exact in f64, converted once to f32
 //     (correctly rounded: the f32 the reference's sum would be without its
 //     rounding error), then the reference epilogue (lib.rs:482-520) in f32.
 // Exact integer sums keep the reference's degenerate-pair behaviour exactly:
 // SA == T implies SAB == SB, so monomorphic-in-mask pairs give 0/0 = NaN and
 // are dropped by the strict r2 > threshold (lib.rs:660).
 //
-// Tiling: a 256-thread workgroup owns a 64x64 tile of site pairs (the tile
-// list is the triangular set of (a-tile, b-tile) with b-tile >= a-tile of the
-// shard's chunk rows); wave w owns the 32x32 sub-tile (w>>1, w&1).  Operands
-// stream through LDS in groups of kGroup 32-sequence stages, double-buffered
-// and filled with global_load_lds (async, no VGPRs): per stage each wave copies
-// one 1 KB code-fragment block (A0, A1, B0, B1 of the fragment-major layout),
-// and per group wave 0 copies the group's 1 KB of weight digits (128 B per
-// stage).  Every DMA is a full-wave 1 KB copy, and a group is consumed only
-// after s_waitcnt vmcnt(0) + a barrier — correctness never depends on the
-// completion order of outstanding loads.  The next group's copies are issued
-// right after that barrier, one group (8 stages of MFMA work) ahead of use.
-// Passing rows are compacted per 64x64 tile in LDS (order.hip assembles the
+// Work decomposition: the pair space is cut into 64x64 site tiles (the
+// triangular list of (a-tile, b-tile), b-tile >= a-tile, of the shard's chunk
+// rows); a 256-thread workgroup computes a tile, wave w the 32x32 sub-tile
+// (w>>1, w&1); two workgroups share a CU, so one's epilogue and first-group
+// latency overlap the other's matrix work.  Operands stream through LDS in
+// groups of kGroup 32-sequence stages, double-buffered and filled by LDS-DMA
+// (global_load_lds_dwordx4, async, no VGPRs): per stage each wave copies one
+// 1 KB code-fragment block (A0, A1, B0, B1 of the fragment-major layout) and
+// per group wave 0 the group's 1 KB of weight digits.  Every DMA is a
+// full-wave 1 KB copy, and a group is consumed only after s_waitcnt vmcnt(0)
+// by every issuing wave + a barrier — correctness never depends on the
+// completion order of outstanding loads; a buffer is refilled only after the
+// barrier that follows its readers' s_waitcnt lgkmcnt(0).  The next group is
+// issued right after the barrier and lands during this group's 8 x 12 MFMAs.
+// Passing rows are compacted per tile in LDS (order.hip assembles the
 // reference order).
 #include "pair_common.hpp"
+
 
 namespace wld {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
-typedef __attribute__((address_space(3))) void lds_void;
 
 bool mfma_supported() { return true; }
-
-#ifdef WLD_EXP_STAMPS
-// diagnostic build only: per-phase cycle sums over all waves (s_memtime)
-__device__ unsigned long long g_stamp[8];
-__device__ __forceinline__ unsigned long long stamp() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define WLD_STAMP(v) const unsigned long long v = stamp()
-#else
-#define WLD_STAMP(v)
-#endif
 
 namespace {
 constexpr int kGroup = 8;                           // 32-sequence stages per LDS group
 constexpr int kStageCodes = 4096;                   // A0 A1 B0 B1, 1 KB each
 constexpr int kDigStage = 128;                      // digit bytes per stage: [plane][half][16] + 32 pad
-constexpr int kGroupBytes = kGroup * (kStageCodes + kDigStage);  // 33 KB; two groups in LDS
+constexpr int kDigGroup = 1024;                     // digit records of one group: one full-wave DMA
+constexpr int kGroupBytes = kGroup * kStageCodes + kDigGroup;  // two groups in LDS
+
+__host__ __device__ inline size_t digf_offset(size_t NP) { return 3 * NP; }
+__host__ __device__ inline size_t okbits_offset(size_t NP) {
+    return 3 * NP + (NP / 32 + kGroup - 1) / kGroup * kDigGroup;
+}
+// byte of the digit record of stage kb within digf
+__host__ __device__ inline size_t digf_stage(uint32_t kb) { return (size_t)(kb / kGroup) * kDigGroup + (kb % kGroup) * kDigStage; }
 }  // namespace
 
-// Weight digits of q = rint(w * 2^shift) in two layouts:
-//   planes[p*NP + k]                      (plane-major, site-major kernel path)
-//   digf[kb*128 + (2p + h)*16 + j]        (per 32-sequence stage, LDS path;
-//                                          k = 32kb + 16h + j; bytes 96..127 pad)
+// planes buffer (mfma_planes_bytes): the weight digits of q = rint(w * 2^shift)
+// in two layouts, then the site filter as bits:
+//   planes[p*NP + k]                      plane-major (site-major kernel path)
+//   digf[(kb/kGroup)*1024 + (kb%kGroup)*128 + (2p + h)*16 + j]
+//                                         per 32-sequence stage, 1 KB per group
+//                                         (LDS path; k = 32kb + 16h + j)
+//   ok_bits[g] bit i = site 64g+i passes  (site_ok, lib.rs:400-408)
+size_t mfma_planes_bytes(size_t LP, size_t NP) { return okbits_offset(NP) + LP / 64 * 8; }
+
 __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict__ w_pad, uint32_t NP, int shift,
                                                          int8_t *__restrict__ planes, int8_t *__restrict__ digf) {
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
@@ -81,8 +82,16 @@ __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict_
         const long long r = ((q + 128) & 255) - 128;  // balanced digit in [-128, 127]
         q = (q - r) / 256;
         planes[p * NP + k] = (int8_t)r;
-        digf[kb * kDigStage + (2 * p + h) * 16 + j] = (int8_t)r;
+        digf[digf_stage(kb) + (2 * p + h) * 16 + j] = (int8_t)r;
     }
+}
+
+// one wave per 64 sites
+__global__ __launch_bounds__(64) void okbits_kernel(const uint8_t *__restrict__ site_ok, uint32_t L,
+                                                     uint64_t *__restrict__ ok_bits) {
+    const uint32_t s = blockIdx.x * 64 + threadIdx.x;
+    const uint64_t m = __ballot(s < L && site_ok[s]);
+    if (threadIdx.x == 0) ok_bits[blockIdx.x] = m;
 }
 
 // codes_frag: the (site, sequence) codes in "fragment-major" order, so a
@@ -93,7 +102,7 @@ __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict_
 // Each byte is stored as a v_perm_b32 selector for its byte position j&3:
 //   12 (not major/minor -> constant 0x00), j&3 (minor), 4 + (j&3) (major),
 // so one v_perm_b32 per dword turns codes + weight digits straight into MFMA
-// operands (perm_operands below) with no mask arithmetic.
+// operands (mfma_block_sel) with no mask arithmetic.
 __global__ __launch_bounds__(256) void frag_kernel(const uint8_t *__restrict__ codes, uint32_t LP, uint32_t NP,
                                                     uint8_t *__restrict__ frag) {
     const uint32_t NKB = NP / 32;
@@ -121,22 +130,6 @@ __global__ __launch_bounds__(256) void frag_kernel(const uint8_t *__restrict__ c
 
 __device__ __forceinline__ v16i mfma_i8(v4i a, v4i b, v16i c) {
     return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
-}
-
-// Byte-wise masks from code bytes c in {0 (out), 1 (minor), 3 (major)}:
-// v_perm_b32 with zero sources returns, per selector byte, 0xFF for >= 13 and
-// 0x00 for 8..12 — a byte compare without a multiply.
-__device__ __forceinline__ v4i mask_in(v4i c) {  // c+12 in {12,13,15}: 00 FF FF
-    v4i m;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) m[e] = (int)__builtin_amdgcn_perm(0u, 0u, (unsigned)c[e] | 0x0C0C0C0Cu);
-    return m;
-}
-__device__ __forceinline__ v4i mask_maj(v4i c) {  // c+10 in {10,11,13}: 00 00 FF
-    v4i m;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) m[e] = (int)__builtin_amdgcn_perm(0u, 0u, (unsigned)c[e] + 0x0A0A0A0Au);
-    return m;
 }
 
 // 12 MFMAs of one 32-sequence block from selector-coded fragments (frag_kernel):
@@ -167,21 +160,24 @@ __device__ __forceinline__ void mfma_block_sel(v16i (&acc)[2][3][2], v4i ca, v4i
     }
 }
 
-// 12 MFMAs of one 32-sequence block for this wave's 32x32 sub-tile (site-major codes)
+// Byte-wise masks from raw code bytes c in {0 (out), 1 (minor), 3 (major)}
+// (site-major path): v_perm_b32 with zero sources returns, per selector byte,
+// 0xFF for >= 13 and 0x00 for 8..12 — a byte compare without a multiply.
+__device__ __forceinline__ v4i mask_in(v4i c) {  // c+12 in {12,13,15}: 00 FF FF
+    v4i m;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e] = (int)__builtin_amdgcn_perm(0u, 0u, (unsigned)c[e] | 0x0C0C0C0Cu);
+    return m;
+}
+__device__ __forceinline__ v4i mask_maj(v4i c) {  // c+10 in {10,11,13}: 00 00 FF
+    v4i m;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e] = (int)__builtin_amdgcn_perm(0u, 0u, (unsigned)c[e] + 0x0A0A0A0Au);
+    return m;
+}
+
+// 12 MFMAs of one 32-sequence block from raw site-major codes
 __device__ __forceinline__ void mfma_block(v16i (&acc)[2][3][2], v4i ca, v4i cb, v4i d0, v4i d1, v4i d2) {
-#ifdef WLD_EXP_NOVALU
-    {  // diagnostic: the 12 MFMAs without the operand VALU
-        const v4i dq[3] = {d0, d1, d2};
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-#pragma unroll
-            for (int x = 0; x < 2; ++x)
-#pragma unroll
-                for (int y = 0; y < 2; ++y)
-                    acc[x][p][y] = mfma_i8(x ? ca : dq[p], y ? cb : dq[(p + 1) % 3], acc[x][p][y]);
-        return;
-    }
-#endif
     const v4i one = {0x01010101, 0x01010101, 0x01010101, 0x01010101};
     const v4i b_in = cb & one;
     const v4i b_maj = (cb >> 1) & one;
@@ -199,40 +195,31 @@ __device__ __forceinline__ void mfma_block(v16i (&acc)[2][3][2], v4i ca, v4i cb,
     }
 }
 
-// DENSE: write every pair's stats (tests).  RING: fragment-major codes through
-// the double-buffered LDS groups (else site-major codes read straight into registers).
-// PREFILTER (threshold > 0): skip the f32 epilogue for pairs whose exact r2,
-// evaluated in f64 from the exact integer sums, lies clearly below the threshold.
-#ifdef WLD_EXP_LB1
-#define WLD_MFMA_WAVES_PER_SIMD 1
-#else
-#define WLD_MFMA_WAVES_PER_SIMD 2
-#endif
-template <bool DENSE, bool RING, bool PREFILTER>
-__global__ __launch_bounds__(256, WLD_MFMA_WAVES_PER_SIMD) void pair_mfma_kernel(const uint8_t *__restrict__ codes,
-                                                            const int8_t *__restrict__ planes,
-                                                            const uint8_t *__restrict__ site_ok,
-                                                            const uint32_t *__restrict__ tiles, uint32_t L,
-                                                            uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
-                                                            OrderArgs o, DenseArgs dn) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kGroupBytes];  // the only LDS object
+// One full-wave LDS-DMA (global_load_lds_dwordx4): each lane copies 16 bytes
+// from gsrc to LDS byte address lds_dst + 16*lane (lds_dst wave-uniform).  Issued
+// as inline asm so that the compiler's wait-count bookkeeping does not see it
+// (it would otherwise wait for every in-flight copy before any LDS read of the
+// other buffer): completion is ordered only by the kernel's own protocol —
+// s_waitcnt vmcnt(0) by every issuing wave, then a barrier, then the reads.
+// M0 is saved and restored inside the statement (it is compiler-reserved).
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+}
 
-    WLD_STAMP(t0);
-    const uint32_t tile = tiles[blockIdx.x];
-    const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
-    const uint32_t a0 = ta * kTile, b0 = tb * kTile;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const uint32_t wa = wave >> 1, wb = wave & 1;
-    const uint32_t r = lane & 31, h = lane >> 5;
-    const uint32_t NKB = NP / 32;
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
 
-    // site filter of the tile's 64 a and 64 b sites as wave-uniform bit masks
-    // (loaded once, ahead of the main loop, instead of per pair in the epilogue)
-    const uint64_t okA = __ballot(a0 + lane < L && site_ok[a0 + lane]);
-    const uint64_t okB = __ballot(b0 + lane < L && site_ok[b0 + lane]);
-
-    v16i acc[2][3][2];
+__device__ __forceinline__ void zero_acc(v16i (&acc)[2][3][2]) {
 #pragma unroll
     for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -241,120 +228,23 @@ __global__ __launch_bounds__(256, WLD_MFMA_WAVES_PER_SIMD) void pair_mfma_kernel
             for (int y = 0; y < 2; ++y)
 #pragma unroll
                 for (int e = 0; e < 16; ++e) acc[x][p][y][e] = 0;
+}
 
-    if constexpr (RING) {
-        // this wave's code block per stage (A0/A1/B0/B1); wave 0 also the digit records
-        const uint32_t g_src = wave < 2 ? (a0 >> 5) + wave : (b0 >> 5) + (wave - 2);
-        const uint8_t *src = codes + ((size_t)g_src * NKB * 64 + lane) * 16;
-        const int8_t *dsrc = planes + 3 * (size_t)NP + lane * 16;  // digf
-        const uint32_t n_groups = (NKB + kGroup - 1) / kGroup;
-#ifdef WLD_EXP_STAMPS
-        unsigned long long t1 = 0;
-#endif
-        auto issue = [&](uint32_t grp) {
-            uint8_t *gb = smem + (grp & 1) * kGroupBytes;
-            const uint32_t kb0 = grp * kGroup;
-#pragma unroll
-            for (int st = 0; st < kGroup; ++st)
-                if (kb0 + st < NKB)
-                    __builtin_amdgcn_global_load_lds(src + (size_t)(kb0 + st) * 1024,
-                                                     (lds_void *)(gb + st * kStageCodes + wave * 1024), 16, 0, 0);
-            if (wave == 0)  // digits of 8 stages = 1 KB (allocation padded to whole groups)
-                __builtin_amdgcn_global_load_lds(dsrc + (size_t)kb0 * kDigStage,
-                                                 (lds_void *)(gb + kGroup * kStageCodes), 16, 0, 0);
-        };
-        issue(0);
-        for (uint32_t grp = 0; grp < n_groups; ++grp) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of group grp landed
-            __builtin_amdgcn_s_barrier();                     // ... and every other wave's; group grp-1 is free
-            asm volatile("" ::: "memory");
-#ifdef WLD_EXP_STAMPS
-            if (grp == 0) t1 = stamp();
-#endif
-#ifdef WLD_EXP_NOLOAD
-            if (grp + 1 < n_groups && grp == 0) issue(grp + 1);  // diagnostic: no streaming
-#else
-            if (grp + 1 < n_groups) issue(grp + 1);
-#endif
-            const uint8_t *gb = smem + (grp & 1) * kGroupBytes;
-            const uint32_t n_st = min((uint32_t)kGroup, NKB - grp * kGroup);
-#ifdef WLD_EXP_PIPE
-            auto ld = [&](uint32_t st, v4i &ca, v4i &cb, v4i &d0, v4i &d1, v4i &d2) {
-                const uint8_t *sc = gb + st * kStageCodes;
-                const uint8_t *sd = gb + kGroup * kStageCodes + st * kDigStage + h * 16;
-                ca = *reinterpret_cast<const v4i *>(sc + wa * 1024 + lane * 16);
-                cb = *reinterpret_cast<const v4i *>(sc + 2048 + wb * 1024 + lane * 16);
-                d0 = *reinterpret_cast<const v4i *>(sd);
-                d1 = *reinterpret_cast<const v4i *>(sd + 32);
-                d2 = *reinterpret_cast<const v4i *>(sd + 64);
-            };
-            v4i ca, cb, d0, d1, d2;
-            ld(0, ca, cb, d0, d1, d2);
-            for (uint32_t st = 0; st < n_st; ++st) {
-                v4i na = ca, nb = cb, n0 = d0, n1 = d1, n2 = d2;
-                if (st + 1 < n_st) ld(st + 1, na, nb, n0, n1, n2);
-                mfma_block_sel(acc, ca, cb, d0, d1, d2);
-                ca = na; cb = nb; d0 = n0; d1 = n1; d2 = n2;
-            }
-#else
-#ifdef WLD_EXP_PURE
-            for (uint32_t st = 0; st < n_st; ++st) {
-                v4i ca = {(int)lane, (int)st, (int)grp, 3}, cb = {(int)(lane ^ 5), 1, 2, (int)st};
-                asm volatile("" : "+v"(ca), "+v"(cb));
-                mfma_block(acc, ca, cb, ca, cb, ca);
-            }
-            if (false)
-#endif
-            for (uint32_t st = 0; st < n_st; ++st) {
-                const uint8_t *sc = gb + st * kStageCodes;
-                const uint8_t *sd = gb + kGroup * kStageCodes + st * kDigStage + h * 16;
-                const v4i ca = *reinterpret_cast<const v4i *>(sc + wa * 1024 + lane * 16);
-                const v4i cb = *reinterpret_cast<const v4i *>(sc + 2048 + wb * 1024 + lane * 16);
-                const v4i d0 = *reinterpret_cast<const v4i *>(sd);
-                const v4i d1 = *reinterpret_cast<const v4i *>(sd + 32);
-                const v4i d2 = *reinterpret_cast<const v4i *>(sd + 64);
-#ifdef WLD_EXP_EARLYD2
-                asm volatile("" ::"v"(d2[0]), "v"(d2[1]), "v"(d2[2]), "v"(d2[3]));
-#endif
-                mfma_block_sel(acc, ca, cb, d0, d1, d2);
-#ifdef WLD_EXP_SGB
-                __builtin_amdgcn_sched_group_barrier(0x100, 5, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
-#pragma unroll
-                for (int q = 0; q < 10; ++q) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-                }
-                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-#endif
-            }
-#endif
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of group grp done before the barrier
-        }
-        __syncthreads();  // LDS reads done before the compaction reuses smem
-#ifdef WLD_EXP_STAMPS
-        WLD_STAMP(t2);
-        if (lane == 0) {
-            atomicAdd(&g_stamp[0], t1 - t0);
-            atomicAdd(&g_stamp[1], t2 - t1);
-            atomicAdd(&g_stamp[5], 1ull);
-        }
-#endif
-    } else {
-        const uint8_t *pa = codes + (size_t)(a0 + 32 * wa + r) * NP + 16 * h;
-        const uint8_t *pb = codes + (size_t)(b0 + 32 * wb + r) * NP + 16 * h;
-        const int8_t *pd = planes + 16 * h;
-        for (uint32_t k0 = 0; k0 < NP; k0 += 32) {
-            const v4i ca = *reinterpret_cast<const v4i *>(pa + k0);
-            const v4i cb = *reinterpret_cast<const v4i *>(pb + k0);
-            const v4i d0 = *reinterpret_cast<const v4i *>(pd + k0);
-            const v4i d1 = *reinterpret_cast<const v4i *>(pd + NP + k0);
-            const v4i d2 = *reinterpret_cast<const v4i *>(pd + 2 * NP + k0);
-            mfma_block(acc, ca, cb, d0, d1, d2);
-        }
-    }
-
-    // ---- epilogue: lane holds b = b0+32wb+r and 16 a rows -------------------
+// Epilogue of one 64x64 tile.  The lane holds b = b0 + 32wb + r and 16 a rows
+// (MFMA C layout: row (i&3) + 8(i>>2) + 4h).  DENSE writes every pair's stats
+// (tests); otherwise passing pairs are compacted through the tile's 64x64
+// pass-bit matrix in LDS into staging, with per-(a, b-tile) segment counts and
+// offsets for order.hip.  PREFILTER (threshold > 0) skips the f32 epilogue for
+// pairs whose exact r2, evaluated in f64 from the exact sums, lies clearly
+// below the threshold.
+template <bool DENSE, bool PREFILTER>
+__device__ __forceinline__ void tile_epilogue(const v16i (&acc)[2][3][2], uint32_t ta, uint32_t tb, uint32_t tid,
+                                              uint64_t okA, uint64_t okB, uint32_t L, uint32_t n_chunk_rows,
+                                              float thr, int shift, const OrderArgs &o, const DenseArgs &dn,
+                                              unsigned long long *sBits, uint32_t *sRowBase) {
+    const uint32_t wave = tid >> 6, lane = tid & 63;
+    const uint32_t wa = wave >> 1, wb = wave & 1, r = lane & 31, h = lane >> 5;
+    const uint32_t a0 = ta * kTile, b0 = tb * kTile;
     const double scale = ldexp(1.0, -shift);
     const uint32_t b_local = 32 * wb + r;
     const uint32_t b = b0 + b_local;
@@ -413,13 +303,8 @@ __global__ __launch_bounds__(256, WLD_MFMA_WAVES_PER_SIMD) void pair_mfma_kernel
         }
     }
     if constexpr (DENSE) return;
-#ifdef WLD_EXP_STAMPS
-    WLD_STAMP(t3);
-#endif
 
     // ---- compaction: a 64x64 pass-bit matrix in LDS, rows in b order ----------
-    unsigned long long *sBits = reinterpret_cast<unsigned long long *>(smem);  // [64]
-    uint32_t *sRowBase = reinterpret_cast<uint32_t *>(smem + kTile * 8);      // [64]
     if (tid < kTile) sBits[tid] = 0ull;
     __syncthreads();
     if (pass) {
@@ -464,35 +349,115 @@ __global__ __launch_bounds__(256, WLD_MFMA_WAVES_PER_SIMD) void pair_mfma_kernel
             }
         }
     }
-#ifdef WLD_EXP_STAMPS
-    WLD_STAMP(t4);
-    if (lane == 0) {
-        atomicAdd(&g_stamp[2], t3 - t0);
-        atomicAdd(&g_stamp[3], t4 - t3);
+}
+
+// LDS-streaming kernel over fragment-major, selector-coded codes: one 64x64
+// tile per workgroup.  (An XCD-contiguous block->tile remap measured no gain:
+// the 41 MB code copy of BASELINE config 4 is served from L2/MALL either way.)
+template <bool DENSE, bool PREFILTER>
+__global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__restrict__ frag,
+                                                            const int8_t *__restrict__ planes,
+                                                            const uint64_t *__restrict__ ok_bits,
+                                                            const uint32_t *__restrict__ tiles, uint32_t L,
+                                                            uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
+                                                            OrderArgs o, DenseArgs dn) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kGroupBytes];  // operand groups (DMA targets)
+    __shared__ unsigned long long sBits[kTile];                              // compaction (never a DMA target)
+    __shared__ uint32_t sRowBase[kTile];
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const uint32_t wa = wave >> 1, wb = wave & 1, h = lane >> 5;
+    const uint32_t NKB = NP / 32;
+    const uint32_t n_groups = (NKB + kGroup - 1) / kGroup;
+
+    const uint32_t tile = tiles[blockIdx.x];
+    const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
+
+    // this wave's 1 KB code block per stage: A0/A1 (a sites), B0/B1 (b sites)
+    const uint32_t g = wave < 2 ? 2 * ta + wave : 2 * tb + (wave - 2);
+    const uint8_t *src = frag + (size_t)g * NKB * 1024;  // wave-uniform
+    const int8_t *digf = planes + digf_offset(NP);
+    const uint32_t smem_lds = lds_addr(smem);
+    auto issue = [&](uint32_t grp, uint32_t buf) {
+        const uint32_t gb = smem_lds + buf * kGroupBytes;
+        const uint32_t kb0 = grp * kGroup;
+        const uint8_t *base = src + (size_t)kb0 * 1024;
+        const uint32_t lane16 = lane * 16;
+#pragma unroll
+        for (int st = 0; st < kGroup; ++st)
+            if (kb0 + st < NKB) glds16(base + (uint32_t)(st * 1024) + lane16, gb + st * kStageCodes + wave * 1024);
+        if (wave == 0)  // digit records of the group = 1 KB (allocation padded to whole groups)
+            glds16(digf + (size_t)grp * kDigGroup + lane16, gb + kGroup * kStageCodes);
+    };
+
+    issue(0, 0);
+    const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
+    v16i acc[2][3][2];
+    zero_acc(acc);
+    uint32_t buf = 0;
+    for (uint32_t grp = 0; grp < n_groups; ++grp) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this group landed
+        __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
+        asm volatile("" ::: "memory");
+        if (grp + 1 < n_groups) issue(grp + 1, buf ^ 1);
+        const uint8_t *gb = smem + buf * kGroupBytes;
+        const uint32_t n_st = min((uint32_t)kGroup, NKB - grp * kGroup);
+        for (uint32_t st = 0; st < n_st; ++st) {
+            const uint8_t *sc = gb + st * kStageCodes;
+            const uint8_t *sd = gb + kGroup * kStageCodes + st * kDigStage + h * 16;
+            const v4i ca = *reinterpret_cast<const v4i *>(sc + wa * 1024 + lane * 16);
+            const v4i cb = *reinterpret_cast<const v4i *>(sc + 2048 + wb * 1024 + lane * 16);
+            const v4i d0 = *reinterpret_cast<const v4i *>(sd);
+            const v4i d1 = *reinterpret_cast<const v4i *>(sd + 32);
+            const v4i d2 = *reinterpret_cast<const v4i *>(sd + 64);
+            mfma_block_sel(acc, ca, cb, d0, d1, d2);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
+        buf ^= 1;
     }
-#endif
+    tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, shift, o, dn, sBits, sRowBase);
 }
 
-#ifdef WLD_EXP_STAMPS
-extern "C" int wld_debug_stamps(unsigned long long *out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp), sizeof(g_stamp)) != hipSuccess) return -1;
-    if (reset) {
-        unsigned long long z[8] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z)) != hipSuccess) return -1;
+// Site-major variant (one tile per workgroup, codes read straight into
+// registers): the reference for the LDS path's race screen and the
+// WLD_MFMA_LAYOUT=rows experiments.
+template <bool DENSE, bool PREFILTER>
+__global__ __launch_bounds__(256, 2) void pair_mfma_rows_kernel(const uint8_t *__restrict__ codes,
+                                                                 const int8_t *__restrict__ planes,
+                                                                 const uint64_t *__restrict__ ok_bits,
+                                                                 const uint32_t *__restrict__ tiles, uint32_t L,
+                                                                 uint32_t NP, uint32_t n_chunk_rows, float thr,
+                                                                 int shift, OrderArgs o, DenseArgs dn) {
+    __shared__ unsigned long long sBits[kTile];
+    __shared__ uint32_t sRowBase[kTile];
+    const uint32_t tile = tiles[blockIdx.x];
+    const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t wa = wave >> 1, wb = wave & 1, r = lane & 31, h = lane >> 5;
+    v16i acc[2][3][2];
+    zero_acc(acc);
+    const uint8_t *pa = codes + (size_t)(ta * kTile + 32 * wa + r) * NP + 16 * h;
+    const uint8_t *pb = codes + (size_t)(tb * kTile + 32 * wb + r) * NP + 16 * h;
+    const int8_t *pd = planes + 16 * h;
+    for (uint32_t k0 = 0; k0 < NP; k0 += 32) {
+        const v4i ca = *reinterpret_cast<const v4i *>(pa + k0);
+        const v4i cb = *reinterpret_cast<const v4i *>(pb + k0);
+        const v4i d0 = *reinterpret_cast<const v4i *>(pd + k0);
+        const v4i d1 = *reinterpret_cast<const v4i *>(pd + NP + k0);
+        const v4i d2 = *reinterpret_cast<const v4i *>(pd + 2 * NP + k0);
+        mfma_block(acc, ca, cb, d0, d1, d2);
     }
-    return 0;
-}
-#endif
-
-size_t mfma_planes_bytes(size_t NP) {
-    const size_t n_groups = (NP / 32 + kGroup - 1) / kGroup;
-    return 3 * NP + n_groups * kGroup * kDigStage;  // digit records padded to whole groups
+    tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, ok_bits[ta], ok_bits[tb], L, n_chunk_rows, thr, shift, o, dn,
+                                    sBits, sRowBase);
 }
 
-void launch_mfma_prep(const uint8_t *, const float *w_pad, size_t, size_t NP, int shift, int8_t *planes,
-                      hipStream_t s) {
+void launch_mfma_prep(const uint8_t *site_ok, const float *w_pad, size_t L, size_t LP, size_t NP, int shift,
+                      int8_t *planes, hipStream_t s) {
     hipLaunchKernelGGL(mfma_prep_kernel, dim3((unsigned)((NP + 255) / 256)), dim3(256), 0, s, w_pad, (uint32_t)NP,
-                       shift, planes, planes + 3 * NP);
+                       shift, planes, planes + digf_offset(NP));
+    hipLaunchKernelGGL(okbits_kernel, dim3((unsigned)(LP / 64)), dim3(64), 0, s, site_ok, (uint32_t)L,
+                       reinterpret_cast<uint64_t *>(planes + okbits_offset(NP)));
 }
 
 void launch_frag(const uint8_t *codes, size_t LP, size_t NP, uint8_t *frag, hipStream_t s) {
@@ -501,33 +466,32 @@ void launch_frag(const uint8_t *codes, size_t LP, size_t NP, uint8_t *frag, hipS
                        (uint32_t)NP, frag);
 }
 
-void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const int8_t *wplanes, const uint8_t *site_ok,
-                      const uint32_t *tiles, uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows,
-                      float thr, int shift, bool prefilter, const OrderArgs &o, const DenseArgs *dense,
-                      hipStream_t s) {
-    const DenseArgs none{nullptr, nullptr, nullptr, nullptr};
+void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const int8_t *wplanes, const uint32_t *tiles,
+                      uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
+                      bool prefilter, const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
+    const DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
+    const uint64_t *ok_bits = reinterpret_cast<const uint64_t *>(wplanes + okbits_offset(NP));
     const dim3 g(n_tiles), b(256);
-    if (dense) {
-        if (frag)
-            hipLaunchKernelGGL((pair_mfma_kernel<true, true, false>), g, b, 0, s, frag, wplanes, site_ok, tiles, L, NP,
-                               n_chunk_rows, thr, shift, o, *dense);
+    if (frag) {
+        if (dense)
+            hipLaunchKernelGGL((pair_mfma_kernel<true, false>), g, b, 0, s, frag, wplanes, ok_bits, tiles, L, NP,
+                               n_chunk_rows, thr, shift, o, dn);
+        else if (prefilter)
+            hipLaunchKernelGGL((pair_mfma_kernel<false, true>), g, b, 0, s, frag, wplanes, ok_bits, tiles, L, NP,
+                               n_chunk_rows, thr, shift, o, dn);
         else
-            hipLaunchKernelGGL((pair_mfma_kernel<true, false, false>), g, b, 0, s, codes, wplanes, site_ok, tiles, L,
-                               NP, n_chunk_rows, thr, shift, o, *dense);
-    } else if (frag) {
-        if (prefilter)
-            hipLaunchKernelGGL((pair_mfma_kernel<false, true, true>), g, b, 0, s, frag, wplanes, site_ok, tiles, L, NP,
-                               n_chunk_rows, thr, shift, o, none);
-        else
-            hipLaunchKernelGGL((pair_mfma_kernel<false, true, false>), g, b, 0, s, frag, wplanes, site_ok, tiles, L,
-                               NP, n_chunk_rows, thr, shift, o, none);
+            hipLaunchKernelGGL((pair_mfma_kernel<false, false>), g, b, 0, s, frag, wplanes, ok_bits, tiles, L, NP,
+                               n_chunk_rows, thr, shift, o, dn);
     } else {
-        if (prefilter)
-            hipLaunchKernelGGL((pair_mfma_kernel<false, false, true>), g, b, 0, s, codes, wplanes, site_ok, tiles, L,
-                               NP, n_chunk_rows, thr, shift, o, none);
+        if (dense)
+            hipLaunchKernelGGL((pair_mfma_rows_kernel<true, false>), g, b, 0, s, codes, wplanes, ok_bits, tiles, L,
+                               NP, n_chunk_rows, thr, shift, o, dn);
+        else if (prefilter)
+            hipLaunchKernelGGL((pair_mfma_rows_kernel<false, true>), g, b, 0, s, codes, wplanes, ok_bits, tiles, L,
+                               NP, n_chunk_rows, thr, shift, o, dn);
         else
-            hipLaunchKernelGGL((pair_mfma_kernel<false, false, false>), g, b, 0, s, codes, wplanes, site_ok, tiles, L,
-                               NP, n_chunk_rows, thr, shift, o, none);
+            hipLaunchKernelGGL((pair_mfma_rows_kernel<false, false>), g, b, 0, s, codes, wplanes, ok_bits, tiles, L,
+                               NP, n_chunk_rows, thr, shift, o, dn);
     }
 }
 
