@@ -68,9 +68,10 @@ def chunk_pairs(L, i):
     return sa * (sa - 1) // 2 if row == col else sa * sb
 
 
-def cpu_baseline(buf, w, thr, target_s=15.0):
-    """Times the oracle (C restatement of the lib.rs simd path) on the first
-    chunks of the same workload in triu order, sized to ~target_s seconds."""
+def cpu_baseline(buf, w, thr, target_s=15.0, max_s=30.0):
+    """Times the oracle (C restatement of the lib.rs simd path) on the same
+    workload: all of it when that fits in max_s seconds of CPU work, else the
+    first chunks in triu order, sized to ~target_s seconds."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import _oracle as O  # checker / baseline only
 
@@ -84,19 +85,26 @@ def cpu_baseline(buf, w, thr, target_s=15.0):
         r = O.all_pairs(buf, w, thr, n_threads=threads, chunk_lo=0, chunk_hi=k)
         return r["pairs"], time.perf_counter() - t0
 
-    k = min(nchunks, max(threads, 4))
+    # calibrate on ~1/16 of the chunks (enough work to amortise thread start-up)
+    k = min(nchunks, max(4 * threads, nchunks // 16))
     p, t = run(k)
     rate = p / max(t, 1e-9)
-    want = rate * target_s
-    k2, acc = 0, 0
-    while k2 < nchunks and acc < want:
-        acc += chunk_pairs(L, k2)
-        k2 += 1
-    p, t = run(max(k2, 1))
+    total = L * (L - 1) // 2
+    if total / rate <= max_s:
+        k2 = nchunks
+        what = "the whole workload (%d reference chunks)" % nchunks
+    else:
+        want = rate * target_s
+        k2, acc = 0, 0
+        while k2 < nchunks and acc < want:
+            acc += chunk_pairs(L, k2)
+            k2 += 1
+        k2 = max(k2, 1)
+        what = "the first %d of %d reference chunks (256x256, triu order) of the same workload" % (k2, nchunks)
+    p, t = run(k2)
     return {"value": p / t, "unit": "site-pairs/s", "cores": threads, "kind": "port",
-            "sample": "first %d of %d reference chunks (256x256, triu order) of the same workload = %d pairs in "
-                      "%.1f s; C restatement of the lib.rs simd path (8-lane f32, rayon-style chunk scheduling), "
-                      "gcc -O3 -march=x86-64-v3" % (max(k2, 1), nchunks, p, t)}
+            "sample": "%s = %d pairs in %.1f s; C restatement of the lib.rs simd path (8-lane f32, rayon-style "
+                      "chunk scheduling), gcc -O3 -march=x86-64-v3" % (what, p, t)}
 
 
 def load_traffic(config, kernel):
@@ -112,8 +120,8 @@ def load_traffic(config, kernel):
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)  # the clock ramps over the first launches
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--kernel", default="auto", choices=["auto", "valu", "mfma"])
     ap.add_argument("--no-cpu-baseline", action="store_true")

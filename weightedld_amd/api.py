@@ -202,7 +202,8 @@ class Context:
 
     def __init__(self, device=0, kernel=KERNEL_AUTO):
         h = ctypes.c_void_p()
-        check(lib().wld_create(device, ctypes.byref(h)), "wld_create")
+        self._lib = lib()  # kept: module globals may be gone when __del__ runs at exit
+        check(self._lib.wld_create(device, ctypes.byref(h)), "wld_create")
         self._h = h
         self.device = device
         if kernel != KERNEL_AUTO:
@@ -210,7 +211,7 @@ class Context:
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
-            lib().wld_destroy(self._h)
+            self._lib.wld_destroy(self._h)
             self._h = None
 
     __del__ = close

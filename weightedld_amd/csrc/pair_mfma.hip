@@ -219,6 +219,21 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
 }
 
+#ifdef WLD_EXP_STAMPS
+// diagnostic build only: per-tile cycle stamps of wave 0 (start, loop end, epilogue end)
+__device__ unsigned long long g_stamps[3u << 18];
+__device__ __forceinline__ unsigned long long stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+extern "C" int wld_debug_stamps_copy(unsigned long long *out, unsigned n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), (size_t)n * 3 * 8) == hipSuccess ? 0 : -1;
+}
+#endif
+
 __device__ __forceinline__ void zero_acc(v16i (&acc)[2][3][2]) {
 #pragma unroll
     for (int x = 0; x < 2; ++x)
@@ -371,6 +386,9 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
     const uint32_t NKB = NP / 32;
     const uint32_t n_groups = (NKB + kGroup - 1) / kGroup;
 
+#ifdef WLD_EXP_STAMPS
+    const unsigned long long ts0 = stamp();
+#endif
     const uint32_t tile = tiles[blockIdx.x];
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
 
@@ -416,7 +434,18 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
         buf ^= 1;
     }
+#ifdef WLD_EXP_STAMPS
+    const unsigned long long ts1 = stamp();
+#endif
     tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, shift, o, dn, sBits, sRowBase);
+#ifdef WLD_EXP_STAMPS
+    const unsigned long long ts2 = stamp();
+    if (tid == 0 && blockIdx.x < (1u << 18)) {
+        g_stamps[3 * blockIdx.x] = ts0;
+        g_stamps[3 * blockIdx.x + 1] = ts1;
+        g_stamps[3 * blockIdx.x + 2] = ts2;
+    }
+#endif
 }
 
 // Site-major variant (one tile per workgroup, codes read straight into
