@@ -179,6 +179,55 @@ def test_dense_nonfinite_weights_valu(ctxs):
     dense_check(ctx, buf, w)
 
 
+@pytest.mark.parametrize("kern", KERNELS)
+def test_dense_vs_oracle_many_sequences(ctxs, kern):
+    # BASELINE config 5's sequence count: 5000 -> 158 32-sequence stages,
+    # 20 LDS groups with a partial last group
+    ctx = _ctx(ctxs, kern)
+    buf = synth(150, 5000, 21)
+    import weightedld_amd as W
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ctx.load(buf, w)
+    dense_check(ctx, buf, w)
+
+
+@pytest.mark.parametrize("kern", KERNELS)
+def test_dense_mixed_sign_weights(ctxs, kern):
+    # Weights are any finite f32 in lib.rs; the MFMA fixed point is signed
+    # (negative balanced digits).  ~10% small negative weights keep the sums
+    # well-conditioned.  (With sums that cancel to ~0, D ~ 1/T^2 amplifies any
+    # f32 or fixed-point rounding and no two summation orders agree to 1e-5 —
+    # the reference's 8-lane f32 sums included)
+    ctx = _ctx(ctxs, kern)
+    buf = synth(120, 333, 17)
+    rng = np.random.default_rng(9)
+    w = (0.5 + 0.5 * rng.random(333)).astype(np.float32)
+    neg = rng.random(333) < 0.1
+    w[neg] = -(0.1 + 0.2 * rng.random(int(neg.sum()))).astype(np.float32)
+    ctx.load(buf, w)
+    dense_check(ctx, buf, w)
+
+
+def test_auto_kernel_choice(W):
+    # AUTO: MFMA for Henikoff-like weights, VALU when the dynamic range exceeds
+    # 2^10 (fixed point could lose small weights) or a weight is non-finite
+    buf = synth(200, 100, 23)
+    ctx = W.Context(0, W.KERNEL_AUTO)
+    w = np.random.default_rng(1).random(100).astype(np.float32) + 0.5
+    ctx.load(buf, w)
+    assert ctx.stats()["kernel"] == W.KERNEL_MFMA
+    w2 = w.copy()
+    w2[3] = 1e-6
+    ctx.load(buf, w2)
+    assert ctx.stats()["kernel"] == W.KERNEL_VALU
+    ctx.run(0.0)
+    compare_rows(ctx.rows(), O.all_pairs(buf, w2, 0.0), 0.0, buf=buf, w=w2)
+    w3 = w.copy()
+    w3[7] = np.inf
+    ctx.load(buf, w3)
+    assert ctx.stats()["kernel"] == W.KERNEL_VALU
+
+
 # ------------------------------------------------------------------ ordered rows
 @pytest.mark.parametrize("kern", KERNELS)
 @pytest.mark.parametrize("L,N,thr", [(1, 10, 0.0), (2, 10, 0.0), (255, 64, 0.0), (256, 100, 0.05), (257, 100, 0.0),
@@ -382,3 +431,32 @@ def test_mfma_lds_pipeline_race_screen(W, monkeypatch):
         assert n == n_ref
         got = wdist.pack_rows_device(ctx, n, dev)
         assert torch.equal(got, ref)
+
+
+def test_config5_full_size_properties(W):
+    """BASELINE config 5 at one GPU: N=5000 x L=50000 (~1.25e9 pairs), thr 0.05.
+    Size-independent properties of the emitted rows plus an exact oracle check
+    of a 400-site window at thr -inf."""
+    L, N = 50000, 5000
+    buf = synth(L, N, 55)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ctx = W.Context(0, W.KERNEL_MFMA)
+    ctx.load(buf, w)
+    n = ctx.run(0.05)
+    st = ctx.stats()
+    assert st["pairs"] == L * (L - 1) // 2
+    store = ctx.rows()
+    assert len(store) == n
+    if n:
+        assert np.all(store.r2 > 0.05)
+        assert np.all(store.site_a < store.site_b)
+        nchunk = (L + 255) // 256
+        ca, cb = store.site_a.astype(np.int64) // 256, store.site_b.astype(np.int64) // 256
+        rf = nchunk - 1 - ca
+        lin = rf * (rf + 1) // 2 + (cb - ca)
+        key = lin * (L * L) + store.site_a.astype(np.int64) * L + store.site_b
+        assert np.all(np.diff(key) > 0)
+    sub = buf[31000:31400]
+    ctx.load(sub, w)
+    ctx.run(float("-inf"))
+    compare_rows(ctx.rows(), O.all_pairs(sub, w, float("-inf")), float("-inf"), buf=sub, w=w)
