@@ -172,6 +172,7 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     c->kernel = k;
     c->safe = !finite;
     c->shift = 0;
+    c->use_frag = false;
     if (k == WLD_KERNEL_MFMA) {
         c->shift = weight_shift(maxabs);
         WLD_TRY(ensure(c->planes, mfma_planes_bytes(c->LP, c->NP)));

@@ -221,7 +221,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
 
 #ifdef WLD_EXP_STAMPS
 // diagnostic build only: per-tile cycle stamps of wave 0 (start, loop end, epilogue end)
-__device__ unsigned long long g_stamps[3u << 18];
+__device__ unsigned long long g_stamps[4u << 18];
 __device__ __forceinline__ unsigned long long stamp() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);
@@ -230,7 +230,7 @@ __device__ __forceinline__ unsigned long long stamp() {
     return t;
 }
 extern "C" int wld_debug_stamps_copy(unsigned long long *out, unsigned n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), (size_t)n * 3 * 8) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), (size_t)n * 4 * 8) == hipSuccess ? 0 : -1;
 }
 #endif
 
@@ -245,6 +245,32 @@ __device__ __forceinline__ void zero_acc(v16i (&acc)[2][3][2]) {
                 for (int e = 0; e < 16; ++e) acc[x][p][y][e] = 0;
 }
 
+// Reference epilogue of one pair from its exact sums (fixed-point units):
+// the optional exact-algebra prefilter, then lib.rs:482-520 in f32.  Returns
+// true when the pair passes (valid and r2 > thr, lib.rs:660); d/dp/r2 are
+// written when the f32 epilogue ran (always for DENSE).
+template <bool DENSE, bool PREFILTER>
+__device__ __forceinline__ bool pair_eval(double T, double SA, double SB, double SAB, bool valid, float thr,
+                                          double scale, float &d, float &dp, float &r2) {
+    if constexpr (!DENSE) {
+        if (!valid) return false;
+        if constexpr (PREFILTER) {
+            // Exact algebra: d = PA*PB - P(AB) and r2 = d^2/(PA Pa PB Pb) become
+            // r2 = (SA*SB - SAB*T)^2 / (SA (T-SA) SB (T-SB)) on the exact sums.
+            // Evaluated in f64 (|err| ~1e-16 relative); pairs more than
+            // 1e-5 + 1e-4|thr| below the threshold cannot pass the f32 epilogue,
+            // so they skip it.  Everything else (and den <= 0, the NaN/inf
+            // cases) takes the full reference epilogue.
+            const double num = SA * SB - SAB * T;
+            const double den = SA * (T - SA) * SB * (T - SB);
+            const double cut = (double)thr - (1e-5 + 1e-4 * fabs((double)thr));
+            if (den > 0.0 && num * num < cut * den) return false;
+        }
+    }
+    ld_epilogue((float)(T * scale), (float)(SA * scale), (float)(SB * scale), (float)(SAB * scale), d, dp, r2);
+    return valid && r2 > thr;
+}
+
 // Epilogue of one 64x64 tile.  The lane holds b = b0 + 32wb + r and 16 a rows
 // (MFMA C layout: row (i&3) + 8(i>>2) + 4h).  DENSE writes every pair's stats
 // (tests); otherwise passing pairs are compacted through the tile's 64x64
@@ -255,8 +281,9 @@ __device__ __forceinline__ void zero_acc(v16i (&acc)[2][3][2]) {
 template <bool DENSE, bool PREFILTER>
 __device__ __forceinline__ void tile_epilogue(const v16i (&acc)[2][3][2], uint32_t ta, uint32_t tb, uint32_t tid,
                                               uint64_t okA, uint64_t okB, uint32_t L, uint32_t n_chunk_rows,
-                                              float thr, int shift, const OrderArgs &o, const DenseArgs &dn,
-                                              unsigned long long *sBits, uint32_t *sRowBase) {
+                                              float thr, int shift, bool narrow, const OrderArgs &o,
+                                              const DenseArgs &dn, unsigned long long *sBits,
+                                              uint32_t *sRowBase) {
     const uint32_t wave = tid >> 6, lane = tid & 63;
     const uint32_t wa = wave >> 1, wb = wave & 1, r = lane & 31, h = lane >> 5;
     const uint32_t a0 = ta * kTile, b0 = tb * kTile;
@@ -271,37 +298,24 @@ __device__ __forceinline__ void tile_epilogue(const v16i (&acc)[2][3][2], uint32
         const uint32_t a_local = 32 * wa + (i & 3) + 8 * (i >> 2) + 4 * h;
         const uint32_t a = a0 + a_local;
         const bool valid = okb && a < b && ((okA >> a_local) & 1);
-        // S = acc_0 + 2^8 acc_1 + 2^16 acc_2: integers below 2^48, exact in f64
+        // S = acc_0 + 2^8 acc_1 + 2^16 acc_2: integers below 2^48, exact in f64.
+        // |acc_p| <= 128 NP, so acc_1 + 2^8 acc_2 is exact in int32 while
+        // 32896 NP < 2^31 (NP <= 65024): one int op, two conversions, one FMA.
         double S[2][2];
 #pragma unroll
         for (int x = 0; x < 2; ++x)
 #pragma unroll
-            for (int y = 0; y < 2; ++y)
-                S[x][y] = fma(65536.0, (double)acc[x][2][y][i],
-                              fma(256.0, (double)acc[x][1][y][i], (double)acc[x][0][y][i]));
-        if constexpr (!DENSE) {
-            if (!valid) continue;
-            if constexpr (PREFILTER) {
-                // Exact algebra: d = PA*PB - P(AB) and r2 = d^2/(PA Pa PB Pb) become
-                // r2 = (SA*SB - SAB*T)^2 / (SA (T-SA) SB (T-SB)) on the exact sums.
-                // Evaluated in f64 (|err| ~1e-16 relative); pairs more than
-                // 1e-5 + 1e-4|thr| below the threshold cannot pass the f32
-                // epilogue, so they skip it.  Everything else (and den <= 0,
-                // the NaN/inf cases) takes the full reference epilogue.
-                const double T = S[0][0], SA = S[1][0], SB = S[0][1], SAB = S[1][1];
-                const double num = SA * SB - SAB * T;
-                const double den = SA * (T - SA) * SB * (T - SB);
-                const double cut = (double)thr - (1e-5 + 1e-4 * fabs((double)thr));
-                if (den > 0.0 && num * num < cut * den) continue;
+            for (int y = 0; y < 2; ++y) {
+                if (narrow) {
+                    const int hi = acc[x][1][y][i] + acc[x][2][y][i] * 256;
+                    S[x][y] = fma(256.0, (double)hi, (double)acc[x][0][y][i]);
+                } else {
+                    S[x][y] = fma(65536.0, (double)acc[x][2][y][i],
+                                  fma(256.0, (double)acc[x][1][y][i], (double)acc[x][0][y][i]));
+                }
             }
-        }
-        float s[2][2];
-#pragma unroll
-        for (int x = 0; x < 2; ++x)
-#pragma unroll
-            for (int y = 0; y < 2; ++y) s[x][y] = (float)(S[x][y] * scale);
-        float d, dp, r2;
-        ld_epilogue(s[0][0], s[1][0], s[0][1], s[1][1], d, dp, r2);
+        float d = 0.f, dp = 0.f, r2 = 0.f;
+        const bool ok = pair_eval<DENSE, PREFILTER>(S[0][0], S[1][0], S[0][1], S[1][1], valid, thr, scale, d, dp, r2);
         res[i][0] = d;
         res[i][1] = dp;
         res[i][2] = r2;
@@ -314,7 +328,7 @@ __device__ __forceinline__ void tile_epilogue(const v16i (&acc)[2][3][2], uint32
                 dn.valid[k] = valid ? 1 : 0;
             }
         } else {
-            if (valid && r2 > thr) pass |= 1u << i;  // lib.rs:660 strict '>'
+            if (ok) pass |= 1u << i;  // lib.rs:660 strict '>'
         }
     }
     if constexpr (DENSE) return;
@@ -414,10 +428,16 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
     v16i acc[2][3][2];
     zero_acc(acc);
     uint32_t buf = 0;
+#ifdef WLD_EXP_STAMPS
+    unsigned long long tsg = 0;
+#endif
     for (uint32_t grp = 0; grp < n_groups; ++grp) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this group landed
         __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
         asm volatile("" ::: "memory");
+#ifdef WLD_EXP_STAMPS
+        if (grp == 0) tsg = stamp();
+#endif
         if (grp + 1 < n_groups) issue(grp + 1, buf ^ 1);
         const uint8_t *gb = smem + buf * kGroupBytes;
         const uint32_t n_st = min((uint32_t)kGroup, NKB - grp * kGroup);
@@ -437,13 +457,15 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
 #ifdef WLD_EXP_STAMPS
     const unsigned long long ts1 = stamp();
 #endif
-    tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, shift, o, dn, sBits, sRowBase);
+    tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, shift, NP <= 65024u, o, dn,
+                                    sBits, sRowBase);
 #ifdef WLD_EXP_STAMPS
     const unsigned long long ts2 = stamp();
     if (tid == 0 && blockIdx.x < (1u << 18)) {
-        g_stamps[3 * blockIdx.x] = ts0;
-        g_stamps[3 * blockIdx.x + 1] = ts1;
-        g_stamps[3 * blockIdx.x + 2] = ts2;
+        g_stamps[4 * blockIdx.x] = ts0;
+        g_stamps[4 * blockIdx.x + 1] = tsg;
+        g_stamps[4 * blockIdx.x + 2] = ts1;
+        g_stamps[4 * blockIdx.x + 3] = ts2;
     }
 #endif
 }
@@ -477,8 +499,8 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_rows_kernel(const uint8_t *_
         const v4i d2 = *reinterpret_cast<const v4i *>(pd + 2 * NP + k0);
         mfma_block(acc, ca, cb, d0, d1, d2);
     }
-    tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, ok_bits[ta], ok_bits[tb], L, n_chunk_rows, thr, shift, o, dn,
-                                    sBits, sRowBase);
+    tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, ok_bits[ta], ok_bits[tb], L, n_chunk_rows, thr, shift,
+                                    NP <= 65024u, o, dn, sBits, sRowBase);
 }
 
 void launch_mfma_prep(const uint8_t *site_ok, const float *w_pad, size_t L, size_t LP, size_t NP, int shift,
