@@ -147,24 +147,47 @@ def main():
 
     N, L, thr, desc = CONFIGS[args.config]
     buf = synth(L, N)
-    weights = W.henikoff_weights(W.SiteSet.from_buffer(buf))  # host pre-pass (lib.rs:340-380)
+    t0 = time.perf_counter()
+    ss = W.SiteSet.from_buffer(buf)
+    kept = ss.filter_sites_of_interest()  # host pre-pass (lib.rs:309-338, main.rs:139)
+    weights = W.henikoff_weights(kept)  # host pre-pass (lib.rs:340-380)
+    prepass_ms = (time.perf_counter() - t0) * 1e3
+    assert kept.n_sites() == L  # the synthetic distribution keeps every site
+    torch.ones(1024, device=device).sum().item()  # CUDA context + allocator up before timing H2D
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     d_buf = torch.from_numpy(buf).to(device)
     d_w = torch.from_numpy(weights).to(device)
     torch.cuda.synchronize()
+    h2d_ms = (time.perf_counter() - t0) * 1e3
 
     kernel = {"auto": W.KERNEL_AUTO, "valu": W.KERNEL_VALU, "mfma": W.KERNEL_MFMA}[args.kernel]
+    # the same pre-pass on the device from the resident raw
+    # buffer (filter + Henikoff + encode), checked bit for bit against the host's
+    pre = W.Context(local_rank, kernel)
+    dev_ms = []
+    for _ in range(3):
+        assert pre.load_filtered_device(d_buf.data_ptr(), L, N) == L
+        dev_ms.append(pre.stats()["load_ms"])
+    assert np.array_equal(pre.weights().view(np.uint32), weights.view(np.uint32))
+    pre.close()
     ctx = W.Context(local_rank, kernel)
     ctx.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
+    load_ms = ctx.stats()["load_ms"]
     rb, re_ = ctx.shard_chunk_rows(L, world, rank)  # row-block shard (weightedld_amd/dist.py)
 
     from weightedld_amd import dist as wdist
 
+    gms = []
+
     def gather(n):
         if world == 1:
             return n
+        tg = time.perf_counter()
         # RCCL gather of this rank's reference-ordered rows to rank 0 (shards
         # concatenate in descending rank order: chunk rows descend)
         rows = wdist.gather_rows(wdist.pack_rows_device(ctx, n, device), rank, world)
+        gms.append((time.perf_counter() - tg) * 1e3)
         return int(rows.shape[1]) if rows is not None else 0
 
     def step():
@@ -243,6 +266,11 @@ def main():
         "north_star_hbm_view": {"algorithmic_bytes_per_pair": 2 * N, "achieved_GBps": hbm_alg,
                                 "peak_GBps": HBM_PEAK_GBPS, "frac": hbm_alg / HBM_PEAK_GBPS},
         "order_ms": float(np.mean(oms)),
+        # SURVEY 8(d) timing window: phases outside `value`'s step are reported, not timed in it
+        "phases_ms": {"host_prepass_filter_henikoff": prepass_ms,
+                      "device_prepass_filter_henikoff_encode": float(min(dev_ms)), "h2d_inputs": h2d_ms,
+                      "device_encode_prep": load_ms, "pair_kernel": kernel_ms, "order_assembly": float(np.mean(oms)),
+                      "gather_rank0": float(np.mean(gms)) if gms else 0.0},
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(buf, weights, thr, args.cpu_seconds)

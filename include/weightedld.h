@@ -170,6 +170,29 @@ int wld_load(wld_ctx *ctx, const uint8_t *sites, size_t n_sites, size_t n_seqs,
 int wld_load_device(wld_ctx *ctx, const void *d_sites, size_t n_sites, size_t n_seqs,
                     const uint64_t *site_map, const void *d_weights);
 
+/* Device pre-pass, replacing the host steps of
+ * main.rs:139-156 for the staged API: from the UNFILTERED SiteSet buffer
+ * (n_sites*n_seqs site-major Symbol codes, lib.rs:163), keeps the sites for
+ * which is_site_of_interest(site, ceil(min_acgt*n_seqs), min_minor, max_minor)
+ * holds (lib.rs:309-338; filter_by, lib.rs:230-251), computes Henikoff weights
+ * on the kept sites (lib.rs:340-380) or unit weights if `unweighted`
+ * (main.rs:150-153), and loads the kept set for wld_run with parent site
+ * indices as its site_map.  Bit-identical to wld_siteset_filter_sites_of_interest
+ * + wld_henikoff_weights + wld_load.  *n_kept receives the kept site count. */
+int wld_load_filtered(wld_ctx *ctx, const uint8_t *sites, size_t n_sites, size_t n_seqs,
+                      const uint64_t *site_map, float min_acgt, float min_minor, float max_minor,
+                      int unweighted, size_t *n_kept);
+/* Same, from a device pointer (read during the call only).  In both, site_map
+ * is the unfiltered SiteSet's own map (host, NULL = identity); kept sites
+ * report site_map[i] as their parent index, as filter_by composes it. */
+int wld_load_filtered_device(wld_ctx *ctx, const void *d_sites, size_t n_sites, size_t n_seqs,
+                             const uint64_t *site_map, float min_acgt, float min_minor, float max_minor,
+                             int unweighted, size_t *n_kept);
+/* After wld_load_filtered[_device]: the n_seqs weights (for the weights TSV,
+ * main.rs:157-165) and the n_kept parent site indices. */
+int wld_weights_copy(wld_ctx *ctx, float *out);
+int wld_site_map_copy(wld_ctx *ctx, uint64_t *out);
+
 /* Number of 256-site chunk rows n = ceil(n_sites/256) (lib.rs:615-619), and a
  * balanced contiguous partition of chunk rows [begin,end) for shard `shard` of
  * `n_shards` (equal pair counts up to chunk granularity).  Each shard's rows

@@ -1,0 +1,12 @@
+#!/bin/bash
+# End-to-end CLI timing (main.rs-style logs) on synthetic FASTA:
+#   tools/cli_e2e.sh -> gpurun_out/cli_e2e/*.log
+out=gpurun_out/cli_e2e; mkdir -p $out
+python3 tools/make_fasta.py 500 2000 /tmp/c2.fasta && python3 tools/make_fasta.py 2000 20000 /tmp/c4.fasta || exit 1
+export RUST_LOG=info
+timeout -k 10 300 weightedld_amd/bin/weighted_ld --fasta-input /tmp/c2.fasta --pair-output /tmp/c2.tsv --r2-threshold 0.0 > $out/c2.log 2>&1 || exit $?
+wc -l /tmp/c2.tsv >> $out/c2.log
+timeout -k 10 300 weightedld_amd/bin/weighted_ld --fasta-input /tmp/c4.fasta --pair-output /tmp/c4.tsv --r2-threshold 0.05 > $out/c4.log 2>&1 || exit $?
+wc -l /tmp/c4.tsv >> $out/c4.log
+timeout -k 10 300 weightedld_amd/bin/weighted_ld --fasta-input /tmp/c4.fasta --pair-output /tmp/c4b.tsv --r2-threshold 0.001 > $out/c4_thr0001.log 2>&1 || exit $?
+wc -l /tmp/c4b.tsv >> $out/c4_thr0001.log

@@ -93,6 +93,12 @@ SIGNATURES = {
     "wld_single_weighted_ld_pair": (_int, [_vp, _u8p, _u8p, _f32p, _sz, _f32p]),
     "wld_load": (_int, [_vp, _u8p, _sz, _sz, _u64p, _f32p]),
     "wld_load_device": (_int, [_vp, _vp, _sz, _sz, _u64p, _vp]),
+    "wld_load_filtered": (_int, [_vp, _u8p, _sz, _sz, _u64p, ctypes.c_float, ctypes.c_float, ctypes.c_float, _int,
+                                 ctypes.POINTER(ctypes.c_size_t)]),
+    "wld_load_filtered_device": (_int, [_vp, _vp, _sz, _sz, _u64p, ctypes.c_float, ctypes.c_float, ctypes.c_float, _int,
+                                        ctypes.POINTER(ctypes.c_size_t)]),
+    "wld_weights_copy": (_int, [_vp, _f32p]),
+    "wld_site_map_copy": (_int, [_vp, _u64p]),
     "wld_chunk_rows": (ctypes.c_uint32, [_sz]),
     "wld_shard_chunk_rows": (_int, [_sz, _int, _int, _u32p, _u32p]),
     "wld_run": (_int, [_vp, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint32, _u64p]),

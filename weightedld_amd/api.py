@@ -234,6 +234,42 @@ class Context:
                                     None if sm is None else _p(sm, ctypes.c_uint64),
                                     ctypes.c_void_p(d_weights_ptr)), "wld_load_device")
 
+    def load_filtered(self, buffer, min_acgt=0.8, min_minor=0.02, max_minor=0.5, unweighted=False, site_map=None):
+        """Device pre-pass (main.rs:139-156 on the GPU): filter the UNFILTERED
+        [n_sites, n_seqs] Symbol buffer with is_site_of_interest, compute
+        Henikoff (or unit) weights on the kept sites and load them.  Returns the
+        kept site count; weights() and site_map() give the pre-pass results."""
+        buf = np.ascontiguousarray(buffer, dtype=np.uint8)
+        L, N = buf.shape
+        sm = None if site_map is None else np.ascontiguousarray(site_map, dtype=np.uint64)
+        n = ctypes.c_size_t()
+        check(lib().wld_load_filtered(self._h, _p(buf, ctypes.c_uint8), L, N,
+                                      None if sm is None else _p(sm, ctypes.c_uint64), min_acgt, min_minor, max_minor,
+                                      int(bool(unweighted)), ctypes.byref(n)), "wld_load_filtered")
+        self._n_seqs, self._n_kept = N, int(n.value)
+        return self._n_kept
+
+    def load_filtered_device(self, d_sites_ptr, n_sites, n_seqs, min_acgt=0.8, min_minor=0.02, max_minor=0.5,
+                             unweighted=False, site_map=None):
+        sm = None if site_map is None else np.ascontiguousarray(site_map, dtype=np.uint64)
+        n = ctypes.c_size_t()
+        check(lib().wld_load_filtered_device(self._h, ctypes.c_void_p(d_sites_ptr), n_sites, n_seqs,
+                                             None if sm is None else _p(sm, ctypes.c_uint64), min_acgt,
+                                             min_minor, max_minor, int(bool(unweighted)), ctypes.byref(n)),
+              "wld_load_filtered_device")
+        self._n_seqs, self._n_kept = n_seqs, int(n.value)
+        return self._n_kept
+
+    def weights(self):
+        w = np.zeros(self._n_seqs, dtype=np.float32)
+        check(lib().wld_weights_copy(self._h, _p(w, ctypes.c_float)), "wld_weights_copy")
+        return w
+
+    def site_map(self):
+        m = np.zeros(self._n_kept, dtype=np.uint64)
+        check(lib().wld_site_map_copy(self._h, _p(m, ctypes.c_uint64)), "wld_site_map_copy")
+        return m
+
     def run(self, r2_threshold, row_begin=0, row_end=0):
         n = ctypes.c_uint64()
         check(lib().wld_run(self._h, r2_threshold, row_begin, row_end, ctypes.byref(n)), "wld_run")

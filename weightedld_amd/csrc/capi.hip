@@ -85,6 +85,9 @@ struct wld_ctx {
     bool loaded = false;
     size_t L = 0, N = 0, LP = 0, NP = 0;
     DevBuf raw, wraw, codes, w_pad, wstats, site_ok, site_map, planes, frag;
+    DevBuf keep, htab, site_index;  // device pre-pass (prepass.hip)
+    std::vector<uint64_t> kept_map;  // parent indices of the kept sites (wld_site_map_copy)
+    bool prepass_loaded = false;
     bool has_map = false;
     bool use_frag = false;
     int kernel = WLD_KERNEL_VALU;
@@ -104,7 +107,7 @@ struct wld_ctx {
 
     ~wld_ctx() {
         (void)hipSetDevice(device);
-        DevBuf *all[] = {&raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &tiles,
+        DevBuf *all[] = {&keep, &htab, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &tiles,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
@@ -143,7 +146,8 @@ int weight_shift(float maxabs) {
     return shift;
 }
 
-int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint64_t *site_map) {
+int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint64_t *site_map,
+                const uint32_t *d_site_index = nullptr) {
     const size_t L = c->L, N = c->N;
     c->LP = round_up(std::max<size_t>(L, 1), kChunk);
     c->NP = round_up(std::max<size_t>(N, 1), kSeqPad);
@@ -152,7 +156,8 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     WLD_TRY(ensure(c->w_pad, c->NP * sizeof(float)));
     WLD_TRY(ensure(c->wstats, 4 * sizeof(float)));
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-    launch_encode(d_sites, L, N, c->LP, c->NP, ptr<uint8_t>(c->codes), ptr<uint8_t>(c->site_ok), c->stream);
+    launch_encode(d_sites, d_site_index, L, N, c->LP, c->NP, ptr<uint8_t>(c->codes), ptr<uint8_t>(c->site_ok),
+                  c->stream);
     HIP_TRY(hipGetLastError());
     launch_weight_prep(d_w, N, c->NP, ptr<float>(c->w_pad), ptr<float>(c->wstats), c->stream);
     HIP_TRY(hipGetLastError());
@@ -325,6 +330,7 @@ int wld_load(wld_ctx *c, const uint8_t *sites, size_t n_sites, size_t n_seqs, co
     if ((!sites && n_sites * n_seqs) || (!weights && n_seqs)) return fail(WLD_E_ARG, "wld_load: null input");
     if (n_sites >= (1u << 16) * (size_t)kTile) return fail(WLD_E_ARG, "n_sites %zu too large", n_sites);
     c->loaded = false;
+    c->prepass_loaded = false;
     c->L = n_sites;
     c->N = n_seqs;
     WLD_TRY(ensure(c->raw, n_sites * n_seqs));
@@ -341,9 +347,100 @@ int wld_load_device(wld_ctx *c, const void *d_sites, size_t n_sites, size_t n_se
     if ((!d_sites && n_sites * n_seqs) || (!d_weights && n_seqs)) return fail(WLD_E_ARG, "wld_load_device: null input");
     if (n_sites >= (1u << 16) * (size_t)kTile) return fail(WLD_E_ARG, "n_sites %zu too large", n_sites);
     c->loaded = false;
+    c->prepass_loaded = false;
     c->L = n_sites;
     c->N = n_seqs;
     return common_load(c, (const uint8_t *)d_sites, (const float *)d_weights, site_map);
+}
+
+namespace {
+// wld_load_filtered[_device]: site stats on every raw site, kept-site map on
+// the host (one byte per site back), Henikoff on the kept sites, then the
+// common load of the kept set straight from the raw rows.
+int load_filtered(wld_ctx *c, const uint8_t *d_raw, size_t n_sites, size_t n_seqs, const uint64_t *raw_map,
+                  float min_acgt, float min_minor, float max_minor, int unweighted, size_t *n_kept) {
+    if (n_sites >= (1u << 31)) return fail(WLD_E_ARG, "n_sites %zu too large", n_sites);
+    c->loaded = false;
+    c->prepass_loaded = false;
+    const size_t L0 = n_sites, N = n_seqs;
+    // main.rs:139: ceil(min_acgt * n_seqs) in f32, `as usize` saturating at 0 (host.cpp)
+    const float cnt = std::ceil(min_acgt * (float)N);
+    const uint32_t min_acgt_cnt = cnt <= 0.0f ? 0u : (uint32_t)std::min<double>(cnt, 4294967295.0);
+    WLD_TRY(ensure(c->keep, std::max<size_t>(L0, 1)));
+    WLD_TRY(ensure(c->htab, std::max<size_t>(L0, 1) * 6 * sizeof(float)));
+    HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+    launch_site_stats(d_raw, L0, N, min_acgt_cnt, min_minor, max_minor, ptr<uint8_t>(c->keep), ptr<float>(c->htab),
+                      c->stream);
+    HIP_TRY(hipGetLastError());
+    std::vector<uint8_t> keep(L0);
+    if (L0) HIP_TRY(hipMemcpyAsync(keep.data(), c->keep.p, L0, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->kept_map.clear();
+    std::vector<uint32_t> idx;
+    for (size_t i = 0; i < L0; ++i)
+        if (keep[i]) {
+            c->kept_map.push_back(raw_map ? raw_map[i] : (uint64_t)i);
+            idx.push_back((uint32_t)i);
+        }
+    const size_t L = idx.size();
+    if (L >= (1u << 16) * (size_t)kTile) return fail(WLD_E_ARG, "%zu kept sites: too many", L);
+    WLD_TRY(ensure(c->site_index, std::max<size_t>(L, 1) * sizeof(uint32_t)));
+    if (L) HIP_TRY(hipMemcpyAsync(c->site_index.p, idx.data(), L * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    WLD_TRY(ensure(c->wraw, std::max<size_t>(N, 1) * sizeof(float)));
+    if (unweighted)
+        launch_fill_ones(ptr<float>(c->wraw), N, c->stream);
+    else
+        launch_henikoff(d_raw, ptr<uint32_t>(c->site_index), L, N, ptr<float>(c->htab), ptr<float>(c->wraw),
+                        c->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    HIP_TRY(hipEventSynchronize(c->ev[1]));
+    const double prepass_ms = event_ms(c->ev[0], c->ev[1]);
+    c->L = L;
+    c->N = N;
+    WLD_TRY(common_load(c, d_raw, ptr<float>(c->wraw), c->kept_map.data(), ptr<uint32_t>(c->site_index)));
+    c->stats.load_ms += prepass_ms;
+    c->prepass_loaded = true;
+    if (n_kept) *n_kept = L;
+    return WLD_OK;
+}
+}  // namespace
+
+int wld_load_filtered(wld_ctx *c, const uint8_t *sites, size_t n_sites, size_t n_seqs, const uint64_t *site_map,
+                      float min_acgt, float min_minor, float max_minor, int unweighted, size_t *n_kept) {
+    WLD_TRY(set_dev(c));
+    if (!sites && n_sites * n_seqs) return fail(WLD_E_ARG, "wld_load_filtered: null input");
+    WLD_TRY(ensure(c->raw, std::max<size_t>(n_sites * n_seqs, 1)));
+    if (n_sites * n_seqs)
+        HIP_TRY(hipMemcpyAsync(c->raw.p, sites, n_sites * n_seqs, hipMemcpyHostToDevice, c->stream));
+    return load_filtered(c, ptr<uint8_t>(c->raw), n_sites, n_seqs, site_map, min_acgt, min_minor, max_minor,
+                         unweighted, n_kept);
+}
+
+int wld_load_filtered_device(wld_ctx *c, const void *d_sites, size_t n_sites, size_t n_seqs,
+                             const uint64_t *site_map, float min_acgt, float min_minor, float max_minor,
+                             int unweighted, size_t *n_kept) {
+    WLD_TRY(set_dev(c));
+    if (!d_sites && n_sites * n_seqs) return fail(WLD_E_ARG, "wld_load_filtered_device: null input");
+    return load_filtered(c, (const uint8_t *)d_sites, n_sites, n_seqs, site_map, min_acgt, min_minor, max_minor,
+                         unweighted, n_kept);
+}
+
+int wld_weights_copy(wld_ctx *c, float *out) {
+    WLD_TRY(set_dev(c));
+    if (!c->prepass_loaded) return fail(WLD_E_STATE, "wld_weights_copy before wld_load_filtered");
+    if (!out && c->N) return fail(WLD_E_ARG, "wld_weights_copy: null output");
+    if (c->N) HIP_TRY(hipMemcpyAsync(out, c->wraw.p, c->N * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return WLD_OK;
+}
+
+int wld_site_map_copy(wld_ctx *c, uint64_t *out) {
+    if (!c) return fail(WLD_E_ARG, "null context");
+    if (!c->prepass_loaded) return fail(WLD_E_STATE, "wld_site_map_copy before wld_load_filtered");
+    if (!out && !c->kept_map.empty()) return fail(WLD_E_ARG, "wld_site_map_copy: null output");
+    std::copy(c->kept_map.begin(), c->kept_map.end(), out);
+    return WLD_OK;
 }
 
 uint32_t wld_chunk_rows(size_t n_sites) { return chunk_rows_of(n_sites); }

@@ -106,6 +106,7 @@ struct Opt {
     std::string fasta_input, vcf_input, weights_output, pair_output;
     float min_acgt = 0.8f, min_minor = 0.02f, max_minor = 0.5f, r2_threshold = 0.1f;
     bool unweighted = false;
+    bool gpu_prepass = false;
     int device = 0;
     int kernel = WLD_KERNEL_AUTO;
 };
@@ -118,6 +119,7 @@ void usage(FILE *f) {
             "FLAGS:\n"
             "    -h, --help          Prints help information\n"
             "        --unweighted    Use unit weights instead of Henikoff weights\n"
+            "        --gpu-prepass   Filter sites and compute Henikoff weights on the GPU (FASTA input)\n"
             "    -V, --version       Prints version information\n\n"
             "OPTIONS:\n"
             "        --fasta-input <fasta-input>          The source file to load\n"
@@ -198,6 +200,8 @@ Opt parse(int argc, char **argv) {
             have_pair = true;
         } else if (a == "--unweighted") {
             o.unweighted = true;
+        } else if (a == "--gpu-prepass") {
+            o.gpu_prepass = true;
         } else if (a == "--device") {
             o.device = atoi(need("--device").c_str());
         } else if (a == "--kernel") {
@@ -284,12 +288,93 @@ int write_pair_stats(const std::string &path, const wld_pairs &p) {
     return ok ? WLD_OK : WLD_E_IO;
 }
 
+// main.rs:186-212 after the pair computation: timing logs, TSV, clean-up.
+int finish(const Opt &opt, wld_ctx *ctx, wld_pairs &pairs, std::chrono::steady_clock::duration dur,
+           uint64_t total_pairs) {
+    using clk = std::chrono::steady_clock;
+    INFO("Finished computing pairwise weighted LD stats in %s", fmt_duration(dur).c_str());
+    const double secs = std::chrono::duration<double>(dur).count();
+    INFO("    %s pairs computed at ~%s, %s passed threshold", human((double)total_pairs).c_str(),
+         human((double)total_pairs / secs, "pairs/s").c_str(), human((double)pairs.n).c_str());
+    wld_run_stats rs;
+    if (wld_last_stats(ctx, &rs) == WLD_OK)
+        log_at(4, "device: kernel=%s pairs=%" PRIu64 " pair_kernel=%.3fms order=%.3fms",
+               rs.kernel == WLD_KERNEL_MFMA ? "mfma" : "valu", rs.pairs, rs.pair_kernel_ms, rs.order_ms);
+
+    INFO("Writing output to %s", debug_path(opt.pair_output).c_str());
+    auto sw = clk::now();
+    if (write_pair_stats(opt.pair_output, pairs) != WLD_OK) {
+        fprintf(stderr, "Error: cannot write %s\n", opt.pair_output.c_str());
+        return 1;
+    }
+    INFO("Finshed writing output in %s", fmt_duration(clk::now() - sw).c_str());  // (sic) main.rs:210
+    wld_pairs_free(&pairs);
+    wld_destroy(ctx);
+    return 0;
+}
+
+// --gpu-prepass: main.rs:139-190 with the site filter and Henikoff weights on
+// the device (wld_load_filtered), then the staged run and a host copy of the rows.
+int run_gpu_prepass(const Opt &opt, wld_siteset *siteset, wld_ctx *ctx) {
+    using clk = std::chrono::steady_clock;
+    const size_t L0 = wld_siteset_n_sites(siteset), N = wld_siteset_n_seqs(siteset);
+    auto sw = clk::now();
+    size_t L = 0;
+    int st = wld_load_filtered(ctx, wld_siteset_buffer(siteset), L0, N, wld_siteset_site_map(siteset), opt.min_acgt,
+                               opt.min_minor, opt.max_minor, opt.unweighted ? 1 : 0, &L);
+    if (st != WLD_OK) die(st, "load_filtered");
+    INFO("Computed + filtered sites of interest%s on the GPU in %s", opt.unweighted ? "" : " and Henikoff weights",
+         fmt_duration(clk::now() - sw).c_str());
+    INFO("    Found %zu sites of interest", L);
+    if (!opt.weights_output.empty()) {
+        std::vector<float> weights(N);
+        if ((st = wld_weights_copy(ctx, weights.data())) != WLD_OK) die(st, "weights_copy");
+        INFO("Writing weights to %s", debug_path(opt.weights_output).c_str());
+        if (write_henikoff_weights(opt.weights_output, weights) != WLD_OK) {
+            fprintf(stderr, "Error: cannot write %s\n", opt.weights_output.c_str());
+            return 1;
+        }
+    }
+    INFO("Beginning pairwise weighted LD computation");
+    sw = clk::now();
+    const uint64_t total_pairs = ((uint64_t)L - 1) * ((uint64_t)L - 2) / 2;  // main.rs:168 (sic, wraps)
+    uint64_t n = 0;
+    if ((st = wld_run(ctx, opt.r2_threshold, 0, 0, &n)) != WLD_OK) die(st, "all_weighted_ld_pairs");
+    wld_pairs pairs;
+    pairs.n = n;
+    const size_t m = std::max<uint64_t>(n, 1);
+    pairs.site_a = (uint32_t *)malloc(m * 4);
+    pairs.site_b = (uint32_t *)malloc(m * 4);
+    pairs.d = (float *)malloc(m * 4);
+    pairs.d_prime = (float *)malloc(m * 4);
+    pairs.r2 = (float *)malloc(m * 4);
+    if (!pairs.site_a || !pairs.site_b || !pairs.d || !pairs.d_prime || !pairs.r2) die(WLD_E_OOM, "rows");
+    if (n && (st = wld_rows_copy(ctx, pairs.site_a, pairs.site_b, pairs.d, pairs.d_prime, pairs.r2)) != WLD_OK)
+        die(st, "rows_copy");
+    return finish(opt, ctx, pairs, clk::now() - sw, total_pairs);
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
     init_logger();
     Opt opt = parse(argc, argv);
     using clk = std::chrono::steady_clock;
+
+    // The device context (HIP runtime start-up) is created while the input is
+    // read, so that the LD timing below covers the computation only.
+    wld_ctx *ctx = nullptr;
+    int ctx_st = WLD_OK;
+    std::thread ctx_thread([&] { ctx_st = wld_create(opt.device, &ctx); });
+    auto get_ctx = [&]() -> wld_ctx * {
+        if (ctx_thread.joinable()) ctx_thread.join();
+        if (ctx_st != WLD_OK) die(ctx_st, "wld_create");
+        if (opt.kernel != WLD_KERNEL_AUTO) {
+            int s2 = wld_set_kernel(ctx, opt.kernel);
+            if (s2 != WLD_OK) die(s2, "wld_set_kernel");
+        }
+        return ctx;
+    };
 
     auto sw = clk::now();
     wld_siteset *siteset = nullptr;
@@ -302,6 +387,8 @@ int main(int argc, char **argv) {
     if (st != WLD_OK) die(st, vcf ? "read_vcf" : "read_fasta");
     INFO("Loaded %s file in %s", vcf ? "vcf" : "fasta", fmt_duration(clk::now() - sw).c_str());
     INFO("    %zu sequences, %zu sites", wld_siteset_n_seqs(siteset), wld_siteset_n_sites(siteset));
+
+    if (opt.gpu_prepass && !vcf) return run_gpu_prepass(opt, siteset, get_ctx());
 
     sw = clk::now();
     wld_siteset *filtered = nullptr;
@@ -336,34 +423,13 @@ int main(int argc, char **argv) {
     INFO("Beginning pairwise weighted LD computation");
     sw = clk::now();
     const uint64_t total_pairs = ((uint64_t)L - 1) * ((uint64_t)L - 2) / 2;  // main.rs:168 (sic, wraps)
-    wld_ctx *ctx = nullptr;
-    st = wld_create(opt.device, &ctx);
-    if (st != WLD_OK) die(st, "wld_create");
-    if (opt.kernel != WLD_KERNEL_AUTO && (st = wld_set_kernel(ctx, opt.kernel)) != WLD_OK) die(st, "wld_set_kernel");
+    get_ctx();
     wld_pairs pairs;
     st = wld_all_weighted_ld_pairs(ctx, wld_siteset_buffer(filtered), L, N, wld_siteset_site_map(filtered),
                                    weights.data(), opt.r2_threshold, nullptr, nullptr, &pairs);
     if (st != WLD_OK) die(st, "all_weighted_ld_pairs");
-    const auto dur = clk::now() - sw;
-    INFO("Finished computing pairwise weighted LD stats in %s", fmt_duration(dur).c_str());
-    const double secs = std::chrono::duration<double>(dur).count();
-    INFO("    %s pairs computed at ~%s, %s passed threshold", human((double)total_pairs).c_str(),
-         human((double)total_pairs / secs, "pairs/s").c_str(), human((double)pairs.n).c_str());
-    wld_run_stats rs;
-    if (wld_last_stats(ctx, &rs) == WLD_OK)
-        log_at(4, "device: kernel=%s pairs=%" PRIu64 " pair_kernel=%.3fms order=%.3fms",
-               rs.kernel == WLD_KERNEL_MFMA ? "mfma" : "valu", rs.pairs, rs.pair_kernel_ms, rs.order_ms);
-
-    INFO("Writing output to %s", debug_path(opt.pair_output).c_str());
-    sw = clk::now();
-    if (write_pair_stats(opt.pair_output, pairs) != WLD_OK) {
-        fprintf(stderr, "Error: cannot write %s\n", opt.pair_output.c_str());
-        return 1;
-    }
-    INFO("Finshed writing output in %s", fmt_duration(clk::now() - sw).c_str());  // (sic) main.rs:210
-    wld_pairs_free(&pairs);
-    wld_destroy(ctx);
+    const int rc = finish(opt, ctx, pairs, clk::now() - sw, total_pairs);
     wld_siteset_free(filtered);
     wld_siteset_free(siteset);
-    return 0;
+    return rc;
 }

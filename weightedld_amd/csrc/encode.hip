@@ -13,15 +13,17 @@
 
 namespace wld {
 
-__global__ __launch_bounds__(256) void encode_kernel(const uint8_t *__restrict__ sites, uint32_t L, uint32_t N,
-                                                      uint32_t NP, uint8_t *__restrict__ codes,
+__global__ __launch_bounds__(256) void encode_kernel(const uint8_t *__restrict__ sites,
+                                                      const uint32_t *__restrict__ site_index, uint32_t L,
+                                                      uint32_t N, uint32_t NP, uint8_t *__restrict__ codes,
                                                       uint8_t *__restrict__ site_ok) {
     __shared__ uint32_t h[6];
     const uint32_t s = blockIdx.x;
     const uint32_t tid = threadIdx.x;
     if (tid < 6) h[tid] = 0;
     __syncthreads();
-    const uint8_t *row = sites + (size_t)s * N;
+    // site_index (device pre-pass): row s of the filtered set is raw row site_index[s]
+    const uint8_t *row = sites + (size_t)(site_index && s < L ? site_index[s] : s) * N;
     if (s < L) {
         uint32_t c[6] = {0, 0, 0, 0, 0, 0};
         for (uint32_t k = tid; k < N; k += 256) {
@@ -98,10 +100,10 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(const float *__restric
     }
 }
 
-void launch_encode(const uint8_t *d_sites, size_t L, size_t N, size_t LP, size_t NP, uint8_t *codes,
-                   uint8_t *site_ok, hipStream_t s) {
-    hipLaunchKernelGGL(encode_kernel, dim3((unsigned)LP), dim3(256), 0, s, d_sites, (uint32_t)L, (uint32_t)N,
-                       (uint32_t)NP, codes, site_ok);
+void launch_encode(const uint8_t *d_sites, const uint32_t *site_index, size_t L, size_t N, size_t LP, size_t NP,
+                   uint8_t *codes, uint8_t *site_ok, hipStream_t s) {
+    hipLaunchKernelGGL(encode_kernel, dim3((unsigned)LP), dim3(256), 0, s, d_sites, site_index, (uint32_t)L,
+                       (uint32_t)N, (uint32_t)NP, codes, site_ok);
 }
 
 void launch_weight_prep(const float *d_w, size_t N, size_t NP, float *w_pad, float *wstats, hipStream_t s) {

@@ -37,9 +37,18 @@ struct DenseArgs {
 };
 
 // encode.hip
-void launch_encode(const uint8_t *d_sites, size_t L, size_t N, size_t LP, size_t NP, uint8_t *codes,
-                   uint8_t *site_ok, hipStream_t s);
+// site_index: nullptr, or the kept-site map of the device pre-pass (row s of the
+// filtered set = raw row site_index[s])
+void launch_encode(const uint8_t *d_sites, const uint32_t *site_index, size_t L, size_t N, size_t LP, size_t NP,
+                   uint8_t *codes, uint8_t *site_ok, hipStream_t s);
 void launch_weight_prep(const float *d_w, size_t N, size_t NP, float *w_pad, float *wstats, hipStream_t s);
+
+// prepass.hip (device site filter + Henikoff weights, bit-exact with host.cpp)
+void launch_site_stats(const uint8_t *raw, size_t L, size_t N, uint32_t min_acgt, float min_minor, float max_minor,
+                       uint8_t *keep, float *tab, hipStream_t s);
+void launch_henikoff(const uint8_t *raw, const uint32_t *site_index, size_t n_kept, size_t N, const float *tab,
+                     float *w, hipStream_t s);
+void launch_fill_ones(float *w, size_t N, hipStream_t s);
 
 // pair_valu.hip
 void launch_pair_valu(const uint8_t *codes, const float *w, const uint8_t *site_ok, const uint32_t *tiles,
