@@ -27,9 +27,9 @@ $(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
 $(PKG)/libweightedld.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS) -lpthread
 
-$(PKG)/bin/weighted_ld: $(CSRC)/cli.cpp $(PKG)/libweightedld.so include/weightedld.h
+$(PKG)/bin/weighted_ld: $(CSRC)/cli.cpp $(CSRC)/tsv_format.hpp $(PKG)/libweightedld.so include/weightedld.h
 	@mkdir -p $(PKG)/bin
-	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $(CSRC)/cli.cpp -L$(PKG) -lweightedld -Wl,-rpath,'$$ORIGIN/..' -lpthread
+	g++ -O2 -std=c++17 -Wall -Iinclude -I$(CSRC) -o $@ $(CSRC)/cli.cpp -L$(PKG) -lweightedld -Wl,-rpath,'$$ORIGIN/..' -lpthread
 
 oracle:
 	$(MAKE) -s -C oracle

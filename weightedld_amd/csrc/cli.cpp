@@ -18,10 +18,13 @@
 #include <ctime>
 #include <string>
 #include <algorithm>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <vector>
 
 #include "weightedld.h"
+#include "tsv_format.hpp"
 
 namespace {
 
@@ -94,13 +97,9 @@ std::string human(double v, const char *units = "") {
     return buf;
 }
 
-// Rust `{:.3}` of an f32 (main.rs:76,106).  Finite values print like C's %.3f
-// on the exact binary value; NaN and infinities use Rust's spelling.
-inline int fmt3(char *out, float v) {
-    if (std::isnan(v)) return sprintf(out, "NaN");
-    if (std::isinf(v)) return sprintf(out, v > 0 ? "inf" : "-inf");
-    return sprintf(out, "%.3f", (double)v);
-}
+// Rust `{:.3}` of an f32 (main.rs:76,106): exact integer rounding, tsv_format.hpp
+using wld_tsv::fmt3;
+using wld_tsv::fmt_u64;
 
 struct Opt {
     std::string fasta_input, vcf_input, weights_output, pair_output;
@@ -238,7 +237,8 @@ int write_henikoff_weights(const std::string &path, const std::vector<float> &w)
     std::string out = "Sequence_index\thk_weight\n";
     char buf[64];
     for (size_t i = 0; i < w.size(); ++i) {
-        int n = snprintf(buf, sizeof buf, "%zu\t", i);
+        int n = fmt_u64(buf, i);
+        buf[n++] = '\t';
         n += fmt3(buf + n, w[i]);
         buf[n++] = '\n';
         out.append(buf, n);
@@ -249,41 +249,86 @@ int write_henikoff_weights(const std::string &path, const std::vector<float> &w)
 }
 
 // main.rs:82-119: header, then "{}\t{}\t{:.3}\t{:.3}\t{:.3}" per row in PairStore order.
-// Rows are formatted in parallel blocks and written in order.
+// Worker threads claim blocks of rows in order and format them into a ring of
+// slot buffers; the calling thread writes finished blocks in order, so
+// formatting overlaps the file write and memory stays at 2 slots per worker.
 int write_pair_stats(const std::string &path, const wld_pairs &p) {
     FILE *f = fopen(path.c_str(), "wb");
     if (!f) return WLD_E_IO;
     const char *hdr = "site_a\tsite_b\td\td'\tr2\n";
     bool ok = fwrite(hdr, 1, strlen(hdr), f) == strlen(hdr);
-    const uint64_t n = p.n;
-    const uint64_t block = 1 << 18;
-    unsigned nt = std::max(1u, std::min(std::thread::hardware_concurrency(), 32u));
-    for (uint64_t base = 0; base < n && ok; base += block * nt) {
-        std::vector<std::string> parts(nt);
-        std::vector<std::thread> th;
-        for (unsigned t = 0; t < nt; ++t) {
-            uint64_t lo = base + t * block, hi = std::min(n, lo + block);
-            if (lo >= hi) break;
-            th.emplace_back([&, lo, hi, t] {
-                std::string &s = parts[t];
-                s.reserve((hi - lo) * 40);
-                char buf[128];
-                for (uint64_t i = lo; i < hi; ++i) {
-                    int k = snprintf(buf, sizeof buf, "%u\t%u\t", p.site_a[i], p.site_b[i]);
-                    k += fmt3(buf + k, p.d[i]);
-                    buf[k++] = '\t';
-                    k += fmt3(buf + k, p.d_prime[i]);
-                    buf[k++] = '\t';
-                    k += fmt3(buf + k, p.r2[i]);
-                    buf[k++] = '\n';
-                    s.append(buf, k);
-                }
-            });
+    const uint64_t n = p.n, block = 1 << 16;
+    const uint64_t n_blocks = (n + block - 1) / block;
+    const unsigned nt =
+        (unsigned)std::max<uint64_t>(1, std::min<uint64_t>({std::thread::hardware_concurrency(), 32, n_blocks}));
+    const uint64_t n_slots = 2 * (uint64_t)nt;
+    struct Slot {
+        std::vector<char> buf;
+        size_t len = 0;
+        uint64_t ready = UINT64_MAX;  // block index whose text the slot holds
+    };
+    std::vector<Slot> slots(n_slots);
+    std::mutex mu;
+    std::condition_variable cv_ready, cv_free;
+    uint64_t next_claim = 0, next_write = 0;
+    bool abort = false;
+    auto worker = [&] {
+        for (;;) {
+            uint64_t b;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                if (next_claim >= n_blocks || abort) return;
+                b = next_claim++;
+                // slot b % n_slots is free once block b - n_slots has been written
+                cv_free.wait(lk, [&] { return abort || next_write + n_slots > b; });
+                if (abort) return;
+            }
+            Slot &sl = slots[b % n_slots];
+            const uint64_t lo = b * block, hi = std::min(n, lo + block);
+            if (sl.buf.size() < (hi - lo) * 48) sl.buf.resize((hi - lo) * 48);
+            size_t k = 0;
+            for (uint64_t i = lo; i < hi; ++i) {
+                if (k + 256 > sl.buf.size()) sl.buf.resize(sl.buf.size() * 2);
+                char *o = sl.buf.data() + k;
+                int m = fmt_u64(o, p.site_a[i]);
+                o[m++] = '\t';
+                m += fmt_u64(o + m, p.site_b[i]);
+                o[m++] = '\t';
+                m += fmt3(o + m, p.d[i]);
+                o[m++] = '\t';
+                m += fmt3(o + m, p.d_prime[i]);
+                o[m++] = '\t';
+                m += fmt3(o + m, p.r2[i]);
+                o[m++] = '\n';
+                k += m;
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                sl.len = k;
+                sl.ready = b;
+            }
+            cv_ready.notify_all();
         }
-        for (auto &x : th) x.join();
-        for (auto &s : parts)
-            if (!s.empty() && fwrite(s.data(), 1, s.size(), f) != s.size()) ok = false;
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt && n_blocks; ++t) th.emplace_back(worker);
+    for (uint64_t b = 0; b < n_blocks; ++b) {
+        Slot &sl = slots[b % n_slots];
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv_ready.wait(lk, [&] { return sl.ready == b; });
+        }
+        if (ok && fwrite(sl.buf.data(), 1, sl.len, f) != sl.len) ok = false;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            sl.ready = UINT64_MAX;
+            ++next_write;
+            if (!ok) abort = true;
+        }
+        cv_free.notify_all();
+        if (!ok) break;
     }
+    for (auto &x : th) x.join();
     if (fclose(f) != 0) ok = false;
     return ok ? WLD_OK : WLD_E_IO;
 }
