@@ -2,7 +2,7 @@
 """Headline benchmark: LD site-pairs/s at N=2000 sequences x L=20000 sites (BASELINE config 4).
 
 A "step" is one all_weighted_ld_pairs pass (lib.rs:578-684) over the whole
-synthetic alignment: the pair kernel over this rank's row-block shard, the
+synthetic alignment: the pair kernel over this rank's chunk-range shard, the
 reference-order assembly of the rows with r2 > 0.05 and, for N>1, their RCCL
 gather to rank 0.  Inputs (site codes + weights) are resident in HBM before
 the timed region.  Total work is fixed as N grows (strong scaling).
@@ -174,7 +174,8 @@ def main():
     ctx = W.Context(local_rank, kernel)
     ctx.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
     load_ms = ctx.stats()["load_ms"]
-    rb, re_ = ctx.shard_chunk_rows(L, world, rank)  # row-block shard (weightedld_amd/dist.py)
+    # contiguous run of the reference chunk sequence, balanced by pairs (weightedld_amd/dist.py)
+    cb, ce = ctx.shard_chunks(L, world, rank)
 
     from weightedld_amd import dist as wdist
 
@@ -191,7 +192,7 @@ def main():
         return int(rows.shape[1]) if rows is not None else 0
 
     def step():
-        n = ctx.run(thr, rb, re_)
+        n = ctx.run_chunks(thr, cb, ce)
         return gather(n)
 
     for _ in range(args.warmup):
@@ -229,7 +230,7 @@ def main():
 
     total_pairs = L * (L - 1) // 2
     value = total_pairs * args.steps / elapsed
-    shard_pairs = pairs_in_rows(L, rb, re_)
+    shard_pairs = ctx.pairs_in_chunks(L, cb, ce)
     # dominant kernel roofline (DESIGN.md "Roofline"): per-launch algorithmic work / HIP-event time
     if kern_name == "mfma":
         ops = shard_pairs * 24.0 * N  # 3 weight planes x 4 masked products x N seqs x 2 ops/MAC
@@ -261,7 +262,7 @@ def main():
         "data": "synthetic (seeded bench_weighted_pair_ld.rs distribution, Henikoff weights)",
         "config": {"workload": desc, "n_seqs": N, "n_sites": L, "r2_threshold": thr, "pairs": total_pairs,
                    "rows_passing": rows, "kernel": kern_name,
-                   "parallelism": "row-block shard x%d%s" % (world, " + RCCL gather" if world > 1 else "")},
+                   "parallelism": "chunk-range shard x%d%s" % (world, " + RCCL gather" if world > 1 else "")},
         "roofline": roof,
         "north_star_hbm_view": {"algorithmic_bytes_per_pair": 2 * N, "achieved_GBps": hbm_alg,
                                 "peak_GBps": HBM_PEAK_GBPS, "frac": hbm_alg / HBM_PEAK_GBPS},

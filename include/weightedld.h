@@ -201,11 +201,28 @@ int wld_site_map_copy(wld_ctx *ctx, uint64_t *out);
 uint32_t wld_chunk_rows(size_t n_sites);
 int wld_shard_chunk_rows(size_t n_sites, int n_shards, int shard, uint32_t *begin, uint32_t *end);
 
+/* The reference's chunk sequence (lib.rs:615-634): n(n+1)/2 chunks of 256x256
+ * sites, linear index i <-> (row, col) by triu_index, rows descending and
+ * columns ascending; PairStore rows come chunk by chunk in this order.
+ * wld_shard_chunks partitions it into contiguous linear ranges [begin,end) of
+ * near-equal pair count (single-chunk granularity, finer than chunk rows);
+ * shard 0 takes the LAST range, so shards concatenate in DESCENDING shard
+ * order, as with wld_shard_chunk_rows.  wld_pairs_in_chunks counts the pairs
+ * (a<b) of a range. */
+uint32_t wld_chunks(size_t n_sites);
+int wld_shard_chunks(size_t n_sites, int n_shards, int shard, uint32_t *begin, uint32_t *end);
+uint64_t wld_pairs_in_chunks(size_t n_sites, uint32_t begin, uint32_t end);
+
 /* Evaluates every pair (a<b) whose a lies in chunk rows [row_begin,row_end)
  * (pass 0, wld_chunk_rows() for all), filters r2 > r2_threshold and leaves
  * the rows on the device in reference order.  *n_rows receives the count. */
 int wld_run(wld_ctx *ctx, float r2_threshold, uint32_t row_begin, uint32_t row_end,
             uint64_t *n_rows);
+/* wld_run over the linear chunk range [chunk_begin,chunk_end) (end 0 = all):
+ * the rows of those chunks, in reference order (all_weighted_ld_pairs'
+ * par_iter over 0..n(n+1)/2, lib.rs:621-683, restricted to a sub-range). */
+int wld_run_chunks(wld_ctx *ctx, float r2_threshold, uint32_t chunk_begin, uint32_t chunk_end,
+                   uint64_t *n_rows);
 /* Device pointers of the last run's rows (valid until the next run/load or
  * destroy; do not free). */
 int wld_rows_device(wld_ctx *ctx, wld_pairs *view);

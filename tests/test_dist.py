@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, L, N, thr, q):
+def _worker(rank, world, port, L, N, thr, q, by_chunk=False):
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import torch.distributed as dist
@@ -40,11 +40,14 @@ def _worker(rank, world, port, L, N, thr, q):
         rng = np.random.default_rng(42)
         buf = rng.integers(0, 5, size=(L, N)).astype(np.uint8)
         w = rng.random(N).astype(np.float32)
-        rb, re_ = wdist.shard_rows(L, world, rank)
-        n = (L + 255) // 256
-        lin = lambda r, c: (n - 1 - r) * (n - r) // 2 + (c - r)  # noqa: E731
-        lo, hi = (lin(re_ - 1, re_ - 1), lin(rb, rb) + (n - rb)) if re_ > rb else (0, 0)
-        mine = O.all_pairs(buf, w, thr, n_threads=2, chunk_lo=lo, chunk_hi=hi) if re_ > rb else \
+        if by_chunk:  # the bench's split: contiguous chunk ranges (wld_shard_chunks)
+            lo, hi = wdist.shard_chunks(L, world, rank)
+        else:  # whole chunk rows (wld_shard_chunk_rows)
+            rb, re_ = wdist.shard_rows(L, world, rank)
+            n = (L + 255) // 256
+            lin = lambda r, c: (n - 1 - r) * (n - r) // 2 + (c - r)  # noqa: E731
+            lo, hi = (lin(re_ - 1, re_ - 1), lin(rb, rb) + (n - rb)) if re_ > rb else (0, 0)
+        mine = O.all_pairs(buf, w, thr, n_threads=2, chunk_lo=lo, chunk_hi=hi) if hi > lo else \
             {f: np.zeros(0, dtype=np.float32 if f in ("d", "d_prime", "r2") else np.uint64) for f in wdist.ROW_FIELDS}
         out = wdist.gather_rows(wdist.pack_rows_host(mine), rank, world)
         if rank == 0:
@@ -56,12 +59,13 @@ def _worker(rank, world, port, L, N, thr, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("by_chunk", [False, True], ids=["rows", "chunks"])
 @pytest.mark.parametrize("world,L,N,thr", [(2, 1300, 24, 0.0), (3, 900, 16, 0.02), (2, 300, 12, 2.0), (4, 600, 8, 0.0)])
-def test_gloo_shard_gather_matches_unsharded(world, L, N, thr):
+def test_gloo_shard_gather_matches_unsharded(world, L, N, thr, by_chunk):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, L, N, thr, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, L, N, thr, q, by_chunk)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -281,6 +281,34 @@ def test_sharded_runs_concatenate_to_reference_order(ctxs, kern, G):
     cat = lambda f: np.concatenate([getattr(p, f) for p in reversed(parts)])  # noqa: E731
     for f in ("site_a", "site_b", "d", "d_prime", "r2"):
         assert np.array_equal(cat(f), getattr(full, f)), f
+    # the finer chunk-range shards (wld_shard_chunks / wld_run_chunks), which
+    # split chunk rows mid-row, concatenate the same way
+    parts = []
+    for g in range(G):
+        b, e = ctx.shard_chunks(L, G, g)
+        assert ctx.run_chunks(0.0, b, e) == len(ctx.rows().site_a)
+        assert ctx.stats()["pairs"] == ctx.pairs_in_chunks(L, b, e)
+        parts.append(ctx.rows())
+    for f in ("site_a", "site_b", "d", "d_prime", "r2"):
+        assert np.array_equal(cat(f), getattr(full, f)), f
+
+
+@pytest.mark.parametrize("kern", ["mfma", "valu"])
+def test_single_chunk_runs_match_oracle(ctxs, kern):
+    """Every chunk run alone (wld_run_chunks(i, i+1)) against the oracle's chunk range."""
+    ctx = _ctx(ctxs, kern)
+    L, N = 700, 96
+    buf = synth(L, N, 5)
+    w = np.random.default_rng(3).random(N).astype(np.float32)
+    ctx.load(buf, w)
+    for i in range(ctx.chunks(L)):
+        ctx.run_chunks(0.0, i, i + 1)
+        got = ctx.rows()
+        ref = O.all_pairs(buf, w, 0.0, chunk_lo=i, chunk_hi=i + 1)
+        assert np.array_equal(got.site_a, ref["site_a"].astype(np.uint32)), i
+        assert np.array_equal(got.site_b, ref["site_b"].astype(np.uint32)), i
+        for f in ("d", "d_prime", "r2"):
+            np.testing.assert_allclose(getattr(got, f), ref[f], atol=1e-5, rtol=0, err_msg="%s chunk %d" % (f, i))
 
 
 # ------------------------------------------------------------------ API + CLI

@@ -59,9 +59,13 @@ def test_prepass_fixtures(W, name, unweighted):
 
 
 @pytest.mark.parametrize("L,N,seed,unknown", [(300, 200, 1, 0.0), (513, 333, 2, 0.03), (257, 1000, 3, 0.2),
-                                              (100, 40000, 4, 0.01)])
+                                              (100, 40000, 4, 0.01), (3, 8193, 5, 0.05), (7, 8192, 7, 0.1),
+                                              (1030, 130, 6, 0.02), (1, 65, 8, 0.1)])
 def test_prepass_synthetic(W, L, N, seed, unknown):
-    # Unknown symbols exercise the Henikoff fill term; N=40000 exceeds the LDS row stage
+    # Unknown symbols exercise the Henikoff fill term; N > 8192 exceeds a wave's
+    # LDS row stage (site_stats_kernel), L % 4 != 0 a partial site workgroup,
+    # N % 64 != 0 a partial sequence workgroup and n_kept % 256 != 0 a partial
+    # site block (henikoff_seq_kernel)
     check_equal(W, synth(L, N, seed, unknown=unknown))
 
 

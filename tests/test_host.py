@@ -187,6 +187,32 @@ def test_shard_partition(L, G):
             assert abs(pairs(b, e) - tot / G) <= 256 * L
 
 
+@pytest.mark.parametrize("L", [0, 1, 255, 256, 257, 700, 2000, 20000, 50000])
+@pytest.mark.parametrize("G", [1, 2, 3, 4, 8])
+def test_shard_chunks_partition(L, G):
+    """wld_shard_chunks: contiguous linear chunk ranges, shard 0 LAST, covering
+    all n(n+1)/2 chunks, pair counts (wld_pairs_in_chunks) summing to L(L-1)/2
+    and each within one chunk (256^2 pairs) of the even share."""
+    n = W.Context.chunk_rows(L)
+    m = W.Context.chunks(L)
+    assert m == n * (n + 1) // 2
+    spans = [W.Context.shard_chunks(L, G, g) for g in range(G)]
+    assert spans[-1][0] == 0 and spans[0][1] == m
+    for (b0, e0), (b1, e1) in zip(spans, spans[1:]):
+        assert b0 == e1 and b0 <= e0  # shard g+1 ends where shard g begins
+    pairs = [W.Context.pairs_in_chunks(L, b, e) for b, e in spans]
+    assert sum(pairs) == L * (L - 1) // 2
+    for p in pairs:
+        assert abs(p - L * (L - 1) / 2 / G) <= 256 * 256
+    # a whole-row range counts the same pairs as the row formula
+    if n:
+        lin = lambda r, c: (n - 1 - r) * (n - r) // 2 + (c - r)  # noqa: E731
+        rb, re_ = 0, max(1, n // 2)
+        a0, a1 = 0, min(L, re_ * 256)
+        assert W.Context.pairs_in_chunks(L, lin(re_ - 1, re_ - 1), lin(rb, rb) + n - rb) == \
+            sum(L - 1 - a for a in range(a0, a1))
+
+
 @pytest.mark.skipif(_gpu_present(), reason="checks the no-GPU error path")
 def test_device_entry_points_fail_loudly_without_gpu():
     with pytest.raises(W.WldError) as e:

@@ -275,6 +275,12 @@ class Context:
         check(lib().wld_run(self._h, r2_threshold, row_begin, row_end, ctypes.byref(n)), "wld_run")
         return int(n.value)
 
+    def run_chunks(self, r2_threshold, chunk_begin=0, chunk_end=0):
+        """wld_run_chunks: pairs of the linear chunk range [chunk_begin, chunk_end) (end 0 = all)."""
+        n = ctypes.c_uint64()
+        check(lib().wld_run_chunks(self._h, r2_threshold, chunk_begin, chunk_end, ctypes.byref(n)), "wld_run_chunks")
+        return int(n.value)
+
     def rows(self):
         v = Pairs()
         check(lib().wld_rows_device(self._h, ctypes.byref(v)), "wld_rows_device")
@@ -325,6 +331,21 @@ class Context:
         b, e = ctypes.c_uint32(), ctypes.c_uint32()
         check(lib().wld_shard_chunk_rows(n_sites, n_shards, shard, ctypes.byref(b), ctypes.byref(e)), "shard")
         return int(b.value), int(e.value)
+
+    @staticmethod
+    def chunks(n_sites):
+        return int(lib().wld_chunks(n_sites))
+
+    @staticmethod
+    def shard_chunks(n_sites, n_shards, shard):
+        """Linear chunk range [begin, end) of `shard` (wld_shard_chunks)."""
+        b, e = ctypes.c_uint32(), ctypes.c_uint32()
+        check(lib().wld_shard_chunks(n_sites, n_shards, shard, ctypes.byref(b), ctypes.byref(e)), "shard_chunks")
+        return int(b.value), int(e.value)
+
+    @staticmethod
+    def pairs_in_chunks(n_sites, begin, end):
+        return int(lib().wld_pairs_in_chunks(n_sites, begin, end))
 
 
 _default = {}

@@ -85,7 +85,7 @@ struct wld_ctx {
     bool loaded = false;
     size_t L = 0, N = 0, LP = 0, NP = 0;
     DevBuf raw, wraw, codes, w_pad, wstats, site_ok, site_map, planes, frag;
-    DevBuf keep, htab, site_index;  // device pre-pass (prepass.hip)
+    DevBuf keep, htab, htab_kept, site_index;  // device pre-pass (prepass.hip)
     std::vector<uint64_t> kept_map;  // parent indices of the kept sites (wld_site_map_copy)
     bool prepass_loaded = false;
     bool has_map = false;
@@ -99,7 +99,7 @@ struct wld_ctx {
     DevBuf st_a, st_b, st_d, st_dp, st_r2;
     DevBuf out_a, out_b, out_d, out_dp, out_r2;
     uint64_t st_capacity = 0;
-    uint32_t tiles_rb = ~0u, tiles_re = ~0u;
+    uint32_t tiles_lb = ~0u, tiles_le = ~0u;  // linear chunk range the tile list covers
     uint32_t n_tiles = 0;
     bool have_rows = false;
     uint64_t rows = 0;
@@ -107,7 +107,7 @@ struct wld_ctx {
 
     ~wld_ctx() {
         (void)hipSetDevice(device);
-        DevBuf *all[] = {&keep, &htab, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &tiles,
+        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &tiles,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
@@ -212,7 +212,7 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     c->stats.weight_shift = c->shift;
     c->loaded = true;
     c->have_rows = false;
-    c->tiles_rb = c->tiles_re = ~0u;
+    c->tiles_lb = c->tiles_le = ~0u;
     return WLD_OK;
 }
 
@@ -227,19 +227,70 @@ uint64_t pairs_in_rows(size_t L, uint32_t rb, uint32_t re) {
     return s;
 }
 
-int build_tiles(wld_ctx *c, uint32_t rb, uint32_t re) {
-    if (c->tiles_rb == rb && c->tiles_re == re && c->n_tiles) return WLD_OK;
+uint32_t chunks_of(size_t L) {
+    const uint32_t n = chunk_rows_of(L);
+    return n * (n + 1) / 2;
+}
+
+// (row, col) of linear chunk i: triu_index (lib.rs:623-632) in exact integers
+void chunk_of_linear_host(uint32_t n, uint32_t i, uint32_t &row, uint32_t &col) {
+    uint32_t rf = (uint32_t)((std::sqrt(8.0 * (double)i + 1.0) - 1.0) * 0.5);
+    while ((uint64_t)(rf + 1) * (rf + 2) / 2 <= i) ++rf;
+    while ((uint64_t)rf * (rf + 1) / 2 > i) --rf;
+    row = n - rf - 1;
+    col = row + i - rf * (rf + 1) / 2;
+}
+
+// pairs (a<b) of chunk (row, col): lib.rs:636-667's a/b loops
+uint64_t pairs_in_chunk(size_t L, uint32_t row, uint32_t col) {
+    auto side = [&](uint32_t r) -> uint64_t {
+        const uint64_t lo = (uint64_t)r * kChunk;
+        return lo >= L ? 0 : std::min<uint64_t>(L - lo, kChunk);
+    };
+    const uint64_t ra = side(row);
+    return row == col ? ra * (ra ? ra - 1 : 0) / 2 : ra * side(col);
+}
+
+uint64_t pairs_in_chunks(size_t L, uint32_t lb, uint32_t le) {
+    const uint32_t n = chunk_rows_of(L);
+    uint64_t s = 0;
+    for (uint32_t i = lb; i < le; ++i) {
+        uint32_t r, c;
+        chunk_of_linear_host(n, i, r, c);
+        s += pairs_in_chunk(L, r, c);
+    }
+    return s;
+}
+
+// linear chunk range of chunk rows [rb, re): rows descend in linear order
+void rows_to_linear(uint32_t n, uint32_t rb, uint32_t re, uint32_t &lb, uint32_t &le) {
+    lb = re > rb ? chunk_linear(n, re - 1, re - 1) : 0;
+    le = re > rb ? chunk_linear(n, rb, rb) + (n - rb) : 0;
+}
+
+// 64x64 tiles (tb >= ta) of the chunks [lb, le), sorted (ta, tb) so a row of
+// tiles shares its A columns in L2 as in a whole-row run
+int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
+    if (c->tiles_lb == lb && c->tiles_le == le && c->n_tiles) return WLD_OK;
     const uint32_t T_used = (uint32_t)((c->L + kTile - 1) / kTile);
+    const uint32_t n = chunk_rows_of(c->L);
     std::vector<uint32_t> t;
-    for (uint32_t ta = rb * kTilesPerChunk; ta < std::min<uint32_t>(re * kTilesPerChunk, T_used); ++ta)
-        for (uint32_t tb = ta; tb < T_used; ++tb) t.push_back((ta << 16) | tb);
+    for (uint32_t i = lb; i < le; ++i) {
+        uint32_t row, col;
+        chunk_of_linear_host(n, i, row, col);
+        for (uint32_t ta = row * kTilesPerChunk; ta < std::min<uint32_t>((row + 1) * kTilesPerChunk, T_used); ++ta)
+            for (uint32_t tb = std::max(ta, col * kTilesPerChunk);
+                 tb < std::min<uint32_t>((col + 1) * kTilesPerChunk, T_used); ++tb)
+                t.push_back((ta << 16) | tb);
+    }
+    std::sort(t.begin(), t.end());
     c->n_tiles = (uint32_t)t.size();
     WLD_TRY(ensure(c->tiles, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));
     if (!t.empty())
         HIP_TRY(hipMemcpyAsync(c->tiles.p, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    c->tiles_rb = rb;
-    c->tiles_re = re;
+    c->tiles_lb = lb;
+    c->tiles_le = le;
     return WLD_OK;
 }
 
@@ -389,9 +440,11 @@ int load_filtered(wld_ctx *c, const uint8_t *d_raw, size_t n_sites, size_t n_seq
     WLD_TRY(ensure(c->wraw, std::max<size_t>(N, 1) * sizeof(float)));
     if (unweighted)
         launch_fill_ones(ptr<float>(c->wraw), N, c->stream);
-    else
-        launch_henikoff(d_raw, ptr<uint32_t>(c->site_index), L, N, ptr<float>(c->htab), ptr<float>(c->wraw),
-                        c->stream);
+    else {
+        WLD_TRY(ensure(c->htab_kept, std::max<size_t>(L, 1) * 6 * sizeof(float)));
+        launch_henikoff(d_raw, ptr<uint32_t>(c->site_index), L, N, ptr<float>(c->htab), ptr<float>(c->htab_kept),
+                        ptr<float>(c->wraw), c->stream);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     HIP_TRY(hipEventSynchronize(c->ev[1]));
@@ -470,20 +523,47 @@ int wld_shard_chunk_rows(size_t n_sites, int n_shards, int shard, uint32_t *begi
     return WLD_OK;
 }
 
-int wld_run(wld_ctx *c, float thr, uint32_t rb, uint32_t re, uint64_t *n_rows) {
-    WLD_TRY(set_dev(c));
-    if (!c->loaded) return fail(WLD_E_STATE, "wld_run before wld_load");
+uint32_t wld_chunks(size_t n_sites) { return chunks_of(n_sites); }
+
+uint64_t wld_pairs_in_chunks(size_t n_sites, uint32_t begin, uint32_t end) {
+    return pairs_in_chunks(n_sites, begin, std::min<uint32_t>(end, chunks_of(n_sites)));
+}
+
+int wld_shard_chunks(size_t n_sites, int n_shards, int shard, uint32_t *begin, uint32_t *end) {
+    if (n_shards < 1 || shard < 0 || shard >= n_shards || !begin || !end)
+        return fail(WLD_E_ARG, "bad shard %d/%d", shard, n_shards);
+    const uint32_t m = chunks_of(n_sites), n = chunk_rows_of(n_sites);
+    std::vector<uint64_t> pre(m + 1, 0);  // pairs in linear chunks [0, i)
+    for (uint32_t i = 0; i < m; ++i) {
+        uint32_t r, c;
+        chunk_of_linear_host(n, i, r, c);
+        pre[i + 1] = pre[i] + pairs_in_chunk(n_sites, r, c);
+    }
+    // boundary j: the linear chunk whose prefix is closest to j/n_shards of the total
+    auto boundary = [&](int j) -> uint32_t {
+        if (j <= 0) return 0;
+        if (j >= n_shards) return m;
+        const long double target = (long double)pre[m] * j / n_shards;
+        uint32_t i = (uint32_t)(std::upper_bound(pre.begin(), pre.end(), (uint64_t)target) - pre.begin()) - 1;
+        if (i < m && (long double)pre[i + 1] - target < target - (long double)pre[i]) ++i;
+        return i;
+    };
+    // shard k takes the k-th range from the END of the linear order, so shards
+    // concatenate in descending shard order as with wld_shard_chunk_rows
+    *begin = boundary(n_shards - 1 - shard);
+    *end = boundary(n_shards - shard);
+    if (*end < *begin) *end = *begin;
+    return WLD_OK;
+}
+
+namespace {
+int run_chunks(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uint64_t *n_rows) {
     const uint32_t n = chunk_rows_of(c->L);
-    if (re == 0 || re > n) re = n;
-    if (rb > re) return fail(WLD_E_ARG, "row range [%u,%u) invalid", rb, re);
     c->have_rows = false;
-    WLD_TRY(build_tiles(c, rb, re));
-    const uint64_t pairs = pairs_in_rows(c->L, rb, re);
+    WLD_TRY(build_tiles(c, lin_begin, lin_end));
+    const uint64_t pairs = pairs_in_chunks(c->L, lin_begin, lin_end);
     const uint32_t T = (uint32_t)(c->LP / kTile);
     const uint32_t n_chunks = n * (n + 1) / 2;
-    // chunks of rows [rb, re): linear range [lin(re-1, re-1), lin(rb, rb) + (n-rb))
-    const uint32_t lin_begin = re > rb ? chunk_linear(n, re - 1, re - 1) : 0;
-    const uint32_t lin_end = re > rb ? chunk_linear(n, rb, rb) + (n - rb) : 0;
     const uint32_t lin_count = lin_end - lin_begin;
 
     // Staging starts at min(pairs, 32M rows) and grows to the exact need: the
@@ -564,6 +644,27 @@ int wld_run(wld_ctx *c, float thr, uint32_t rb, uint32_t re, uint64_t *n_rows) {
     if (n_rows) *n_rows = rows;
     return WLD_OK;
 }
+}  // namespace
+
+int wld_run(wld_ctx *c, float thr, uint32_t rb, uint32_t re, uint64_t *n_rows) {
+    WLD_TRY(set_dev(c));
+    if (!c->loaded) return fail(WLD_E_STATE, "wld_run before wld_load");
+    const uint32_t n = chunk_rows_of(c->L);
+    if (re == 0 || re > n) re = n;
+    if (rb > re) return fail(WLD_E_ARG, "row range [%u,%u) invalid", rb, re);
+    uint32_t lb, le;
+    rows_to_linear(n, rb, re, lb, le);
+    return run_chunks(c, thr, lb, le, n_rows);
+}
+
+int wld_run_chunks(wld_ctx *c, float thr, uint32_t chunk_begin, uint32_t chunk_end, uint64_t *n_rows) {
+    WLD_TRY(set_dev(c));
+    if (!c->loaded) return fail(WLD_E_STATE, "wld_run_chunks before wld_load");
+    const uint32_t m = chunks_of(c->L);
+    if (chunk_end == 0 || chunk_end > m) chunk_end = m;
+    if (chunk_begin > chunk_end) return fail(WLD_E_ARG, "chunk range [%u,%u) invalid", chunk_begin, chunk_end);
+    return run_chunks(c, thr, chunk_begin, chunk_end, n_rows);
+}
 
 int wld_rows_device(wld_ctx *c, wld_pairs *v) {
     if (!c || !v) return fail(WLD_E_ARG, "null argument");
@@ -614,8 +715,7 @@ int wld_dense(wld_ctx *c, float *d, float *d_prime, float *r2, uint8_t *valid) {
     const size_t L = c->L, LL = L * L;
     if (LL == 0) return WLD_OK;
     if (L > 8192) return fail(WLD_E_ARG, "wld_dense is for tests (n_sites <= 8192)");
-    const uint32_t n = chunk_rows_of(L);
-    WLD_TRY(build_tiles(c, 0, n));
+    WLD_TRY(build_tiles(c, 0, chunks_of(L)));
     DevBuf dd, ddp, dr2, dv;
     int st = WLD_OK;
     if ((st = ensure(dd, LL * 4)) || (st = ensure(ddp, LL * 4)) || (st = ensure(dr2, LL * 4)) || (st = ensure(dv, LL))) {

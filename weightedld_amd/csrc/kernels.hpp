@@ -47,7 +47,7 @@ void launch_weight_prep(const float *d_w, size_t N, size_t NP, float *w_pad, flo
 void launch_site_stats(const uint8_t *raw, size_t L, size_t N, uint32_t min_acgt, float min_minor, float max_minor,
                        uint8_t *keep, float *tab, hipStream_t s);
 void launch_henikoff(const uint8_t *raw, const uint32_t *site_index, size_t n_kept, size_t N, const float *tab,
-                     float *w, hipStream_t s);
+                     float *tabK, float *w, hipStream_t s);
 void launch_fill_ones(float *w, size_t N, hipStream_t s);
 
 // pair_valu.hip

@@ -1,8 +1,9 @@
 """Multi-GPU sharding of the pair space and the gather of passing rows.
 
-The L^2 pair space is split by contiguous 256-site chunk rows (the reference's
-chunking, lib.rs:615-634) into balanced row blocks, one per rank (one process
-per GPU).  Pairs are independent, so ranks exchange nothing while computing.
+The L^2 pair space is split into contiguous runs of the reference's 256x256
+chunk sequence (lib.rs:615-634, triu_index order), balanced by pair count at
+single-chunk granularity, one run per rank (one process per GPU); the coarser
+chunk-row split (shard_rows) is kept for callers that want whole rows.  Pairs are independent, so ranks exchange nothing while computing.
 Each rank leaves its rows on its GPU in reference order; the only collective is
 the final gather of those rows to rank 0 (RCCL over xGMI with the "nccl"
 backend; gloo in the CPU tests).  Because chunk rows DESCEND in the reference's
@@ -21,11 +22,18 @@ def shard_rows(n_sites, world, rank):
     return Context.shard_chunk_rows(n_sites, world, rank)
 
 
+def shard_chunks(n_sites, world, rank):
+    """Linear chunk range [begin, end) of this rank (balanced pair counts)."""
+    return Context.shard_chunks(n_sites, world, rank)
+
+
 def pack_rows_device(ctx, n, device):
-    """The last run's rows as one [5, n] int32 tensor on `device` (floats bit-cast)."""
+    """The last run's rows as one [5, n] int32 tensor on `device` (floats bit-cast).
+    Every element is overwritten by the copy (synchronous on the context's
+    stream), so the buffer needs no initialising kernel on torch's stream."""
     import torch
 
-    packed = torch.zeros((5, max(n, 0)), dtype=torch.int32, device=device)
+    packed = torch.empty((5, max(n, 0)), dtype=torch.int32, device=device)
     if n:
         ctx.rows_copy_device(*(packed[i].data_ptr() for i in range(5)))
     return packed
