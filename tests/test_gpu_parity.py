@@ -192,6 +192,18 @@ def test_dense_vs_oracle_many_sequences(ctxs, kern):
 
 
 @pytest.mark.parametrize("kern", KERNELS)
+def test_dense_vs_oracle_wide_sums(ctxs, kern):
+    # 66,000 sequences: NP > 65024, so the MFMA epilogue takes the wide form
+    # (S = acc0 + 2^8 acc1 + 2^16 acc2 assembled in f64, no int32 pre-combination)
+    ctx = _ctx(ctxs, kern)
+    buf = synth(40, 66000, 31)
+    import weightedld_amd as W
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ctx.load(buf, w)
+    dense_check(ctx, buf, w)
+
+
+@pytest.mark.parametrize("kern", KERNELS)
 def test_dense_mixed_sign_weights(ctxs, kern):
     # Weights are any finite f32 in lib.rs; the MFMA fixed point is signed
     # (negative balanced digits).  ~10% small negative weights keep the sums

@@ -79,6 +79,8 @@ struct wld_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
+    unsigned long long *h_cnt = nullptr;  // mapped pinned {cursor, rows} written by chunk_scan_kernel
+    unsigned long long *d_hcnt = nullptr;
     int kernel_pref = WLD_KERNEL_AUTO;
 
     // loaded SiteSet
@@ -113,6 +115,7 @@ struct wld_ctx {
         for (DevBuf *b : all) release(*b);
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
+        if (h_cnt) (void)hipHostFree(h_cnt);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -361,6 +364,13 @@ int wld_create(int device, wld_ctx **out) {
             delete c;
             return fail(WLD_E_HIP, "hipEventCreate failed");
         }
+    if (hipHostMalloc((void **)&c->h_cnt, 4 * sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void **)&c->d_hcnt, c->h_cnt, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        delete c;
+        return fail(WLD_E_HIP, "hipHostMalloc of the run counters failed");
+    }
     *out = c;
     return WLD_OK;
 }
@@ -595,23 +605,26 @@ int run_chunks(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uint
     unsigned long long h[2] = {0, 0};
     OrderArgs o;
     for (int attempt = 0; attempt < 2; ++attempt) {
-        HIP_TRY(hipMemsetAsync(c->counters.p, 0, 4 * sizeof(unsigned long long), c->stream));
-        HIP_TRY(hipMemsetAsync(c->seg_cnt.p, 0, c->LP * T, c->stream));
-        if (lin_count)
-            HIP_TRY(hipMemsetAsync(ptr<uint32_t>(c->chunk_total) + lin_begin, 0, lin_count * sizeof(uint32_t),
-                                   c->stream));
+        launch_run_init(ptr<unsigned long long>(c->counters), ptr<uint32_t>(c->chunk_total), lin_begin, lin_count,
+                        ptr<uint32_t>(c->seg_cnt), c->LP * T / 4, c->stream);
+        HIP_TRY(hipGetLastError());
         o = order_args(c);
         HIP_TRY(hipEventRecord(c->ev[2], c->stream));
         if (c->n_tiles) WLD_TRY(launch_pairs(c, thr, o, nullptr));
         HIP_TRY(hipEventRecord(c->ev[3], c->stream));
         unsigned long long *d_total = ptr<unsigned long long>(c->counters) + 1;
         if (lin_count) {
+            c->h_cnt[0] = c->h_cnt[1] = ~0ull;
             launch_chunk_scan(ptr<uint32_t>(c->chunk_total), lin_begin, lin_count, ptr<uint32_t>(c->chunk_base),
-                              d_total, c->stream);
+                              d_total, ptr<unsigned long long>(c->counters), c->d_hcnt, c->stream);
             HIP_TRY(hipGetLastError());
         }
-        HIP_TRY(hipMemcpyAsync(h, c->counters.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipEventRecord(c->ev[4], c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        if (lin_count) {
+            h[0] = __atomic_load_n(&c->h_cnt[0], __ATOMIC_ACQUIRE);
+            h[1] = __atomic_load_n(&c->h_cnt[1], __ATOMIC_ACQUIRE);
+        }
         if (h[0] <= c->st_capacity) break;
         if (attempt == 1) return fail(WLD_E_HIP, "internal: staging overflow after resize");
         WLD_TRY(grow_staging(h[0]));
@@ -623,23 +636,24 @@ int run_chunks(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uint
     WLD_TRY(ensure(c->out_d, std::max<uint64_t>(rows, 1) * 4));
     WLD_TRY(ensure(c->out_dp, std::max<uint64_t>(rows, 1) * 4));
     WLD_TRY(ensure(c->out_r2, std::max<uint64_t>(rows, 1) * 4));
-    HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+    int order_end = 4;  // with no rows the order phase ends at the scan
     if (rows && lin_count) {
         launch_gather(o, ptr<uint32_t>(c->chunk_base), lin_begin, lin_count, n, (uint32_t)c->L,
                       c->has_map ? ptr<uint32_t>(c->site_map) : nullptr, ptr<uint32_t>(c->out_a),
                       ptr<uint32_t>(c->out_b), ptr<float>(c->out_d), ptr<float>(c->out_dp), ptr<float>(c->out_r2),
                       c->stream);
         HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->ev[5], c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        order_end = 5;
     }
-    HIP_TRY(hipEventRecord(c->ev[5], c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
     c->rows = rows;
     c->have_rows = true;
     c->stats.kernel = c->kernel;
     c->stats.pairs = pairs;
     c->stats.rows = rows;
     c->stats.pair_kernel_ms = event_ms(c->ev[2], c->ev[3]);
-    c->stats.order_ms = event_ms(c->ev[3], c->ev[5]);
+    c->stats.order_ms = event_ms(c->ev[3], c->ev[order_end]);
     c->stats.pair_kernel_launches = c->n_tiles ? 1 : 0;
     if (n_rows) *n_rows = rows;
     return WLD_OK;

@@ -69,8 +69,11 @@ void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const int8_t *w
                       bool prefilter, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
 
 // order.hip
+void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t lin_begin, uint32_t lin_count,
+                     uint32_t *seg_cnt_words, size_t n_words, hipStream_t s);
 void launch_chunk_scan(const uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
-                       unsigned long long *total, hipStream_t s);
+                       unsigned long long *total, const unsigned long long *cursor, unsigned long long *host_out,
+                       hipStream_t s);
 void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,
                    uint32_t n_chunk_rows, uint32_t L, const uint32_t *site_map, uint32_t *out_a, uint32_t *out_b,
                    float *out_d, float *out_dp, float *out_r2, hipStream_t s);

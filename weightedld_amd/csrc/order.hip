@@ -10,13 +10,31 @@
 //   gather:     one workgroup per chunk; scans its 256 rows x 4 segments and
 //               copies the rows, mapping filtered site indices to parent
 //               indices through site_map (lib.rs:662-663).
+#include <algorithm>
+
 #include "pair_common.hpp"
 
 namespace wld {
 
+// Zeroes a run's counters, its chunk totals and the segment counts (one launch
+// instead of three memsets).
+__global__ __launch_bounds__(256) void run_init_kernel(unsigned long long *__restrict__ counters,
+                                                        uint32_t *__restrict__ chunk_total, uint32_t lin_begin,
+                                                        uint32_t lin_count, uint32_t *__restrict__ seg_cnt_words,
+                                                        uint32_t n_words) {
+    const uint32_t i0 = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
+    if (i0 < 4) counters[i0] = 0;
+    for (uint32_t i = i0; i < lin_count; i += stride) chunk_total[lin_begin + i] = 0;
+    for (uint32_t i = i0; i < n_words; i += stride) seg_cnt_words[i] = 0;
+}
+
+// host_out (mapped pinned host memory) receives {staging cursor, row total}:
+// the run's only device-to-host transfer, without a copy command.
 __global__ __launch_bounds__(1024) void chunk_scan_kernel(const uint32_t *__restrict__ chunk_total, uint32_t lin_begin,
                                                            uint32_t count, uint32_t *__restrict__ chunk_base,
-                                                           unsigned long long *__restrict__ total) {
+                                                           unsigned long long *__restrict__ total,
+                                                           const unsigned long long *__restrict__ cursor,
+                                                           unsigned long long *host_out) {
     __shared__ unsigned long long sw[16];
     const uint32_t tid = threadIdx.x;
     const uint32_t per = (count + 1023) / 1024;
@@ -41,6 +59,11 @@ __global__ __launch_bounds__(1024) void chunk_scan_kernel(const uint32_t *__rest
             run += t;
         }
         *total = run;
+        if (host_out) {
+            host_out[0] = *cursor;
+            host_out[1] = run;
+            __threadfence_system();
+        }
     }
     __syncthreads();
     unsigned long long base = sw[wv] + v - s;
@@ -113,9 +136,19 @@ __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t
     }
 }
 
+void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t lin_begin, uint32_t lin_count,
+                     uint32_t *seg_cnt_words, size_t n_words, hipStream_t s) {
+    const size_t n = std::max<size_t>(std::max<size_t>(n_words, lin_count), 4);
+    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(run_init_kernel, dim3(blocks), dim3(256), 0, s, counters, chunk_total, lin_begin, lin_count,
+                       seg_cnt_words, (uint32_t)n_words);
+}
+
 void launch_chunk_scan(const uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
-                       unsigned long long *total, hipStream_t s) {
-    hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(1024), 0, s, chunk_total, lin_begin, count, chunk_base, total);
+                       unsigned long long *total, const unsigned long long *cursor, unsigned long long *host_out,
+                       hipStream_t s) {
+    hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(1024), 0, s, chunk_total, lin_begin, count, chunk_base, total,
+                       cursor, host_out);
 }
 
 void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,

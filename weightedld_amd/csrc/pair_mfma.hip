@@ -220,8 +220,10 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
 }
 
 #ifdef WLD_EXP_STAMPS
-// diagnostic build only: per-tile cycle stamps of wave 0 (start, loop end, epilogue end)
-__device__ unsigned long long g_stamps[4u << 18];
+// diagnostic build only: per-tile cycle stamps of wave 0 (start, first group,
+// loop end, epilogue end) and where it ran (HW_ID | XCC_ID << 32)
+constexpr unsigned kStampWords = 5;
+__device__ unsigned long long g_stamps[kStampWords << 18];
 __device__ __forceinline__ unsigned long long stamp() {
     unsigned long long t;
     __builtin_amdgcn_sched_barrier(0);
@@ -230,7 +232,7 @@ __device__ __forceinline__ unsigned long long stamp() {
     return t;
 }
 extern "C" int wld_debug_stamps_copy(unsigned long long *out, unsigned n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), (size_t)n * 4 * 8) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), (size_t)n * kStampWords * 8) == hipSuccess ? 0 : -1;
 }
 #endif
 
@@ -432,6 +434,9 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
     v16i acc[2][3][2];
     zero_acc(acc);
     uint32_t buf = 0;
+#ifdef WLD_EXP_PRIO
+    __builtin_amdgcn_s_setprio(WLD_EXP_PRIO);  // the matrix loop outranks a partner's epilogue VALU
+#endif
 #ifdef WLD_EXP_STAMPS
     unsigned long long tsg = 0;
 #endif
@@ -445,6 +450,30 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
         if (grp + 1 < n_groups) issue(grp + 1, buf ^ 1);
         const uint8_t *gb = smem + buf * kGroupBytes;
         const uint32_t n_st = min((uint32_t)kGroup, NKB - grp * kGroup);
+#ifdef WLD_EXP_PF
+        // operands of stage st+1 are read while stage st's MFMAs run
+        auto rd = [&](uint32_t st, v4i &ca, v4i &cb, v4i &d0, v4i &d1, v4i &d2) {
+            const uint8_t *sc = gb + st * kStageCodes;
+            const uint8_t *sd = gb + kGroup * kStageCodes + st * kDigStage + h * 16;
+            ca = *reinterpret_cast<const v4i *>(sc + wa * 1024 + lane * 16);
+            cb = *reinterpret_cast<const v4i *>(sc + 2048 + wb * 1024 + lane * 16);
+            d0 = *reinterpret_cast<const v4i *>(sd);
+            d1 = *reinterpret_cast<const v4i *>(sd + 32);
+            d2 = *reinterpret_cast<const v4i *>(sd + 64);
+        };
+        v4i ca, cb, d0, d1, d2;
+        rd(0, ca, cb, d0, d1, d2);
+        for (uint32_t st = 0; st < n_st; ++st) {
+            v4i na = ca, nb = cb, n0 = d0, n1 = d1, n2 = d2;
+            if (st + 1 < n_st) rd(st + 1, na, nb, n0, n1, n2);
+            mfma_block_sel(acc, ca, cb, d0, d1, d2);
+            ca = na;
+            cb = nb;
+            d0 = n0;
+            d1 = n1;
+            d2 = n2;
+        }
+#else
         for (uint32_t st = 0; st < n_st; ++st) {
             const uint8_t *sc = gb + st * kStageCodes;
             const uint8_t *sd = gb + kGroup * kStageCodes + st * kDigStage + h * 16;
@@ -455,21 +484,28 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
             const v4i d2 = *reinterpret_cast<const v4i *>(sd + 64);
             mfma_block_sel(acc, ca, cb, d0, d1, d2);
         }
+#endif
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
         buf ^= 1;
     }
 #ifdef WLD_EXP_STAMPS
     const unsigned long long ts1 = stamp();
 #endif
+#ifdef WLD_EXP_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, shift, NP <= 65024u, o, dn,
                                     sBits, sRowBase);
 #ifdef WLD_EXP_STAMPS
     const unsigned long long ts2 = stamp();
     if (tid == 0 && blockIdx.x < (1u << 18)) {
-        g_stamps[4 * blockIdx.x] = ts0;
-        g_stamps[4 * blockIdx.x + 1] = tsg;
-        g_stamps[4 * blockIdx.x + 2] = ts1;
-        g_stamps[4 * blockIdx.x + 3] = ts2;
+        const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
+        const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
+        g_stamps[kStampWords * blockIdx.x] = ts0;
+        g_stamps[kStampWords * blockIdx.x + 1] = tsg;
+        g_stamps[kStampWords * blockIdx.x + 2] = ts1;
+        g_stamps[kStampWords * blockIdx.x + 3] = ts2;
+        g_stamps[kStampWords * blockIdx.x + 4] = hw | ((unsigned long long)xcc << 32);
     }
 #endif
 }

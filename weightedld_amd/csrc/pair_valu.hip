@@ -29,7 +29,8 @@ __global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__rest
                                                          const float *__restrict__ w,
                                                          const uint8_t *__restrict__ site_ok,
                                                          const uint32_t *__restrict__ tiles, uint32_t L, uint32_t NP,
-                                                         uint32_t n_chunk_rows, float thr, OrderArgs o, DenseArgs dn) {
+                                                         uint32_t flush, uint32_t n_chunk_rows, float thr, OrderArgs o,
+                                                         DenseArgs dn) {
     __shared__ __attribute__((aligned(16))) uint8_t sA[kTile * kStride];
     __shared__ __attribute__((aligned(16))) uint8_t sB[kTile * kStride];
     __shared__ __attribute__((aligned(16))) float sW[64];
@@ -40,11 +41,12 @@ __global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__rest
     const uint32_t tid = threadIdx.x;
     const uint32_t tx = tid & 15, ty = tid >> 4;
 
-    // Two-level summation: acc holds the current 64-sequence stage, tot the
-    // running total (tot += acc after every stage).  A plain running sum over
-    // thousands of sequences loses ~N*2^-24 relative (e.g. 5008 Henikoff
-    // weights of ~0.002 into a total of ~10); the reference's 8 lane sums
-    // (lib.rs:418-445) lose N/8*2^-24; 64-term stages lose far less than both.
+    // Two-level summation: acc holds a block of `flush` 64-sequence stages,
+    // tot the running total (tot += acc after every block).  A plain running
+    // sum over thousands of sequences loses ~N*2^-24 relative (e.g. 5008
+    // Henikoff weights of ~0.002 into a total of ~10); the reference's 8 lane
+    // sums (lib.rs:418-445) lose N/8*2^-24; blocks of ~sqrt(N) sequences
+    // (flush = round(sqrt(NP)/64), launch_pair_valu) leave ~2 sqrt(N)*2^-24.
     float acc[4][4][4], tot[4][4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -57,6 +59,7 @@ __global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__rest
     const uint8_t *gA = codes + (size_t)(a0 + lr) * NP + part * 16;
     const uint8_t *gB = codes + (size_t)(b0 + lr) * NP + part * 16;
 
+    uint32_t left = 0;  // stages until the next flush of acc into tot
     for (uint32_t k0 = 0; k0 < NP; k0 += 64) {
         const uint4 va = *reinterpret_cast<const uint4 *>(gA + k0);
         const uint4 vb = *reinterpret_cast<const uint4 *>(gB + k0);
@@ -68,12 +71,15 @@ __global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__rest
         pb[0] = vb.x; pb[1] = vb.y; pb[2] = vb.z; pb[3] = vb.w;
         if (tid < 64) sW[tid] = wv;
         __syncthreads();
+        if (left == 0) {
+            left = flush;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) acc[i][j][q] = 0.0f;
+                    for (int q = 0; q < 4; ++q) acc[i][j][q] = 0.0f;
+        }
 
 #pragma unroll 2
         for (int kk = 0; kk < 64; kk += 4) {
@@ -127,12 +133,15 @@ __global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__rest
                 }
             }
         }
+        if (--left == 0 || k0 + 64 >= NP) {
+            left = 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) tot[i][j][q] += acc[i][j][q];
+                    for (int q = 0; q < 4; ++q) tot[i][j][q] += acc[i][j][q];
+        }
     }
 
     // ---- epilogue ------------------------------------------------------
@@ -227,20 +236,21 @@ void launch_pair_valu(const uint8_t *codes, const float *w, const uint8_t *site_
                       uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, bool safe,
                       const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
     DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
+    const uint32_t flush = (uint32_t)std::max(1.0, std::floor(std::sqrt((double)NP) / 64.0 + 0.5));
     if (dense) {
         if (safe)
             hipLaunchKernelGGL((pair_valu_kernel<true, true>), dim3(n_tiles), dim3(256), 0, s, codes, w, site_ok, tiles,
-                               L, NP, n_chunk_rows, thr, o, dn);
+                               L, NP, flush, n_chunk_rows, thr, o, dn);
         else
             hipLaunchKernelGGL((pair_valu_kernel<true, false>), dim3(n_tiles), dim3(256), 0, s, codes, w, site_ok,
-                               tiles, L, NP, n_chunk_rows, thr, o, dn);
+                               tiles, L, NP, flush, n_chunk_rows, thr, o, dn);
     } else {
         if (safe)
             hipLaunchKernelGGL((pair_valu_kernel<false, true>), dim3(n_tiles), dim3(256), 0, s, codes, w, site_ok,
-                               tiles, L, NP, n_chunk_rows, thr, o, dn);
+                               tiles, L, NP, flush, n_chunk_rows, thr, o, dn);
         else
             hipLaunchKernelGGL((pair_valu_kernel<false, false>), dim3(n_tiles), dim3(256), 0, s, codes, w, site_ok,
-                               tiles, L, NP, n_chunk_rows, thr, o, dn);
+                               tiles, L, NP, flush, n_chunk_rows, thr, o, dn);
     }
 }
 

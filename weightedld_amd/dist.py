@@ -69,7 +69,7 @@ def gather_rows(packed, rank, world, group=None):
     cnt = torch.tensor([packed.shape[1]], dtype=torch.int64, device=packed.device)
     cnts = [torch.zeros_like(cnt) for _ in range(world)]
     dist.all_gather(cnts, cnt, group=group)
-    counts = [int(c.item()) for c in cnts]
+    counts = [int(c) for c in torch.cat(cnts).cpu().tolist()]  # one device sync
     m = max(counts)
     if m == 0:
         return torch.zeros((5, 0), dtype=torch.int32, device=packed.device) if rank == 0 else None
