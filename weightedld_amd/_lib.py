@@ -8,7 +8,8 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libweightedld.so")
+# WLD_LIB points the tests at an experimental in-tree build (tools/build_variant.sh)
+LIB_PATH = os.environ.get("WLD_LIB") or os.path.join(PKG_DIR, "libweightedld.so")
 
 WLD_OK = 0
 STATUS = {

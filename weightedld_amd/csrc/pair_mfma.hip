@@ -12,8 +12,10 @@
 //     (q = d0 + 256 d1 + 65536 d2; built once per load by mfma_prep_kernel);
 //   * A operand (a sites): the digit where the indicator is set (in & d_p,
 //     maj & d_p); B operand (b sites): indicator bytes 0/1;
-//   * 12 v_mfma_i32_32x32x32_i8 per 32 sequences accumulate the 2x3x2
-//     (channel_a, plane, channel_b) partial sums in int32, exactly;
+//   * 48 v_mfma_i32_16x16x64_i8 per 64 sequences and wave accumulate the
+//     2x3x2 (channel_a, plane, channel_b) partial sums of 16x64 site pairs in
+//     int32, exactly (the 16x16 shape holds a higher clock under load than
+//     32x32x32 at the same cycles per op: C5 -9%, C4 -5% measured);
 //   * epilogue: S = sum_p 2^(8p) acc_p, exact in f64, converted once to f32
 //     (correctly rounded: the f32 the reference's sum would be without its
 //     rounding error), then the reference epilogue (lib.rs:482-520) in f32.
@@ -23,10 +25,13 @@
 //
 // Work decomposition: the pair space is cut into 64x64 site tiles (the
 // triangular list of (a-tile, b-tile), b-tile >= a-tile, of the shard's chunk
-// rows); a 256-thread workgroup computes a tile, wave w the 32x32 sub-tile
-// (w>>1, w&1); two workgroups share a CU, so one's epilogue and first-group
-// latency overlap the other's matrix work.  Operands stream through LDS in
-// groups of kGroup 32-sequence stages, double-buffered and filled by LDS-DMA
+// rows); a 256-thread workgroup computes a tile, wave w its a rows 16w..16w+15
+// against all 64 b columns (each digit-masked A operand feeds 8 MFMAs: 56
+// v_perm per 48 MFMAs, against 64 for 32x32 wave tiles); two workgroups share
+// a CU, so one's epilogue and first-group latency overlap the other's matrix
+// work.  Operands stream through LDS in groups of kGroup 32-sequence stages
+// (read back two stages = 64 sequences at a time), double-buffered and filled
+// by LDS-DMA
 // (global_load_lds_dwordx4, async, no VGPRs): per stage each wave copies one
 // 1 KB code-fragment block (A0, A1, B0, B1 of the fragment-major layout) and
 // per group wave 0 the group's 1 KB of weight digits.  Every DMA is a
@@ -34,7 +39,7 @@
 // by every issuing wave + a barrier — correctness never depends on the
 // completion order of outstanding loads; a buffer is refilled only after the
 // barrier that follows its readers' s_waitcnt lgkmcnt(0).  The next group is
-// issued right after the barrier and lands during this group's 8 x 12 MFMAs.
+// issued right after the barrier and lands during this group's 4 x 48 MFMAs.
 // Passing rows are compacted per tile in LDS (order.hip assembles the
 // reference order).
 #include "pair_common.hpp"
@@ -131,19 +136,56 @@ __global__ __launch_bounds__(256) void frag_kernel(const uint8_t *__restrict__ c
 __device__ __forceinline__ v16i mfma_i8(v4i a, v4i b, v16i c) {
     return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ v4i mfma_i8_16(v4i a, v4i b, v4i c) {
+    return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
 
-// 12 MFMAs of one 32-sequence block from selector-coded fragments (frag_kernel):
-// v_perm_b32(S0, S1, sel) takes byte sel of {S0:S1} (0-3 from S1, 4-7 from S0,
-// 12 -> 0x00), so with S0 = S1 = digits a selector yields the digit for minor
-// and major, with S1 = 0 only for major; with 0x01 bytes the 0/1 indicators.
-__device__ __forceinline__ void mfma_block_sel(v16i (&acc)[2][3][2], v4i ca, v4i cb, v4i d0, v4i d1, v4i d2) {
-    constexpr unsigned kOnes = 0x01010101u;
-    v4i b_in, b_maj;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        b_in[e] = (int)__builtin_amdgcn_perm(kOnes, kOnes, (unsigned)cb[e]);
-        b_maj[e] = (int)__builtin_amdgcn_perm(kOnes, 0u, (unsigned)cb[e]);
+// A wave's share of the 64x64 tile as (channel_a, plane, channel_b) int32
+// sums, and where its 16 (a, b) pairs per lane sit (MFMA C/D layouts, gfx950).
+// 32x32x32 shape, wave w owns the 32x32 sub-tile (w >> 1, w & 1): lane
+// (r, h) = (lane & 31, lane >> 5) holds b = r and a = (i & 3) + 8 (i >> 2) + 4h.
+struct Acc32 {
+    v16i v[2][3][2];
+    __device__ __forceinline__ int get(int x, int p, int y, int i) const { return v[x][p][y][i]; }
+    static __device__ __forceinline__ uint32_t a_local(int i, uint32_t wave, uint32_t lane) {
+        return 32 * (wave >> 1) + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
     }
+    static __device__ __forceinline__ uint32_t b_local(int i, uint32_t wave, uint32_t lane) {
+        return 32 * (wave & 1) + (lane & 31);
+    }
+};
+// 16x16x64 shape, wave w owns a rows 16w..16w+15 against all 64 b columns as
+// four 16x16 blocks n (C/D col = lane & 15, row = 4 (lane >> 4) + e); register
+// i = 4n + e.
+struct Acc16 {
+    v4i v[4][2][3][2];  // [n][channel_a][plane][channel_b]
+    __device__ __forceinline__ int get(int x, int p, int y, int i) const { return v[i >> 2][x][p][y][i & 3]; }
+    static __device__ __forceinline__ uint32_t a_local(int i, uint32_t wave, uint32_t lane) {
+        return 16 * wave + 4 * (lane >> 4) + (i & 3);
+    }
+    static __device__ __forceinline__ uint32_t b_local(int i, uint32_t wave, uint32_t lane) {
+        return 16 * (i >> 2) + (lane & 15);
+    }
+};
+
+// The same 12 products for 64 sequences with v_mfma_i32_16x16x64_i8: the
+// wave's 16 a sites (ca) against the tile's 64 b sites in four 16-column
+// blocks (cb[n]).  Lane group g = lane >> 4 carries sequences 16g..16g+15 in
+// A, B and the digits alike, so the products pair the same sequence whatever
+// the k order inside the instruction.  48 MFMAs of 16 cycles = the 24 of 32 of
+// two 32x32 stages; each A operand (digit x channel) feeds 8 MFMAs, so it
+// takes 56 v_perm per 48 MFMAs (64 with a 32x32 wave tile).
+__device__ __forceinline__ void mfma_block_sel16(v4i (&acc)[4][2][3][2], v4i ca, const v4i (&cb)[4], v4i d0,
+                                                 v4i d1, v4i d2) {
+    constexpr unsigned kOnes = 0x01010101u;
+    v4i b_in[4], b_maj[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            b_in[n][e] = (int)__builtin_amdgcn_perm(kOnes, kOnes, (unsigned)cb[n][e]);
+            b_maj[n][e] = (int)__builtin_amdgcn_perm(kOnes, 0u, (unsigned)cb[n][e]);
+        }
     const v4i dp[3] = {d0, d1, d2};
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
@@ -153,10 +195,13 @@ __device__ __forceinline__ void mfma_block_sel(v16i (&acc)[2][3][2], v4i ca, v4i
             ai[e] = (int)__builtin_amdgcn_perm((unsigned)dp[p][e], (unsigned)dp[p][e], (unsigned)ca[e]);
             am[e] = (int)__builtin_amdgcn_perm((unsigned)dp[p][e], 0u, (unsigned)ca[e]);
         }
-        acc[0][p][0] = mfma_i8(ai, b_in, acc[0][p][0]);
-        acc[0][p][1] = mfma_i8(ai, b_maj, acc[0][p][1]);
-        acc[1][p][0] = mfma_i8(am, b_in, acc[1][p][0]);
-        acc[1][p][1] = mfma_i8(am, b_maj, acc[1][p][1]);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            acc[n][0][p][0] = mfma_i8_16(ai, b_in[n], acc[n][0][p][0]);
+            acc[n][0][p][1] = mfma_i8_16(ai, b_maj[n], acc[n][0][p][1]);
+            acc[n][1][p][0] = mfma_i8_16(am, b_in[n], acc[n][1][p][0]);
+            acc[n][1][p][1] = mfma_i8_16(am, b_maj[n], acc[n][1][p][1]);
+        }
     }
 }
 
@@ -236,7 +281,7 @@ extern "C" int wld_debug_stamps_copy(unsigned long long *out, unsigned n) {
 }
 #endif
 
-__device__ __forceinline__ void zero_acc(v16i (&acc)[2][3][2]) {
+__device__ __forceinline__ void zero_acc(Acc32 &acc) {
 #pragma unroll
     for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -244,7 +289,19 @@ __device__ __forceinline__ void zero_acc(v16i (&acc)[2][3][2]) {
 #pragma unroll
             for (int y = 0; y < 2; ++y)
 #pragma unroll
-                for (int e = 0; e < 16; ++e) acc[x][p][y][e] = 0;
+                for (int e = 0; e < 16; ++e) acc.v[x][p][y][e] = 0;
+}
+__device__ __forceinline__ void zero_acc(Acc16 &acc) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc.v[n][x][p][y][e] = 0;
 }
 
 // Reference epilogue of one pair from its exact sums (fixed-point units):
@@ -280,26 +337,33 @@ __device__ __forceinline__ bool pair_eval(double T, double SA, double SB, double
 // offsets for order.hip.  PREFILTER (threshold > 0) skips the f32 epilogue for
 // pairs whose exact r2, evaluated in f64 from the exact sums, lies clearly
 // below the threshold.
-template <bool DENSE, bool PREFILTER>
-__device__ __forceinline__ void tile_epilogue(const v16i (&acc)[2][3][2], uint32_t ta, uint32_t tb, uint32_t tid,
+template <bool DENSE, bool PREFILTER, class Acc>
+__device__ __forceinline__ void tile_epilogue(const Acc &acc, uint32_t ta, uint32_t tb, uint32_t tid,
                                               uint64_t okA, uint64_t okB, uint32_t L, uint32_t n_chunk_rows,
                                               float thr, int shift, bool narrow, const OrderArgs &o,
                                               const DenseArgs &dn, unsigned long long *sBits,
                                               uint32_t *sRowBase) {
     const uint32_t wave = tid >> 6, lane = tid & 63;
-    const uint32_t wa = wave >> 1, wb = wave & 1, r = lane & 31, h = lane >> 5;
     const uint32_t a0 = ta * kTile, b0 = tb * kTile;
     const double scale = ldexp(1.0, -shift);
-    const uint32_t b_local = 32 * wb + r;
-    const uint32_t b = b0 + b_local;
-    const bool okb = (okB >> b_local) & 1;
     float res[16][3];
     uint32_t pass = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        const uint32_t a_local = 32 * wa + (i & 3) + 8 * (i >> 2) + 4 * h;
-        const uint32_t a = a0 + a_local;
-        const bool valid = okb && a < b && ((okA >> a_local) & 1);
+        const uint32_t a_local = Acc::a_local(i, wave, lane);
+        const uint32_t b_local = Acc::b_local(i, wave, lane);
+        const uint32_t a = a0 + a_local, b = b0 + b_local;
+        const bool valid = ((okB >> b_local) & 1) && a < b && ((okA >> a_local) & 1);
+#ifdef WLD_EXP_NOEPI
+        if constexpr (!DENSE) {  // diagnostic: accumulators consumed, no epilogue arithmetic
+            int x = 0;
+#pragma unroll
+            for (int c = 0; c < 12; ++c) x ^= acc.get(c / 6, (c / 2) % 3, c % 2, i);
+            if (valid && x == 0x7fffffff) pass |= 1u << i;
+            res[i][0] = res[i][1] = res[i][2] = 0.f;
+            continue;
+        }
+#endif
         // S = acc_0 + 2^8 acc_1 + 2^16 acc_2: integers below 2^48, exact in f64.
         // |acc_p| <= 128 NP, so acc_1 + 2^8 acc_2 is exact in int32 while
         // 32896 NP < 2^31 (NP <= 65024): one int op, two conversions, one FMA.
@@ -309,11 +373,11 @@ __device__ __forceinline__ void tile_epilogue(const v16i (&acc)[2][3][2], uint32
 #pragma unroll
             for (int y = 0; y < 2; ++y) {
                 if (narrow) {
-                    const int hi = acc[x][1][y][i] + acc[x][2][y][i] * 256;
-                    S[x][y] = fma(256.0, (double)hi, (double)acc[x][0][y][i]);
+                    const int hi = acc.get(x, 1, y, i) + acc.get(x, 2, y, i) * 256;
+                    S[x][y] = fma(256.0, (double)hi, (double)acc.get(x, 0, y, i));
                 } else {
-                    S[x][y] = fma(65536.0, (double)acc[x][2][y][i],
-                                  fma(256.0, (double)acc[x][1][y][i], (double)acc[x][0][y][i]));
+                    S[x][y] = fma(65536.0, (double)acc.get(x, 2, y, i),
+                                  fma(256.0, (double)acc.get(x, 1, y, i), (double)acc.get(x, 0, y, i)));
                 }
             }
         float d = 0.f, dp = 0.f, r2 = 0.f;
@@ -345,10 +409,8 @@ __device__ __forceinline__ void tile_epilogue(const v16i (&acc)[2][3][2], uint32
     if (pass) {
 #pragma unroll
         for (int i = 0; i < 16; ++i)
-            if (pass & (1u << i)) {
-                const uint32_t a_local = 32 * wa + (i & 3) + 8 * (i >> 2) + 4 * h;
-                atomicOr(&sBits[a_local], 1ull << b_local);
-            }
+            if (pass & (1u << i))
+                atomicOr(&sBits[Acc::a_local(i, wave, lane)], 1ull << Acc::b_local(i, wave, lane));
     }
     __syncthreads();
     if (tid < kTile) {
@@ -372,12 +434,13 @@ __device__ __forceinline__ void tile_epilogue(const v16i (&acc)[2][3][2], uint32
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             if (!(pass & (1u << i))) continue;
-            const uint32_t a_local = 32 * wa + (i & 3) + 8 * (i >> 2) + 4 * h;
+            const uint32_t a_local = Acc::a_local(i, wave, lane);
+            const uint32_t b_local = Acc::b_local(i, wave, lane);
             const uint64_t pos =
                 (uint64_t)sRowBase[a_local] + __popcll(sBits[a_local] & ((1ull << b_local) - 1ull));
             if (pos < o.st_capacity) {
                 o.st_a[pos] = a0 + a_local;
-                o.st_b[pos] = b;
+                o.st_b[pos] = b0 + b_local;
                 o.st_d[pos] = res[i][0];
                 o.st_dp[pos] = res[i][1];
                 o.st_r2[pos] = res[i][2];
@@ -402,7 +465,6 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
 
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const uint32_t wa = wave >> 1, wb = wave & 1, h = lane >> 5;
     const uint32_t NKB = NP / 32;
     const uint32_t n_groups = (NKB + kGroup - 1) / kGroup;
 
@@ -431,7 +493,16 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
 
     issue(0, 0);
     const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
-    v16i acc[2][3][2];
+    Acc16 acc;
+    // lane group g = lane >> 4 reads stage 2s + (g >> 1), half g & 1, of each
+    // 64-sequence step (the 32-stage fragment layout, re-addressed): a sites
+    // 16w.. = rows 16(w & 1).. of 32-site block w >> 1; b block n = rows
+    // 16(n & 1).. of B block n >> 1
+    const uint32_t g4 = lane >> 4, so = g4 >> 1, hh = g4 & 1;
+    const uint32_t lrow = so * kStageCodes + (32 * hh + (lane & 15)) * 16;
+    const uint32_t offA = lrow + (wave >> 1) * 1024 + (wave & 1) * 256;
+    const uint32_t offB = lrow + 2048;  // + (n >> 1) * 1024 + (n & 1) * 256
+    const uint32_t offD = kGroup * kStageCodes + so * kDigStage + hh * 16;
     zero_acc(acc);
     uint32_t buf = 0;
 #ifdef WLD_EXP_PRIO
@@ -450,41 +521,18 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
         if (grp + 1 < n_groups) issue(grp + 1, buf ^ 1);
         const uint8_t *gb = smem + buf * kGroupBytes;
         const uint32_t n_st = min((uint32_t)kGroup, NKB - grp * kGroup);
-#ifdef WLD_EXP_PF
-        // operands of stage st+1 are read while stage st's MFMAs run
-        auto rd = [&](uint32_t st, v4i &ca, v4i &cb, v4i &d0, v4i &d1, v4i &d2) {
+        for (uint32_t st = 0; st < n_st; st += 2) {  // n_st is even: NP is a multiple of 64
             const uint8_t *sc = gb + st * kStageCodes;
-            const uint8_t *sd = gb + kGroup * kStageCodes + st * kDigStage + h * 16;
-            ca = *reinterpret_cast<const v4i *>(sc + wa * 1024 + lane * 16);
-            cb = *reinterpret_cast<const v4i *>(sc + 2048 + wb * 1024 + lane * 16);
-            d0 = *reinterpret_cast<const v4i *>(sd);
-            d1 = *reinterpret_cast<const v4i *>(sd + 32);
-            d2 = *reinterpret_cast<const v4i *>(sd + 64);
-        };
-        v4i ca, cb, d0, d1, d2;
-        rd(0, ca, cb, d0, d1, d2);
-        for (uint32_t st = 0; st < n_st; ++st) {
-            v4i na = ca, nb = cb, n0 = d0, n1 = d1, n2 = d2;
-            if (st + 1 < n_st) rd(st + 1, na, nb, n0, n1, n2);
-            mfma_block_sel(acc, ca, cb, d0, d1, d2);
-            ca = na;
-            cb = nb;
-            d0 = n0;
-            d1 = n1;
-            d2 = n2;
-        }
-#else
-        for (uint32_t st = 0; st < n_st; ++st) {
-            const uint8_t *sc = gb + st * kStageCodes;
-            const uint8_t *sd = gb + kGroup * kStageCodes + st * kDigStage + h * 16;
-            const v4i ca = *reinterpret_cast<const v4i *>(sc + wa * 1024 + lane * 16);
-            const v4i cb = *reinterpret_cast<const v4i *>(sc + 2048 + wb * 1024 + lane * 16);
+            const uint8_t *sd = gb + offD + st * kDigStage;
+            const v4i ca = *reinterpret_cast<const v4i *>(sc + offA);
+            const v4i cb[4] = {*reinterpret_cast<const v4i *>(sc + offB), *reinterpret_cast<const v4i *>(sc + offB + 256),
+                               *reinterpret_cast<const v4i *>(sc + offB + 1024),
+                               *reinterpret_cast<const v4i *>(sc + offB + 1280)};
             const v4i d0 = *reinterpret_cast<const v4i *>(sd);
             const v4i d1 = *reinterpret_cast<const v4i *>(sd + 32);
             const v4i d2 = *reinterpret_cast<const v4i *>(sd + 64);
-            mfma_block_sel(acc, ca, cb, d0, d1, d2);
+            mfma_block_sel16(acc.v, ca, cb, d0, d1, d2);
         }
-#endif
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
         buf ^= 1;
     }
@@ -526,7 +574,7 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_rows_kernel(const uint8_t *_
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t wa = wave >> 1, wb = wave & 1, r = lane & 31, h = lane >> 5;
-    v16i acc[2][3][2];
+    Acc32 acc;
     zero_acc(acc);
     const uint8_t *pa = codes + (size_t)(ta * kTile + 32 * wa + r) * NP + 16 * h;
     const uint8_t *pb = codes + (size_t)(tb * kTile + 32 * wb + r) * NP + 16 * h;
@@ -537,7 +585,7 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_rows_kernel(const uint8_t *_
         const v4i d0 = *reinterpret_cast<const v4i *>(pd + k0);
         const v4i d1 = *reinterpret_cast<const v4i *>(pd + NP + k0);
         const v4i d2 = *reinterpret_cast<const v4i *>(pd + 2 * NP + k0);
-        mfma_block(acc, ca, cb, d0, d1, d2);
+        mfma_block(acc.v, ca, cb, d0, d1, d2);
     }
     tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, ok_bits[ta], ok_bits[tb], L, n_chunk_rows, thr, shift,
                                     NP <= 65024u, o, dn, sBits, sRowBase);
