@@ -180,6 +180,7 @@ def main():
     from weightedld_amd import dist as wdist
 
     gms = []
+    row_gather = wdist.RowGather(rank, world, device)
 
     def gather(n):
         if world == 1:
@@ -187,7 +188,7 @@ def main():
         tg = time.perf_counter()
         # RCCL gather of this rank's reference-ordered rows to rank 0 (shards
         # concatenate in descending rank order: chunk rows descend)
-        rows = wdist.gather_rows(wdist.pack_rows_device(ctx, n, device), rank, world)
+        rows = row_gather(wdist.pack_rows_device(ctx, n, device))
         gms.append((time.perf_counter() - tg) * 1e3)
         return int(rows.shape[1]) if rows is not None else 0
 

@@ -57,27 +57,44 @@ def unpack_rows(packed):
             "d_prime": a[3].view(np.float32), "r2": a[4].view(np.float32)}
 
 
-def gather_rows(packed, rank, world, group=None):
-    """Gathers every rank's [5, n_r] rows to rank 0.  Returns the [5, sum n_r]
-    concatenation in reference order on rank 0 (shards in descending rank
-    order), None elsewhere.  One count all_gather + one padded gather."""
-    import torch
-    import torch.distributed as dist
+class RowGather:
+    """Per-step gather of every rank's [5, n_r] rows to rank 0, with the
+    count exchange on persistent buffers: one all_gather_into_tensor of the
+    int64 counts (no host-to-device tensor build, no list of outputs) and one
+    host read of the result; only when some rank has rows, one padded gather.
+    Rank 0 gets the [5, sum n_r] concatenation in reference order (shards in
+    descending rank order), other ranks None."""
 
-    if world == 1:
-        return packed
-    cnt = torch.tensor([packed.shape[1]], dtype=torch.int64, device=packed.device)
-    cnts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(cnts, cnt, group=group)
-    counts = [int(c) for c in torch.cat(cnts).cpu().tolist()]  # one device sync
-    m = max(counts)
-    if m == 0:
-        return torch.zeros((5, 0), dtype=torch.int32, device=packed.device) if rank == 0 else None
-    if packed.shape[1] < m:
-        pad = torch.zeros((5, m - packed.shape[1]), dtype=torch.int32, device=packed.device)
-        packed = torch.cat([packed, pad], dim=1)
-    gl = [torch.empty_like(packed) for _ in range(world)] if rank == 0 else None
-    dist.gather(packed.contiguous(), gl, dst=0, group=group)
-    if rank != 0:
-        return None
-    return torch.cat([gl[g][:, :counts[g]] for g in reversed(range(world))], dim=1)
+    def __init__(self, rank, world, device, group=None):
+        import torch
+
+        self.rank, self.world, self.group, self.device = rank, world, group, device
+        self.cnt = torch.zeros(1, dtype=torch.int64, device=device)
+        self.cnts = torch.zeros(world, dtype=torch.int64, device=device)
+
+    def __call__(self, packed):
+        import torch
+        import torch.distributed as dist
+
+        if self.world == 1:
+            return packed
+        self.cnt.fill_(packed.shape[1])
+        dist.all_gather_into_tensor(self.cnts, self.cnt, group=self.group)
+        counts = self.cnts.tolist()  # the one host sync of a step without rows
+        m = max(counts)
+        if m == 0:
+            return packed[:, :0] if self.rank == 0 else None
+        if packed.shape[1] < m:
+            pad = torch.zeros((5, m - packed.shape[1]), dtype=torch.int32, device=packed.device)
+            packed = torch.cat([packed, pad], dim=1)
+        gl = [torch.empty_like(packed) for _ in range(self.world)] if self.rank == 0 else None
+        dist.gather(packed.contiguous(), gl, dst=0, group=self.group)
+        if self.rank != 0:
+            return None
+        return torch.cat([gl[g][:, :counts[g]] for g in reversed(range(self.world))], dim=1)
+
+
+def gather_rows(packed, rank, world, group=None):
+    """One-shot RowGather: every rank's [5, n_r] rows to rank 0 in reference
+    order (shards in descending rank order), None elsewhere."""
+    return RowGather(rank, world, packed.device, group)(packed)
