@@ -126,6 +126,7 @@ def main():
     ap.add_argument("--kernel", default="auto", choices=["auto", "valu", "mfma"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--unweighted", action="store_true", help="unit weights (main.rs:150-153 --unweighted)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -151,6 +152,8 @@ def main():
     ss = W.SiteSet.from_buffer(buf)
     kept = ss.filter_sites_of_interest()  # host pre-pass (lib.rs:309-338, main.rs:139)
     weights = W.henikoff_weights(kept)  # host pre-pass (lib.rs:340-380)
+    if args.unweighted:
+        weights = np.ones(N, dtype=np.float32)
     prepass_ms = (time.perf_counter() - t0) * 1e3
     assert kept.n_sites() == L  # the synthetic distribution keeps every site
     torch.ones(1024, device=device).sum().item()  # CUDA context + allocator up before timing H2D
@@ -167,7 +170,7 @@ def main():
     pre = W.Context(local_rank, kernel)
     dev_ms = []
     for _ in range(3):
-        assert pre.load_filtered_device(d_buf.data_ptr(), L, N) == L
+        assert pre.load_filtered_device(d_buf.data_ptr(), L, N, unweighted=args.unweighted) == L
         dev_ms.append(pre.stats()["load_ms"])
     assert np.array_equal(pre.weights().view(np.uint32), weights.view(np.uint32))
     pre.close()
@@ -223,6 +226,7 @@ def main():
         kernel_ms = float(np.mean(kms))
     st = ctx.stats()
     kern_name = "mfma" if st["kernel"] == W.KERNEL_MFMA else "valu"
+    planes = st["mfma_planes"]
 
     if rank != 0:
         if world > 1:
@@ -234,7 +238,7 @@ def main():
     shard_pairs = ctx.pairs_in_chunks(L, cb, ce)
     # dominant kernel roofline (DESIGN.md "Roofline"): per-launch algorithmic work / HIP-event time
     if kern_name == "mfma":
-        ops = shard_pairs * 24.0 * N  # 3 weight planes x 4 masked products x N seqs x 2 ops/MAC
+        ops = shard_pairs * 8.0 * planes * N  # active weight planes x 4 masked products x N seqs x 2 ops/MAC
         achieved = ops / (kernel_ms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": achieved, "peak": I8_MFMA_PEAK_TOPS, "unit": "TFLOP/s",
                 "frac": achieved / I8_MFMA_PEAK_TOPS}
@@ -245,7 +249,7 @@ def main():
                 "frac": achieved / F32_VALU_PEAK_TFLOPS}
     roof["kernel"] = "pair_%s_kernel" % kern_name
     roof["kernel_ms"] = kernel_ms
-    tr = load_traffic(args.config, kern_name)
+    tr = load_traffic(args.config + ("-unweighted" if args.unweighted else ""), kern_name)
     roof["traffic"] = tr.get("hbm_bytes_per_launch") if tr else None
     hbm_alg = shard_pairs * 2.0 * N / (kernel_ms * 1e-3) / 1e9  # 2N bytes per pair
     out = {
@@ -260,9 +264,10 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "i8" if kern_name == "mfma" else "f32",
-        "data": "synthetic (seeded bench_weighted_pair_ld.rs distribution, Henikoff weights)",
+        "data": "synthetic (seeded bench_weighted_pair_ld.rs distribution, %s weights)" % (
+            "unit (--unweighted)" if args.unweighted else "Henikoff"),
         "config": {"workload": desc, "n_seqs": N, "n_sites": L, "r2_threshold": thr, "pairs": total_pairs,
-                   "rows_passing": rows, "kernel": kern_name,
+                   "rows_passing": rows, "kernel": kern_name, "mfma_planes": planes,
                    "parallelism": "chunk-range shard x%d%s" % (world, " + RCCL gather" if world > 1 else "")},
         "roofline": roof,
         "north_star_hbm_view": {"algorithmic_bytes_per_pair": 2 * N, "achieved_GBps": hbm_alg,

@@ -247,6 +247,7 @@ typedef struct {
     double load_ms;          /* HIP-event time of the encode kernel (last load)    */
     uint64_t pair_kernel_launches;
     int weight_shift;        /* fixed-point exponent of the MFMA weight planes     */
+    int mfma_planes;         /* weight-digit planes the MFMA kernel multiplies (1-3; all-zero planes skipped) */
 } wld_run_stats;
 int wld_last_stats(wld_ctx *ctx, wld_run_stats *out);
 

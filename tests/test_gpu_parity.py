@@ -240,6 +240,46 @@ def test_auto_kernel_choice(W):
     assert ctx.stats()["kernel"] == W.KERNEL_VALU
 
 
+# ------------------------------------------------------- skipped weight-digit planes
+# weights -> digit planes the MFMA kernel multiplies.  max|w| = 1 gives the
+# fixed point q = rint(w 2^22) = d0 + 256 d1 + 65536 d2 (balanced digits):
+# w = 1 -> d2 = 64 only; 3/256 -> d1 = -64, d2 = 1; 1 - 2^-22 -> d0 = -1, d2 = 64.
+PLANE_CASES = {
+    "unweighted": (lambda r, n: np.ones(n, np.float32), 1),
+    "planes_1_2": (lambda r, n: np.where(r.random(n) < 0.5, 1.0, 3 / 256).astype(np.float32), 2),
+    "planes_0_2": (lambda r, n: np.where(r.random(n) < 0.5, 1.0, 1.0 - 2.0 ** -22).astype(np.float32), 2),
+    "henikoff_like": (lambda r, n: (0.2 + 0.8 * r.random(n)).astype(np.float32), 3),
+}
+
+
+@pytest.mark.parametrize("case", sorted(PLANE_CASES))
+def test_mfma_skips_zero_digit_planes(ctxs, case, monkeypatch):
+    # The kernel multiplies only the planes with a nonzero digit (4 products
+    # each); the integer sums are the same, so every output is bit-identical
+    # to the all-planes run (WLD_ALL_PLANES=1) and agrees with the oracle.
+    ctx = _ctx(ctxs, "mfma")
+    make_w, planes = PLANE_CASES[case]
+    buf = synth(300, 700, 31)
+    w = make_w(np.random.default_rng(5), 700)
+    ctx.load(buf, w)
+    assert ctx.stats()["mfma_planes"] == planes
+    got = ctx.dense(300)
+    compare_dense(got, O.all_pairs_dense(buf, w), O.all_pairs_dense_f64(buf, w)[:3])
+    n = ctx.run(0.02)
+    rows = ctx.rows()
+    compare_rows(rows, O.all_pairs(buf, w, 0.02), 0.02, buf=buf, w=w)
+    monkeypatch.setenv("WLD_ALL_PLANES", "1")
+    ctx.load(buf, w)
+    assert ctx.stats()["mfma_planes"] == 3
+    full = ctx.dense(300)
+    iu = np.triu_indices(300, 1)
+    for g, f in zip(got, full):
+        assert np.array_equal(g[iu].view(np.uint32) if g.dtype == np.float32 else g[iu],
+                              f[iu].view(np.uint32) if f.dtype == np.float32 else f[iu])
+    assert ctx.run(0.02) == n
+    monkeypatch.delenv("WLD_ALL_PLANES")
+
+
 # ------------------------------------------------------------------ ordered rows
 @pytest.mark.parametrize("kern", KERNELS)
 @pytest.mark.parametrize("L,N,thr", [(1, 10, 0.0), (2, 10, 0.0), (255, 64, 0.0), (256, 100, 0.05), (257, 100, 0.0),

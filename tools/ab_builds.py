@@ -9,10 +9,12 @@ import statistics
 import subprocess
 import sys
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(path, config, reps, thr):
+def child(path, config, reps, thr, unweighted=False):
     sys.path.insert(0, REPO)
     import torch  # noqa: F401
     import weightedld_amd._lib as L
@@ -26,6 +28,10 @@ def child(path, config, reps, thr):
     thr = thr0 if thr is None else thr
     buf = bench.synth(Ls, N)
     w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    if unweighted:
+        w = np.ones(N, dtype=np.float32)
+    if os.environ.get("WLD_AB_WEIGHTS") == "2pl":  # two active digit planes (1 and 2)
+        w = np.where(np.random.default_rng(3).random(N) < 0.5, 1.0, 3 / 256).astype(np.float32)
     ctx = W.Context(0, W.KERNEL_MFMA)
     ctx.load(buf, w)
     ctx.run(thr)
@@ -40,7 +46,7 @@ def child(path, config, reps, thr):
         rows = ctx.run(thr)
         t.append(ctx.stats()["pair_kernel_ms"])
     out = {"ms": t, "rows": rows}
-    ops = 24.0 * ((N + 63) // 64 * 64) * (Ls * (Ls - 1) / 2)
+    ops = 8.0 * ctx.stats()["mfma_planes"] * ((N + 63) // 64 * 64) * (Ls * (Ls - 1) / 2)
     out["tops"] = ops / (sorted(t)[len(t) // 2] * 1e-3) / 1e12
     if st is not None:
         lib.wld_debug_stamps(st, 0)
@@ -57,10 +63,11 @@ def main():
     ap.add_argument("--thr", type=float)
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--unweighted", action="store_true")
     ap.add_argument("builds", nargs="*", help="name=path/to/libweightedld.so")
     a = ap.parse_args()
     if a.child:
-        return child(a.child, a.config, a.reps, a.thr)
+        return child(a.child, a.config, a.reps, a.thr, a.unweighted)
     res = {}
     for _ in range(a.rounds):
         for b in a.builds:
@@ -72,6 +79,8 @@ def main():
                     k, v = kv.split("=", 1)
                     env[k] = v
             cmd = [sys.executable, __file__, "--child", path, "--config", a.config, "--reps", str(a.reps)]
+            if a.unweighted:
+                cmd += ["--unweighted"]
             if a.thr is not None:
                 cmd += ["--thr", str(a.thr)]
             out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)

@@ -52,6 +52,7 @@ class RunStats(ctypes.Structure):
         ("load_ms", ctypes.c_double),
         ("pair_kernel_launches", ctypes.c_uint64),
         ("weight_shift", ctypes.c_int),
+        ("mfma_planes", ctypes.c_int),
     ]
 
 

@@ -95,6 +95,7 @@ struct wld_ctx {
     int kernel = WLD_KERNEL_VALU;
     bool safe = false;
     int shift = 0;
+    unsigned plane_mask = 7;  // weight-digit planes with a nonzero digit (MFMA)
 
     // run state
     DevBuf tiles, seg_cnt, seg_off, chunk_total, chunk_base, counters;
@@ -210,7 +211,11 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
         if (L) HIP_TRY(hipMemcpyAsync(c->site_map.p, m.data(), L * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
+    c->plane_mask = c->kernel == WLD_KERNEL_MFMA && !getenv("WLD_ALL_PLANES")
+                        ? mfma_plane_mask(ptr<int8_t>(c->planes), c->LP, c->NP, c->stream)
+                        : 7u;
     c->stats.load_ms = event_ms(c->ev[0], c->ev[1]);
+    c->stats.mfma_planes = c->kernel == WLD_KERNEL_MFMA ? __builtin_popcount(c->plane_mask) : 0;
     c->stats.kernel = c->kernel;
     c->stats.weight_shift = c->shift;
     c->loaded = true;
@@ -321,7 +326,7 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         const bool prefilter = thr > 0.0f && !getenv("WLD_NO_PREFILTER");
         launch_pair_mfma(ptr<uint8_t>(c->codes), c->use_frag ? ptr<uint8_t>(c->frag) : nullptr,
                          ptr<int8_t>(c->planes), ptr<uint32_t>(c->tiles), c->n_tiles, (uint32_t)c->L,
-                         (uint32_t)c->NP, n, thr, c->shift, prefilter, o, dense, c->stream);
+                         (uint32_t)c->NP, n, thr, c->shift, c->plane_mask, prefilter, o, dense, c->stream);
     } else
         launch_pair_valu(ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), ptr<uint8_t>(c->site_ok),
                          ptr<uint32_t>(c->tiles), c->n_tiles, (uint32_t)c->L, (uint32_t)c->NP, n, thr, c->safe, o,

@@ -64,9 +64,14 @@ void launch_mfma_prep(const uint8_t *site_ok, const float *w_pad, size_t L, size
 void launch_frag(const uint8_t *codes, size_t LP, size_t NP, uint8_t *frag, hipStream_t s);
 // frag != nullptr: LDS-streaming kernel on the fragment-major copy; else the
 // site-major kernel
+// plane_mask: the weight-digit planes with a nonzero digit (mfma_plane_mask);
+// the LDS kernel runs 4 MFMA products per active plane
 void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const int8_t *wplanes, const uint32_t *tiles,
                       uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
-                      bool prefilter, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
+                      unsigned plane_mask, bool prefilter, const OrderArgs &o, const DenseArgs *dense,
+                      hipStream_t s);
+// after launch_mfma_prep on stream s: bit p = plane p has a nonzero digit (synchronises s)
+unsigned mfma_plane_mask(const int8_t *wplanes, size_t LP, size_t NP, hipStream_t s);
 
 // order.hip
 void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t lin_begin, uint32_t lin_count,

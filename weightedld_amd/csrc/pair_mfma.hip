@@ -74,12 +74,16 @@ __host__ __device__ inline size_t digf_stage(uint32_t kb) { return (size_t)(kb /
 //                                         per 32-sequence stage, 1 KB per group
 //                                         (LDS path; k = 32kb + 16h + j)
 //   ok_bits[g] bit i = site 64g+i passes  (site_ok, lib.rs:400-408)
-size_t mfma_planes_bytes(size_t LP, size_t NP) { return okbits_offset(NP) + LP / 64 * 8; }
+//   plane_mask (u32 after the bits)       bit p = some digit of plane p is nonzero
+__host__ __device__ inline size_t planemask_offset(size_t LP, size_t NP) { return okbits_offset(NP) + LP / 64 * 8; }
+size_t mfma_planes_bytes(size_t LP, size_t NP) { return planemask_offset(LP, NP) + 16; }
 
 __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict__ w_pad, uint32_t NP, int shift,
-                                                         int8_t *__restrict__ planes, int8_t *__restrict__ digf) {
+                                                         int8_t *__restrict__ planes, int8_t *__restrict__ digf,
+                                                         unsigned *__restrict__ plane_mask) {
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
     if (k >= NP) return;
+    unsigned used = 0;
     long long q = llrint(ldexp((double)w_pad[k], shift));
     const uint32_t kb = k >> 5, h = (k >> 4) & 1, j = k & 15;
 #pragma unroll
@@ -88,7 +92,9 @@ __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict_
         q = (q - r) / 256;
         planes[p * NP + k] = (int8_t)r;
         digf[digf_stage(kb) + (2 * p + h) * 16 + j] = (int8_t)r;
+        used |= (r != 0) << p;
     }
+    if (used) atomicOr(plane_mask, used);
 }
 
 // one wave per 64 sites
@@ -144,8 +150,10 @@ __device__ __forceinline__ v4i mfma_i8_16(v4i a, v4i b, v4i c) {
 // sums, and where its 16 (a, b) pairs per lane sit (MFMA C/D layouts, gfx950).
 // 32x32x32 shape, wave w owns the 32x32 sub-tile (w >> 1, w & 1): lane
 // (r, h) = (lane & 31, lane >> 5) holds b = r and a = (i & 3) + 8 (i >> 2) + 4h.
+template <int NPL>
 struct Acc32 {
-    v16i v[2][3][2];
+    static constexpr int kPlanes = NPL;
+    v16i v[2][NPL][2];  // [channel_a][plane][channel_b]
     __device__ __forceinline__ int get(int x, int p, int y, int i) const { return v[x][p][y][i]; }
     static __device__ __forceinline__ uint32_t a_local(int i, uint32_t wave, uint32_t lane) {
         return 32 * (wave >> 1) + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
@@ -156,9 +164,12 @@ struct Acc32 {
 };
 // 16x16x64 shape, wave w owns a rows 16w..16w+15 against all 64 b columns as
 // four 16x16 blocks n (C/D col = lane & 15, row = 4 (lane >> 4) + e); register
-// i = 4n + e.
+// i = 4n + e.  NPL = the weight-digit planes that are not all zero (3 for
+// general weights, 1 for equal weights, e.g. --unweighted).
+template <int NPL>
 struct Acc16 {
-    v4i v[4][2][3][2];  // [n][channel_a][plane][channel_b]
+    static constexpr int kPlanes = NPL;
+    v4i v[4][2][NPL][2];  // [n][channel_a][plane][channel_b]
     __device__ __forceinline__ int get(int x, int p, int y, int i) const { return v[i >> 2][x][p][y][i & 3]; }
     static __device__ __forceinline__ uint32_t a_local(int i, uint32_t wave, uint32_t lane) {
         return 16 * wave + 4 * (lane >> 4) + (i & 3);
@@ -175,8 +186,9 @@ struct Acc16 {
 // the k order inside the instruction.  48 MFMAs of 16 cycles = the 24 of 32 of
 // two 32x32 stages; each A operand (digit x channel) feeds 8 MFMAs, so it
 // takes 56 v_perm per 48 MFMAs (64 with a 32x32 wave tile).
-__device__ __forceinline__ void mfma_block_sel16(v4i (&acc)[4][2][3][2], v4i ca, const v4i (&cb)[4], v4i d0,
-                                                 v4i d1, v4i d2) {
+template <int NPL>
+__device__ __forceinline__ void mfma_block_sel16(v4i (&acc)[4][2][NPL][2], v4i ca, const v4i (&cb)[4],
+                                                 const v4i (&dp)[NPL]) {
     constexpr unsigned kOnes = 0x01010101u;
     v4i b_in[4], b_maj[4];
 #pragma unroll
@@ -186,9 +198,8 @@ __device__ __forceinline__ void mfma_block_sel16(v4i (&acc)[4][2][3][2], v4i ca,
             b_in[n][e] = (int)__builtin_amdgcn_perm(kOnes, kOnes, (unsigned)cb[n][e]);
             b_maj[n][e] = (int)__builtin_amdgcn_perm(kOnes, 0u, (unsigned)cb[n][e]);
         }
-    const v4i dp[3] = {d0, d1, d2};
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
+    for (int p = 0; p < NPL; ++p) {
         v4i ai, am;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -281,23 +292,25 @@ extern "C" int wld_debug_stamps_copy(unsigned long long *out, unsigned n) {
 }
 #endif
 
-__device__ __forceinline__ void zero_acc(Acc32 &acc) {
+template <int NPL>
+__device__ __forceinline__ void zero_acc(Acc32<NPL> &acc) {
 #pragma unroll
     for (int x = 0; x < 2; ++x)
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NPL; ++p)
 #pragma unroll
             for (int y = 0; y < 2; ++y)
 #pragma unroll
                 for (int e = 0; e < 16; ++e) acc.v[x][p][y][e] = 0;
 }
-__device__ __forceinline__ void zero_acc(Acc16 &acc) {
+template <int NPL>
+__device__ __forceinline__ void zero_acc(Acc16<NPL> &acc) {
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int x = 0; x < 2; ++x)
 #pragma unroll
-            for (int p = 0; p < 3; ++p)
+            for (int p = 0; p < NPL; ++p)
 #pragma unroll
                 for (int y = 0; y < 2; ++y)
 #pragma unroll
@@ -340,10 +353,13 @@ __device__ __forceinline__ bool pair_eval(double T, double SA, double SB, double
 template <bool DENSE, bool PREFILTER, class Acc>
 __device__ __forceinline__ void tile_epilogue(const Acc &acc, uint32_t ta, uint32_t tb, uint32_t tid,
                                               uint64_t okA, uint64_t okB, uint32_t L, uint32_t n_chunk_rows,
-                                              float thr, int shift, bool narrow, const OrderArgs &o,
-                                              const DenseArgs &dn, unsigned long long *sBits,
+                                              float thr, int shift, bool narrow, uint32_t plane_idx,
+                                              const OrderArgs &o, const DenseArgs &dn, unsigned long long *sBits,
                                               uint32_t *sRowBase) {
     const uint32_t wave = tid >> 6, lane = tid & 63;
+    double pscale[Acc::kPlanes];  // 2^(8 idx_j) of the j-th active plane (plane_idx: 2 bits per plane)
+#pragma unroll
+    for (int j = 0; j < Acc::kPlanes; ++j) pscale[j] = (double)(1u << (8 * ((plane_idx >> (2 * j)) & 3)));
     const uint32_t a0 = ta * kTile, b0 = tb * kTile;
     const double scale = ldexp(1.0, -shift);
     float res[16][3];
@@ -358,7 +374,8 @@ __device__ __forceinline__ void tile_epilogue(const Acc &acc, uint32_t ta, uint3
         if constexpr (!DENSE) {  // diagnostic: accumulators consumed, no epilogue arithmetic
             int x = 0;
 #pragma unroll
-            for (int c = 0; c < 12; ++c) x ^= acc.get(c / 6, (c / 2) % 3, c % 2, i);
+            for (int c = 0; c < 4 * Acc::kPlanes; ++c)
+                x ^= acc.get(c / (2 * Acc::kPlanes), (c / 2) % Acc::kPlanes, c % 2, i);
             if (valid && x == 0x7fffffff) pass |= 1u << i;
             res[i][0] = res[i][1] = res[i][2] = 0.f;
             continue;
@@ -367,12 +384,18 @@ __device__ __forceinline__ void tile_epilogue(const Acc &acc, uint32_t ta, uint3
         // S = acc_0 + 2^8 acc_1 + 2^16 acc_2: integers below 2^48, exact in f64.
         // |acc_p| <= 128 NP, so acc_1 + 2^8 acc_2 is exact in int32 while
         // 32896 NP < 2^31 (NP <= 65024): one int op, two conversions, one FMA.
+        // With fewer planes (all-zero digit planes skipped) S = sum_j 2^(8 idx_j) acc_j.
         double S[2][2];
 #pragma unroll
         for (int x = 0; x < 2; ++x)
 #pragma unroll
             for (int y = 0; y < 2; ++y) {
-                if (narrow) {
+                if constexpr (Acc::kPlanes < 3) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int j = 0; j < Acc::kPlanes; ++j) v = fma(pscale[j], (double)acc.get(x, j, y, i), v);
+                    S[x][y] = v;
+                } else if (narrow) {
                     const int hi = acc.get(x, 1, y, i) + acc.get(x, 2, y, i) * 256;
                     S[x][y] = fma(256.0, (double)hi, (double)acc.get(x, 0, y, i));
                 } else {
@@ -452,13 +475,13 @@ __device__ __forceinline__ void tile_epilogue(const Acc &acc, uint32_t ta, uint3
 // LDS-streaming kernel over fragment-major, selector-coded codes: one 64x64
 // tile per workgroup.  (An XCD-contiguous block->tile remap measured no gain:
 // the 41 MB code copy of BASELINE config 4 is served from L2/MALL either way.)
-template <bool DENSE, bool PREFILTER>
+template <bool DENSE, bool PREFILTER, int NPL>
 __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__restrict__ frag,
                                                             const int8_t *__restrict__ planes,
                                                             const uint64_t *__restrict__ ok_bits,
                                                             const uint32_t *__restrict__ tiles, uint32_t L,
                                                             uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
-                                                            OrderArgs o, DenseArgs dn) {
+                                                            uint32_t plane_idx, OrderArgs o, DenseArgs dn) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kGroupBytes];  // operand groups (DMA targets)
     __shared__ unsigned long long sBits[kTile];                              // compaction (never a DMA target)
     __shared__ uint32_t sRowBase[kTile];
@@ -493,7 +516,7 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
 
     issue(0, 0);
     const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
-    Acc16 acc;
+    Acc16<NPL> acc;
     // lane group g = lane >> 4 reads stage 2s + (g >> 1), half g & 1, of each
     // 64-sequence step (the 32-stage fragment layout, re-addressed): a sites
     // 16w.. = rows 16(w & 1).. of 32-site block w >> 1; b block n = rows
@@ -503,6 +526,9 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
     const uint32_t offA = lrow + (wave >> 1) * 1024 + (wave & 1) * 256;
     const uint32_t offB = lrow + 2048;  // + (n >> 1) * 1024 + (n & 1) * 256
     const uint32_t offD = kGroup * kStageCodes + so * kDigStage + hh * 16;
+    uint32_t offP[NPL];  // the active planes' 32-byte rows of a stage's digit record
+#pragma unroll
+    for (int j = 0; j < NPL; ++j) offP[j] = offD + 32 * ((plane_idx >> (2 * j)) & 3);
     zero_acc(acc);
     uint32_t buf = 0;
 #ifdef WLD_EXP_PRIO
@@ -523,15 +549,15 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
         const uint32_t n_st = min((uint32_t)kGroup, NKB - grp * kGroup);
         for (uint32_t st = 0; st < n_st; st += 2) {  // n_st is even: NP is a multiple of 64
             const uint8_t *sc = gb + st * kStageCodes;
-            const uint8_t *sd = gb + offD + st * kDigStage;
+            const uint8_t *sd = gb + st * kDigStage;
             const v4i ca = *reinterpret_cast<const v4i *>(sc + offA);
             const v4i cb[4] = {*reinterpret_cast<const v4i *>(sc + offB), *reinterpret_cast<const v4i *>(sc + offB + 256),
                                *reinterpret_cast<const v4i *>(sc + offB + 1024),
                                *reinterpret_cast<const v4i *>(sc + offB + 1280)};
-            const v4i d0 = *reinterpret_cast<const v4i *>(sd);
-            const v4i d1 = *reinterpret_cast<const v4i *>(sd + 32);
-            const v4i d2 = *reinterpret_cast<const v4i *>(sd + 64);
-            mfma_block_sel16(acc.v, ca, cb, d0, d1, d2);
+            v4i dp[NPL];
+#pragma unroll
+            for (int j = 0; j < NPL; ++j) dp[j] = *reinterpret_cast<const v4i *>(sd + offP[j]);
+            mfma_block_sel16<NPL>(acc.v, ca, cb, dp);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
         buf ^= 1;
@@ -542,8 +568,8 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
 #ifdef WLD_EXP_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
-    tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, shift, NP <= 65024u, o, dn,
-                                    sBits, sRowBase);
+    tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, shift, NP <= 65024u,
+                                    plane_idx, o, dn, sBits, sRowBase);
 #ifdef WLD_EXP_STAMPS
     const unsigned long long ts2 = stamp();
     if (tid == 0 && blockIdx.x < (1u << 18)) {
@@ -574,7 +600,7 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_rows_kernel(const uint8_t *_
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t wa = wave >> 1, wb = wave & 1, r = lane & 31, h = lane >> 5;
-    Acc32 acc;
+    Acc32<3> acc;
     zero_acc(acc);
     const uint8_t *pa = codes + (size_t)(ta * kTile + 32 * wa + r) * NP + 16 * h;
     const uint8_t *pb = codes + (size_t)(tb * kTile + 32 * wb + r) * NP + 16 * h;
@@ -588,13 +614,15 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_rows_kernel(const uint8_t *_
         mfma_block(acc.v, ca, cb, d0, d1, d2);
     }
     tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, ok_bits[ta], ok_bits[tb], L, n_chunk_rows, thr, shift,
-                                    NP <= 65024u, o, dn, sBits, sRowBase);
+                                    NP <= 65024u, 0x24u, o, dn, sBits, sRowBase);
 }
 
 void launch_mfma_prep(const uint8_t *site_ok, const float *w_pad, size_t L, size_t LP, size_t NP, int shift,
                       int8_t *planes, hipStream_t s) {
+    unsigned *mask = reinterpret_cast<unsigned *>(planes + planemask_offset(LP, NP));
+    (void)hipMemsetAsync(mask, 0, sizeof(unsigned), s);
     hipLaunchKernelGGL(mfma_prep_kernel, dim3((unsigned)((NP + 255) / 256)), dim3(256), 0, s, w_pad, (uint32_t)NP,
-                       shift, planes, planes + digf_offset(NP));
+                       shift, planes, planes + digf_offset(NP), mask);
     hipLaunchKernelGGL(okbits_kernel, dim3((unsigned)(LP / 64)), dim3(64), 0, s, site_ok, (uint32_t)L,
                        reinterpret_cast<uint64_t *>(planes + okbits_offset(NP)));
 }
@@ -605,22 +633,55 @@ void launch_frag(const uint8_t *codes, size_t LP, size_t NP, uint8_t *frag, hipS
                        (uint32_t)NP, frag);
 }
 
+template <int NPL>
+void launch_lds(const uint8_t *frag, const int8_t *wplanes, const uint64_t *ok_bits, const uint32_t *tiles,
+                uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
+                uint32_t plane_idx, bool prefilter, const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
+    const DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
+    const dim3 g(n_tiles), b(256);
+    if (dense)
+        hipLaunchKernelGGL((pair_mfma_kernel<true, false, NPL>), g, b, 0, s, frag, wplanes, ok_bits, tiles, L,
+                           NP, n_chunk_rows, thr, shift, plane_idx, o, dn);
+    else if (prefilter)
+        hipLaunchKernelGGL((pair_mfma_kernel<false, true, NPL>), g, b, 0, s, frag, wplanes, ok_bits, tiles, L,
+                           NP, n_chunk_rows, thr, shift, plane_idx, o, dn);
+    else
+        hipLaunchKernelGGL((pair_mfma_kernel<false, false, NPL>), g, b, 0, s, frag, wplanes, ok_bits, tiles, L,
+                           NP, n_chunk_rows, thr, shift, plane_idx, o, dn);
+}
+
+unsigned mfma_plane_mask(const int8_t *wplanes, size_t LP, size_t NP, hipStream_t s) {
+    unsigned m = 7;
+    if (hipMemcpyAsync(&m, wplanes + planemask_offset(LP, NP), sizeof(m), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return 7;  // all planes: always correct
+    return m & 7;
+}
+
 void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const int8_t *wplanes, const uint32_t *tiles,
                       uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
-                      bool prefilter, const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
+                      unsigned plane_mask, bool prefilter, const OrderArgs &o, const DenseArgs *dense,
+                      hipStream_t s) {
     const DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
     const uint64_t *ok_bits = reinterpret_cast<const uint64_t *>(wplanes + okbits_offset(NP));
     const dim3 g(n_tiles), b(256);
     if (frag) {
-        if (dense)
-            hipLaunchKernelGGL((pair_mfma_kernel<true, false>), g, b, 0, s, frag, wplanes, ok_bits, tiles, L, NP,
-                               n_chunk_rows, thr, shift, o, dn);
-        else if (prefilter)
-            hipLaunchKernelGGL((pair_mfma_kernel<false, true>), g, b, 0, s, frag, wplanes, ok_bits, tiles, L, NP,
-                               n_chunk_rows, thr, shift, o, dn);
+        // the nonzero digit planes in ascending order, 2 bits each; no plane is
+        // all zero only if some weight is nonzero, which the caller guarantees
+        plane_mask &= 7;
+        if (!plane_mask) plane_mask = 7;
+        uint32_t idx = 0, n = 0;
+        for (uint32_t p = 0; p < 3; ++p)
+            if (plane_mask >> p & 1) idx |= p << (2 * n++);
+        if (n == 3)
+            launch_lds<3>(frag, wplanes, ok_bits, tiles, n_tiles, L, NP, n_chunk_rows, thr, shift, idx, prefilter, o,
+                          dense, s);
+        else if (n == 2)
+            launch_lds<2>(frag, wplanes, ok_bits, tiles, n_tiles, L, NP, n_chunk_rows, thr, shift, idx, prefilter, o,
+                          dense, s);
         else
-            hipLaunchKernelGGL((pair_mfma_kernel<false, false>), g, b, 0, s, frag, wplanes, ok_bits, tiles, L, NP,
-                               n_chunk_rows, thr, shift, o, dn);
+            launch_lds<1>(frag, wplanes, ok_bits, tiles, n_tiles, L, NP, n_chunk_rows, thr, shift, idx, prefilter, o,
+                          dense, s);
     } else {
         if (dense)
             hipLaunchKernelGGL((pair_mfma_rows_kernel<true, false>), g, b, 0, s, codes, wplanes, ok_bits, tiles, L,
