@@ -183,21 +183,19 @@ def main():
     from weightedld_amd import dist as wdist
 
     gms = []
-    row_gather = wdist.RowGather(rank, world, device)
-
-    def gather(n):
-        if world == 1:
-            return n
-        tg = time.perf_counter()
-        # RCCL gather of this rank's reference-ordered rows to rank 0 (shards
-        # concatenate in descending rank order: chunk rows descend)
-        rows = row_gather(wdist.pack_rows_device(ctx, n, device))
-        gms.append((time.perf_counter() - tg) * 1e3)
-        return int(rows.shape[1]) if rows is not None else 0
+    # N>1: the shard's pair kernel and row count on the library's stream, the
+    # RCCL count all_gather ordered after them on that stream, one host wait;
+    # rows (if any) then gathered to rank 0 in reference order (shards
+    # concatenate in descending rank order: chunk rows descend)
+    shard_step = wdist.ShardStep(ctx, rank, world, device)
 
     def step():
-        n = ctx.run_chunks(thr, cb, ce)
-        return gather(n)
+        if world == 1:
+            return ctx.run_chunks(thr, cb, ce)
+        tg = time.perf_counter()
+        _, rows = shard_step(thr, cb, ce)
+        gms.append((time.perf_counter() - tg) * 1e3 - ctx.stats()["pair_kernel_ms"])
+        return int(rows.shape[1]) if rows is not None else 0
 
     for _ in range(args.warmup):
         step()
@@ -277,7 +275,7 @@ def main():
         "phases_ms": {"host_prepass_filter_henikoff": prepass_ms,
                       "device_prepass_filter_henikoff_encode": float(min(dev_ms)), "h2d_inputs": h2d_ms,
                       "device_encode_prep": load_ms, "pair_kernel": kernel_ms, "order_assembly": float(np.mean(oms)),
-                      "gather_rank0": float(np.mean(gms)) if gms else 0.0},
+                      "step_minus_kernel_rank0": float(np.mean(gms)) if gms else 0.0},
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(buf, weights, thr, args.cpu_seconds)

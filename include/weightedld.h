@@ -223,6 +223,18 @@ int wld_run(wld_ctx *ctx, float r2_threshold, uint32_t row_begin, uint32_t row_e
  * par_iter over 0..n(n+1)/2, lib.rs:621-683, restricted to a sub-range). */
 int wld_run_chunks(wld_ctx *ctx, float r2_threshold, uint32_t chunk_begin, uint32_t chunk_end,
                    uint64_t *n_rows);
+/* The same run in two calls, for callers that overlap it with a collective:
+ * wld_run_chunks_async enqueues the pair kernel and the row count on the
+ * context's stream (wld_stream) and returns without waiting; when
+ * d_count_out (device, 8 bytes) is given the run's row total lands there as a
+ * uint64 on that stream.  wld_run_wait completes the run (host wait, staging
+ * regrowth, reference-order assembly) exactly as wld_run_chunks would.  No
+ * other call may touch the context in between. */
+int wld_run_chunks_async(wld_ctx *ctx, float r2_threshold, uint32_t chunk_begin, uint32_t chunk_end,
+                         void *d_count_out);
+int wld_run_wait(wld_ctx *ctx, uint64_t *n_rows);
+/* The context's HIP stream (hipStream_t), for ordering caller work after a run. */
+void *wld_stream(wld_ctx *ctx);
 /* Device pointers of the last run's rows (valid until the next run/load or
  * destroy; do not free). */
 int wld_rows_device(wld_ctx *ctx, wld_pairs *view);

@@ -540,3 +540,70 @@ def test_config5_full_size_properties(W):
     ctx.load(sub, w)
     ctx.run(float("-inf"))
     compare_rows(ctx.rows(), O.all_pairs(sub, w, float("-inf")), float("-inf"), buf=sub, w=w)
+
+
+# ------------------------------------------------------------ async run + ShardStep
+def test_run_chunks_async_matches_sync(W, ctxs, monkeypatch):
+    # wld_run_chunks_async + wld_run_wait == wld_run_chunks: same rows, the row
+    # total in the caller's device word, the staging-regrow re-run inside
+    # run_wait, and an empty range writing 0.
+    import torch
+
+    ctx = _ctx(ctxs, "mfma")
+    L, N = 900, 300
+    buf = synth(L, N, 77)
+    w = np.random.default_rng(3).random(N).astype(np.float32) + 0.1
+    ctx.load(buf, w)
+    cnt = torch.full((1,), -1, dtype=torch.int64, device="cuda:0")
+    for thr, init_rows in ((0.0, None), (0.01, None), (0.0, "1000")):
+        if init_rows:
+            monkeypatch.setenv("WLD_INITIAL_STAGING_ROWS", init_rows)
+            ctx.load(buf, w)  # fresh staging sized by the env
+        ctx.run_chunks_async(thr, 0, 0, cnt.data_ptr())  # first: with tiny staging it must regrow
+        n = ctx.run_wait()
+        torch.cuda.synchronize()
+        got = ctx.rows()
+        n_ref = ctx.run_chunks(thr, 0, 0)
+        ref = ctx.rows()
+        assert n == n_ref == int(cnt.item())
+        for f in ("site_a", "site_b", "d", "d_prime", "r2"):
+            assert np.array_equal(getattr(got, f).view(np.uint32), getattr(ref, f).view(np.uint32)), f
+        if init_rows:
+            monkeypatch.delenv("WLD_INITIAL_STAGING_ROWS")
+    ctx.run_chunks_async(0.0, 3, 3, cnt.data_ptr())
+    assert ctx.run_wait() == 0
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == 0
+    with pytest.raises(W.WldError):
+        ctx.run_wait()  # nothing in flight
+
+
+def test_shard_step_world1_rccl(W, ctxs):
+    # ShardStep (the bench's N>1 step) through a real world-1 RCCL group: the
+    # count all_gather ordered on the library's stream, then the rows.
+    import torch
+    import torch.distributed as dist
+    from weightedld_amd import dist as wdist
+
+    ctx = _ctx(ctxs, "mfma")
+    L, N = 700, 256
+    buf = synth(L, N, 78)
+    w = np.random.default_rng(4).random(N).astype(np.float32) + 0.1
+    ctx.load(buf, w)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29561")
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        step = wdist.ShardStep(ctx, 0, 1, dev)
+        for thr in (0.0, 0.02, 2.0):
+            ref = O.all_pairs(buf, w, thr)
+            for _ in range(2):
+                n, rows = step(thr, 0, 0)
+                got = wdist.unpack_rows(rows)
+                assert n == rows.shape[1]
+                assert list(zip(got["site_a"].tolist(), got["site_b"].tolist())) == \
+                    list(zip(ref["site_a"].tolist(), ref["site_b"].tolist()))
+                assert np.abs(got["r2"].astype(np.float64) - ref["r2"]).max(initial=0.0) < 1e-5
+    finally:
+        dist.destroy_process_group()

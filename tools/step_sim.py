@@ -30,6 +30,7 @@ ctx.load(buf, w)
 b, e = ctx.shard_chunks(L, 8, 0)
 rg = wdist.RowGather(0, 1, dev)
 rg.world = 2  # force the collective path (the count buffers stay world-1 sized)
+ss = wdist.ShardStep(ctx, 0, 1, dev)  # world-1 group: the same collective calls
 
 
 def old_gather(packed):
@@ -43,6 +44,7 @@ variants = {
     "run only": lambda: ctx.run_chunks(thr, b, e),
     "run + RowGather": lambda: rg(wdist.pack_rows_device(ctx, ctx.run_chunks(thr, b, e), dev)),
     "run + old all_gather": lambda: old_gather(wdist.pack_rows_device(ctx, ctx.run_chunks(thr, b, e), dev)),
+    "ShardStep (async)": lambda: ss(thr, b, e),
 }
 for name, f in variants.items():
     for _ in range(20):

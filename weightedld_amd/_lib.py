@@ -108,6 +108,9 @@ SIGNATURES = {
     "wld_shard_chunks": (_int, [_sz, _int, _int, _u32p, _u32p]),
     "wld_pairs_in_chunks": (ctypes.c_uint64, [_sz, ctypes.c_uint32, ctypes.c_uint32]),
     "wld_run_chunks": (_int, [_vp, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint32, _u64p]),
+    "wld_run_chunks_async": (_int, [_vp, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint32, _vp]),
+    "wld_run_wait": (_int, [_vp, _u64p]),
+    "wld_stream": (_vp, [_vp]),
     "wld_rows_device": (_int, [_vp, ctypes.POINTER(Pairs)]),
     "wld_rows_copy": (_int, [_vp, _u32p, _u32p, _f32p, _f32p, _f32p]),
     "wld_rows_copy_device": (_int, [_vp, _vp, _vp, _vp, _vp, _vp]),

@@ -281,6 +281,24 @@ class Context:
         check(lib().wld_run_chunks(self._h, r2_threshold, chunk_begin, chunk_end, ctypes.byref(n)), "wld_run_chunks")
         return int(n.value)
 
+    def run_chunks_async(self, r2_threshold, chunk_begin=0, chunk_end=0, d_count_ptr=None):
+        """wld_run_chunks_async: enqueue the run on the context's stream; the row
+        total lands in the device uint64 at d_count_ptr (if given).  Complete
+        it with run_wait() before any other call on this context."""
+        check(lib().wld_run_chunks_async(self._h, r2_threshold, chunk_begin, chunk_end,
+                                         ctypes.c_void_p(d_count_ptr) if d_count_ptr else None),
+              "wld_run_chunks_async")
+
+    def run_wait(self):
+        """wld_run_wait: completes the run started by run_chunks_async; returns its row count."""
+        n = ctypes.c_uint64()
+        check(lib().wld_run_wait(self._h, ctypes.byref(n)), "wld_run_wait")
+        return int(n.value)
+
+    def stream_ptr(self):
+        """The context's hipStream_t as an int (torch.cuda.ExternalStream)."""
+        return int(lib().wld_stream(self._h) or 0)
+
     def rows(self):
         v = Pairs()
         check(lib().wld_rows_device(self._h, ctypes.byref(v)), "wld_rows_device")

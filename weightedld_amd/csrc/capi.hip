@@ -75,10 +75,21 @@ size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 
 }  // namespace
 
+// A run between wld_run_chunks_async (or run_chunks' first phase) and its
+// completion: what run_complete needs to check, re-run and assemble it.
+struct RunPending {
+    bool active = false;
+    float thr = 0.f;
+    uint32_t lin_begin = 0, lin_end = 0;
+    uint64_t pairs = 0;
+    unsigned long long *count_out = nullptr;
+};
+
 struct wld_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
+    RunPending pend;                      // the run between run_enqueue and run_complete
     unsigned long long *h_cnt = nullptr;  // mapped pinned {cursor, rows} written by chunk_scan_kernel
     unsigned long long *d_hcnt = nullptr;
     int kernel_pref = WLD_KERNEL_AUTO;
@@ -572,67 +583,91 @@ int wld_shard_chunks(size_t n_sites, int n_shards, int shard, uint32_t *begin, u
 }
 
 namespace {
-int run_chunks(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uint64_t *n_rows) {
+int grow_staging(wld_ctx *c, uint64_t cap) {
+    cap = std::max<uint64_t>(cap, 1);
+    if (c->st_capacity >= cap) return WLD_OK;
+    WLD_TRY(ensure(c->st_a, cap * 4));
+    WLD_TRY(ensure(c->st_b, cap * 4));
+    WLD_TRY(ensure(c->st_d, cap * 4));
+    WLD_TRY(ensure(c->st_dp, cap * 4));
+    WLD_TRY(ensure(c->st_r2, cap * 4));
+    c->st_capacity = cap;
+    return WLD_OK;
+}
+
+// One pass of a run, enqueued on the context's stream with no host wait:
+// run-state init, the pair kernel, then the chunk scan, which leaves
+// {staging cursor, row total} in the mapped host counters (and the total in
+// the caller's device word, if given).
+int enqueue_pass(wld_ctx *c) {
+    const RunPending &r = c->pend;
+    const uint32_t T = (uint32_t)(c->LP / kTile);
+    const uint32_t lin_count = r.lin_end - r.lin_begin;
+    launch_run_init(ptr<unsigned long long>(c->counters), ptr<uint32_t>(c->chunk_total), r.lin_begin, lin_count,
+                    ptr<uint32_t>(c->seg_cnt), c->LP * T / 4, c->stream);
+    HIP_TRY(hipGetLastError());
+    const OrderArgs o = order_args(c);
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    if (c->n_tiles) WLD_TRY(launch_pairs(c, r.thr, o, nullptr));
+    HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+    c->h_cnt[0] = c->h_cnt[1] = lin_count ? ~0ull : 0ull;
+    if (lin_count) {
+        launch_chunk_scan(ptr<uint32_t>(c->chunk_total), r.lin_begin, lin_count, ptr<uint32_t>(c->chunk_base),
+                          ptr<unsigned long long>(c->counters) + 1, ptr<unsigned long long>(c->counters), c->d_hcnt,
+                          r.count_out, c->stream);
+        HIP_TRY(hipGetLastError());
+    } else if (r.count_out) {
+        HIP_TRY(hipMemsetAsync(r.count_out, 0, sizeof(unsigned long long), c->stream));
+    }
+    HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+    return WLD_OK;
+}
+
+// Phase 1 of a run over linear chunks [lin_begin, lin_end): sizing, then the
+// first pass, enqueued.  Staging starts at min(pairs, 32M rows); the pair
+// kernels count every passing row but store only below capacity, so an
+// overflow is detected from the cursor in run_complete and the pass re-run
+// once with staging of the exact size.
+int run_enqueue(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, unsigned long long *count_out) {
     const uint32_t n = chunk_rows_of(c->L);
     c->have_rows = false;
+    c->pend.active = false;
     WLD_TRY(build_tiles(c, lin_begin, lin_end));
     const uint64_t pairs = pairs_in_chunks(c->L, lin_begin, lin_end);
     const uint32_t T = (uint32_t)(c->LP / kTile);
     const uint32_t n_chunks = n * (n + 1) / 2;
-    const uint32_t lin_count = lin_end - lin_begin;
-
-    // Staging starts at min(pairs, 32M rows) and grows to the exact need: the
-    // pair kernels count every passing row but store only below capacity, so
-    // an overflow is detected from the cursor and the pass is re-run once.
     if (pairs > 0xFFFFFFFFull)
         return fail(WLD_E_ARG, "shard has %llu pairs; > 2^32 per device not supported (shard over more devices)",
                     (unsigned long long)pairs);
-    auto grow_staging = [&](uint64_t cap) -> int {
-        cap = std::max<uint64_t>(cap, 1);
-        if (c->st_capacity >= cap) return WLD_OK;
-        WLD_TRY(ensure(c->st_a, cap * 4));
-        WLD_TRY(ensure(c->st_b, cap * 4));
-        WLD_TRY(ensure(c->st_d, cap * 4));
-        WLD_TRY(ensure(c->st_dp, cap * 4));
-        WLD_TRY(ensure(c->st_r2, cap * 4));
-        c->st_capacity = cap;
-        return WLD_OK;
-    };
     uint64_t init_rows = 1ull << 25;
     if (const char *e = getenv("WLD_INITIAL_STAGING_ROWS")) init_rows = strtoull(e, nullptr, 10);  // tests
-    WLD_TRY(grow_staging(std::min<uint64_t>(pairs, init_rows)));
+    WLD_TRY(grow_staging(c, std::min<uint64_t>(pairs, init_rows)));
     WLD_TRY(ensure(c->seg_cnt, c->LP * T));
     WLD_TRY(ensure(c->seg_off, c->LP * T * sizeof(uint32_t)));
     WLD_TRY(ensure(c->chunk_total, std::max<size_t>(n_chunks, 1) * sizeof(uint32_t)));
     WLD_TRY(ensure(c->chunk_base, std::max<size_t>(n_chunks, 1) * sizeof(uint32_t)));
     WLD_TRY(ensure(c->counters, 4 * sizeof(unsigned long long)));
+    c->pend = RunPending{true, thr, lin_begin, lin_end, pairs, count_out};
+    return enqueue_pass(c);
+}
 
+// Phase 2: one host wait, the overflow re-run if needed, then (only when rows
+// passed) the reference-order gather.
+int run_complete(wld_ctx *c, uint64_t *n_rows) {
+    if (!c->pend.active) return fail(WLD_E_STATE, "no run in flight");
+    c->pend.active = false;
+    const RunPending r = c->pend;
+    const uint32_t n = chunk_rows_of(c->L);
+    const uint32_t lin_count = r.lin_end - r.lin_begin;
     unsigned long long h[2] = {0, 0};
-    OrderArgs o;
     for (int attempt = 0; attempt < 2; ++attempt) {
-        launch_run_init(ptr<unsigned long long>(c->counters), ptr<uint32_t>(c->chunk_total), lin_begin, lin_count,
-                        ptr<uint32_t>(c->seg_cnt), c->LP * T / 4, c->stream);
-        HIP_TRY(hipGetLastError());
-        o = order_args(c);
-        HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-        if (c->n_tiles) WLD_TRY(launch_pairs(c, thr, o, nullptr));
-        HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-        unsigned long long *d_total = ptr<unsigned long long>(c->counters) + 1;
-        if (lin_count) {
-            c->h_cnt[0] = c->h_cnt[1] = ~0ull;
-            launch_chunk_scan(ptr<uint32_t>(c->chunk_total), lin_begin, lin_count, ptr<uint32_t>(c->chunk_base),
-                              d_total, ptr<unsigned long long>(c->counters), c->d_hcnt, c->stream);
-            HIP_TRY(hipGetLastError());
-        }
-        HIP_TRY(hipEventRecord(c->ev[4], c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
-        if (lin_count) {
-            h[0] = __atomic_load_n(&c->h_cnt[0], __ATOMIC_ACQUIRE);
-            h[1] = __atomic_load_n(&c->h_cnt[1], __ATOMIC_ACQUIRE);
-        }
+        h[0] = __atomic_load_n(&c->h_cnt[0], __ATOMIC_ACQUIRE);
+        h[1] = __atomic_load_n(&c->h_cnt[1], __ATOMIC_ACQUIRE);
         if (h[0] <= c->st_capacity) break;
         if (attempt == 1) return fail(WLD_E_HIP, "internal: staging overflow after resize");
-        WLD_TRY(grow_staging(h[0]));
+        WLD_TRY(grow_staging(c, h[0]));
+        WLD_TRY(enqueue_pass(c));
     }
     const uint64_t rows = h[1];
     if (h[0] != h[1]) return fail(WLD_E_HIP, "internal: staging cursor %llu != chunk total %llu", h[0], h[1]);
@@ -643,7 +678,7 @@ int run_chunks(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uint
     WLD_TRY(ensure(c->out_r2, std::max<uint64_t>(rows, 1) * 4));
     int order_end = 4;  // with no rows the order phase ends at the scan
     if (rows && lin_count) {
-        launch_gather(o, ptr<uint32_t>(c->chunk_base), lin_begin, lin_count, n, (uint32_t)c->L,
+        launch_gather(order_args(c), ptr<uint32_t>(c->chunk_base), r.lin_begin, lin_count, n, (uint32_t)c->L,
                       c->has_map ? ptr<uint32_t>(c->site_map) : nullptr, ptr<uint32_t>(c->out_a),
                       ptr<uint32_t>(c->out_b), ptr<float>(c->out_d), ptr<float>(c->out_dp), ptr<float>(c->out_r2),
                       c->stream);
@@ -655,13 +690,18 @@ int run_chunks(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uint
     c->rows = rows;
     c->have_rows = true;
     c->stats.kernel = c->kernel;
-    c->stats.pairs = pairs;
+    c->stats.pairs = r.pairs;
     c->stats.rows = rows;
     c->stats.pair_kernel_ms = event_ms(c->ev[2], c->ev[3]);
     c->stats.order_ms = event_ms(c->ev[3], c->ev[order_end]);
     c->stats.pair_kernel_launches = c->n_tiles ? 1 : 0;
     if (n_rows) *n_rows = rows;
     return WLD_OK;
+}
+
+int run_chunks(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uint64_t *n_rows) {
+    WLD_TRY(run_enqueue(c, thr, lin_begin, lin_end, nullptr));
+    return run_complete(c, n_rows);
 }
 }  // namespace
 
@@ -684,6 +724,22 @@ int wld_run_chunks(wld_ctx *c, float thr, uint32_t chunk_begin, uint32_t chunk_e
     if (chunk_begin > chunk_end) return fail(WLD_E_ARG, "chunk range [%u,%u) invalid", chunk_begin, chunk_end);
     return run_chunks(c, thr, chunk_begin, chunk_end, n_rows);
 }
+
+int wld_run_chunks_async(wld_ctx *c, float thr, uint32_t chunk_begin, uint32_t chunk_end, void *d_count_out) {
+    WLD_TRY(set_dev(c));
+    if (!c->loaded) return fail(WLD_E_STATE, "wld_run_chunks_async before wld_load");
+    const uint32_t m = chunks_of(c->L);
+    if (chunk_end == 0 || chunk_end > m) chunk_end = m;
+    if (chunk_begin > chunk_end) return fail(WLD_E_ARG, "chunk range [%u,%u) invalid", chunk_begin, chunk_end);
+    return run_enqueue(c, thr, chunk_begin, chunk_end, static_cast<unsigned long long *>(d_count_out));
+}
+
+int wld_run_wait(wld_ctx *c, uint64_t *n_rows) {
+    WLD_TRY(set_dev(c));
+    return run_complete(c, n_rows);
+}
+
+void *wld_stream(wld_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
 int wld_rows_device(wld_ctx *c, wld_pairs *v) {
     if (!c || !v) return fail(WLD_E_ARG, "null argument");

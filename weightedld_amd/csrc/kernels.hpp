@@ -76,9 +76,10 @@ unsigned mfma_plane_mask(const int8_t *wplanes, size_t LP, size_t NP, hipStream_
 // order.hip
 void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t lin_begin, uint32_t lin_count,
                      uint32_t *seg_cnt_words, size_t n_words, hipStream_t s);
+// count_out (device, may be null): also receives the run's row total
 void launch_chunk_scan(const uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
                        unsigned long long *total, const unsigned long long *cursor, unsigned long long *host_out,
-                       hipStream_t s);
+                       unsigned long long *count_out, hipStream_t s);
 void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,
                    uint32_t n_chunk_rows, uint32_t L, const uint32_t *site_map, uint32_t *out_a, uint32_t *out_b,
                    float *out_d, float *out_dp, float *out_r2, hipStream_t s);

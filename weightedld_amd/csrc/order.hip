@@ -34,7 +34,8 @@ __global__ __launch_bounds__(1024) void chunk_scan_kernel(const uint32_t *__rest
                                                            uint32_t count, uint32_t *__restrict__ chunk_base,
                                                            unsigned long long *__restrict__ total,
                                                            const unsigned long long *__restrict__ cursor,
-                                                           unsigned long long *host_out) {
+                                                           unsigned long long *host_out,
+                                                           unsigned long long *__restrict__ count_out) {
     __shared__ unsigned long long sw[16];
     const uint32_t tid = threadIdx.x;
     const uint32_t per = (count + 1023) / 1024;
@@ -59,6 +60,7 @@ __global__ __launch_bounds__(1024) void chunk_scan_kernel(const uint32_t *__rest
             run += t;
         }
         *total = run;
+        if (count_out) *count_out = run;  // e.g. the caller's tensor for the RCCL count exchange
         if (host_out) {
             host_out[0] = *cursor;
             host_out[1] = run;
@@ -146,9 +148,9 @@ void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32
 
 void launch_chunk_scan(const uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
                        unsigned long long *total, const unsigned long long *cursor, unsigned long long *host_out,
-                       hipStream_t s) {
+                       unsigned long long *count_out, hipStream_t s) {
     hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(1024), 0, s, chunk_total, lin_begin, count, chunk_base, total,
-                       cursor, host_out);
+                       cursor, host_out, count_out);
 }
 
 void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,

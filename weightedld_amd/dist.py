@@ -72,15 +72,17 @@ class RowGather:
         self.cnt = torch.zeros(1, dtype=torch.int64, device=device)
         self.cnts = torch.zeros(world, dtype=torch.int64, device=device)
 
-    def __call__(self, packed):
+    def __call__(self, packed, counts=None):
+        """counts: the ranks' row counts when already exchanged (ShardStep)."""
         import torch
         import torch.distributed as dist
 
         if self.world == 1:
             return packed
-        self.cnt.fill_(packed.shape[1])
-        dist.all_gather_into_tensor(self.cnts, self.cnt, group=self.group)
-        counts = self.cnts.tolist()  # the one host sync of a step without rows
+        if counts is None:
+            self.cnt.fill_(packed.shape[1])
+            dist.all_gather_into_tensor(self.cnts, self.cnt, group=self.group)
+            counts = self.cnts.tolist()  # the one host sync of a step without rows
         m = max(counts)
         if m == 0:
             return packed[:, :0] if self.rank == 0 else None
@@ -92,6 +94,37 @@ class RowGather:
         if self.rank != 0:
             return None
         return torch.cat([gl[g][:, :counts[g]] for g in reversed(range(self.world))], dim=1)
+
+
+class ShardStep:
+    """One all_weighted_ld_pairs pass over this rank's chunk range with the
+    row gather to rank 0, in one host wait when no rank has rows: the pair
+    kernel and the row count are enqueued on the context's stream
+    (wld_run_chunks_async), the count all_gather is ordered after them on that
+    same stream, and one device-to-host read of the gathered counts completes
+    both.  Returns (rows on this rank, gathered [5, n] rows on rank 0 / None)."""
+
+    def __init__(self, ctx, rank, world, device, group=None):
+        import torch
+
+        self.ctx = ctx
+        self.gather = RowGather(rank, world, device, group)
+        self.stream = torch.cuda.ExternalStream(ctx.stream_ptr(), device=device)
+
+    def __call__(self, thr, chunk_begin, chunk_end):
+        import torch
+        import torch.distributed as dist
+
+        g = self.gather
+        with torch.cuda.stream(self.stream):
+            self.ctx.run_chunks_async(thr, chunk_begin, chunk_end, g.cnt.data_ptr())
+            dist.all_gather_into_tensor(g.cnts, g.cnt, group=g.group)
+            counts = g.cnts.tolist()  # the step's one host wait when no rank has rows
+        n = self.ctx.run_wait()  # returns at once: the stream is idle
+        if max(counts) == 0:
+            return n, (g.cnt.new_zeros((5, 0), dtype=torch.int32) if g.rank == 0 else None)
+        packed = pack_rows_device(self.ctx, n, g.device)
+        return n, (packed if g.world == 1 else g(packed, counts))
 
 
 def gather_rows(packed, rank, world, group=None):
