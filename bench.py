@@ -127,6 +127,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--unweighted", action="store_true", help="unit weights (main.rs:150-153 --unweighted)")
+    ap.add_argument("--thr", type=float, help="override the config's r2 threshold (non-headline lines)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -147,6 +148,9 @@ def main():
     import weightedld_amd as W
 
     N, L, thr, desc = CONFIGS[args.config]
+    if args.thr is not None and args.thr != thr:
+        thr = args.thr
+        desc += " (r2_threshold overridden to %g)" % thr
     buf = synth(L, N)
     t0 = time.perf_counter()
     ss = W.SiteSet.from_buffer(buf)

@@ -84,47 +84,55 @@ __device__ inline void chunk_of_linear(uint32_t n, uint32_t i, uint32_t &row, ui
     col = row + i - rf * (rf + 1) / 2;
 }
 
+// One workgroup per (chunk, 16-row slice): every slice re-derives the chunk's
+// row prefix from the segment counts (256 rows x 4 bytes), then copies only
+// its 16 rows, so a chunk full of rows spreads over 16 workgroups.
+constexpr uint32_t kGatherRows = 16;
+
 __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t *__restrict__ chunk_base,
                                                       uint32_t lin_begin, uint32_t n_chunk_rows, uint32_t L,
                                                       const uint32_t *__restrict__ site_map,
                                                       uint32_t *__restrict__ out_a, uint32_t *__restrict__ out_b,
                                                       float *__restrict__ out_d, float *__restrict__ out_dp,
                                                       float *__restrict__ out_r2) {
-    __shared__ uint8_t sCnt[kChunk][kTilesPerChunk];
-    __shared__ uint32_t sOff[kChunk][kTilesPerChunk];
-    __shared__ uint32_t sPre[kChunk][kTilesPerChunk];
+    __shared__ uint8_t sCnt[kGatherRows][kTilesPerChunk];
+    __shared__ uint32_t sOff[kGatherRows][kTilesPerChunk];
+    __shared__ uint32_t sPre[kGatherRows][kTilesPerChunk];
     __shared__ uint32_t sWave[4];
     const uint32_t lin = lin_begin + blockIdx.x;
     uint32_t row, col;
     chunk_of_linear(n_chunk_rows, lin, row, col);
     const uint32_t base = chunk_base[blockIdx.x];
     const uint32_t tid = threadIdx.x;
+    const uint32_t r0 = blockIdx.y * kGatherRows;
     const uint32_t a = row * kChunk + tid;
-    uint32_t rowtot = 0;
+    uint32_t cnt[kTilesPerChunk], rowtot = 0;
 #pragma unroll
     for (int s = 0; s < kTilesPerChunk; ++s) {
         const uint32_t tb = col * kTilesPerChunk + s;
-        uint32_t c = 0, off = 0;
-        if (a < L && tb < o.T) {
-            c = o.seg_cnt[(size_t)a * o.T + tb];
-            off = o.seg_off[(size_t)a * o.T + tb];
-        }
-        sCnt[tid][s] = (uint8_t)c;
-        sOff[tid][s] = off;
-        sPre[tid][s] = rowtot;
-        rowtot += c;
+        cnt[s] = (a < L && tb < o.T) ? o.seg_cnt[(size_t)a * o.T + tb] : 0u;
+        rowtot += cnt[s];
     }
     const uint32_t incl = wave_inclusive_scan(rowtot);
     if ((tid & 63) == 63) sWave[tid >> 6] = incl;
     __syncthreads();
-    uint32_t wbase = 0;
-    for (uint32_t k = 0; k < (tid >> 6); ++k) wbase += sWave[k];
-    const uint32_t rowbase = base + wbase + incl - rowtot;
+    const uint32_t slice_end = r0 + kGatherRows;
+    if (tid >= r0 && tid < slice_end) {  // this slice's rows
+        uint32_t wbase = 0;
+        for (uint32_t k = 0; k < (tid >> 6); ++k) wbase += sWave[k];
+        uint32_t pre = base + wbase + incl - rowtot;
 #pragma unroll
-    for (int s = 0; s < kTilesPerChunk; ++s) sPre[tid][s] += rowbase;
+        for (int s = 0; s < kTilesPerChunk; ++s) {
+            const uint32_t tb = col * kTilesPerChunk + s;
+            sCnt[tid - r0][s] = (uint8_t)cnt[s];
+            sOff[tid - r0][s] = cnt[s] ? o.seg_off[(size_t)a * o.T + tb] : 0u;
+            sPre[tid - r0][s] = pre;
+            pre += cnt[s];
+        }
+    }
     __syncthreads();
     const uint32_t s = tid >> 6, e = tid & 63;
-    for (uint32_t r = 0; r < kChunk; ++r) {
+    for (uint32_t r = 0; r < kGatherRows; ++r) {
         if (e < sCnt[r][s]) {
             const uint64_t src = (uint64_t)sOff[r][s] + e;
             const uint64_t dst = (uint64_t)sPre[r][s] + e;
@@ -157,7 +165,8 @@ void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_
                    uint32_t n_chunk_rows, uint32_t L, const uint32_t *site_map, uint32_t *out_a, uint32_t *out_b,
                    float *out_d, float *out_dp, float *out_r2, hipStream_t s) {
     if (!count) return;
-    hipLaunchKernelGGL(gather_kernel, dim3(count), dim3(256), 0, s, o, chunk_base, lin_begin, n_chunk_rows, L,
+    hipLaunchKernelGGL(gather_kernel, dim3(count, kChunk / kGatherRows), dim3(256), 0, s, o, chunk_base, lin_begin,
+                       n_chunk_rows, L,
                        site_map, out_a, out_b, out_d, out_dp, out_r2);
 }
 
