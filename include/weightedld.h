@@ -235,6 +235,12 @@ int wld_run_chunks_async(wld_ctx *ctx, float r2_threshold, uint32_t chunk_begin,
 int wld_run_wait(wld_ctx *ctx, uint64_t *n_rows);
 /* The context's HIP stream (hipStream_t), for ordering caller work after a run. */
 void *wld_stream(wld_ctx *ctx);
+/* All pairs of the loaded set, any size, rows to host: runs the reference's
+ * chunk sequence in batches of at most 2^31 pairs (one wld_run_chunks each),
+ * appending each batch's rows to library-allocated host arrays in reference
+ * order (release with wld_pairs_free); progress (may be NULL) gets the running
+ * pair count after each batch, on the calling thread. */
+int wld_run_host(wld_ctx *ctx, float r2_threshold, wld_progress_fn progress, void *user, wld_pairs *out);
 /* Device pointers of the last run's rows (valid until the next run/load or
  * destroy; do not free). */
 int wld_rows_device(wld_ctx *ctx, wld_pairs *view);

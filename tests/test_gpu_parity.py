@@ -607,3 +607,26 @@ def test_shard_step_world1_rccl(W, ctxs):
                 assert np.abs(got["r2"].astype(np.float64) - ref["r2"]).max(initial=0.0) < 1e-5
     finally:
         dist.destroy_process_group()
+
+
+def test_run_host_batches_concatenate(W, ctxs, monkeypatch):
+    # wld_run_host / wld_all_weighted_ld_pairs split the chunk sequence into
+    # batches (<= 2^31 pairs; forced small here) and append their rows: the
+    # result equals one run, in reference order, with per-batch progress.
+    ctx = _ctx(ctxs, "mfma")
+    L, N = 1100, 200
+    buf = synth(L, N, 90)
+    w = np.random.default_rng(6).random(N).astype(np.float32) + 0.1
+    ref = O.all_pairs(buf, w, 0.01)
+    ctx.load(buf, w)
+    whole = ctx.run_host(0.01)
+    monkeypatch.setenv("WLD_HOST_BATCH_PAIRS", "70000")  # about one chunk per batch
+    seen = []
+    got = ctx.run_host(0.01, seen.append)
+    assert len(seen) > 5 and seen == sorted(seen) and seen[-1] == L * (L - 1) // 2
+    for f in ("site_a", "site_b", "d", "d_prime", "r2"):
+        assert np.array_equal(getattr(got, f).view(np.uint32), getattr(whole, f).view(np.uint32)), f
+    compare_rows(got, ref, 0.01, buf=buf, w=w)
+    store = W.all_weighted_ld_pairs(W.SiteSet.from_buffer(buf), w, 0.01)
+    assert np.array_equal(store.site_a, got.site_a) and np.array_equal(store.r2.view(np.uint32),
+                                                                       got.r2.view(np.uint32))

@@ -295,6 +295,14 @@ class Context:
         check(lib().wld_run_wait(self._h, ctypes.byref(n)), "wld_run_wait")
         return int(n.value)
 
+    def run_host(self, r2_threshold, progress_report=None):
+        """wld_run_host: every pair of the loaded set, in batches of <= 2^31
+        pairs, rows to host in reference order (a PairStore)."""
+        cb = PROGRESS_FN(lambda n, _u: progress_report(int(n))) if progress_report else PROGRESS_FN()
+        out = Pairs()
+        check(lib().wld_run_host(self._h, r2_threshold, cb, None, ctypes.byref(out)), "wld_run_host")
+        return _take_pairs(out)
+
     def stream_ptr(self):
         """The context's hipStream_t as an int (torch.cuda.ExternalStream)."""
         return int(lib().wld_stream(self._h) or 0)
@@ -406,6 +414,11 @@ def all_weighted_ld_pairs(site_set, weights, r2_threshold, progress_report=None,
     check(lib().wld_all_weighted_ld_pairs(ctx._h, _p(buf, ctypes.c_uint8), buf.shape[0], buf.shape[1],
                                           None if sm is None else _p(sm, ctypes.c_uint64), _p(w, ctypes.c_float),
                                           r2_threshold, cb, None, ctypes.byref(out)), "all_weighted_ld_pairs")
+    return _take_pairs(out)
+
+
+def _take_pairs(out):
+    """Library-allocated host wld_pairs -> PairStore (copies, then frees)."""
     n = int(out.n)
 
     def grab(p, dt):

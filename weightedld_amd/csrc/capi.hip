@@ -830,6 +830,63 @@ void wld_pairs_free(wld_pairs *p) {
     memset(p, 0, sizeof(*p));
 }
 
+int wld_run_host(wld_ctx *c, float r2_threshold, wld_progress_fn progress, void *user, wld_pairs *out) {
+    if (!out) return fail(WLD_E_ARG, "null out");
+    memset(out, 0, sizeof(*out));
+    WLD_TRY(set_dev(c));
+    if (!c->loaded) return fail(WLD_E_STATE, "wld_run_host before wld_load");
+    // Batches of whole chunks, contiguous in the reference order, of at most
+    // 2^31 pairs each (a run's staging positions are 32-bit); their rows
+    // concatenate in order.  progress gets the running pair count per batch.
+    uint64_t limit = 1ull << 31;
+    if (const char *e = getenv("WLD_HOST_BATCH_PAIRS")) limit = std::max<uint64_t>(1, strtoull(e, nullptr, 10));  // tests
+    const uint32_t m = chunks_of(c->L);
+    uint64_t cap = 0, done = 0, pairs_done = 0;
+    auto grow = [&](uint64_t need) -> int {
+        if (need <= cap) return WLD_OK;
+        uint64_t k = std::max<uint64_t>(need, cap + cap / 2);
+        void *p[5] = {realloc(out->site_a, k * 4), nullptr, nullptr, nullptr, nullptr};
+        if (p[0]) out->site_a = (uint32_t *)p[0];
+        if (p[0] && (p[1] = realloc(out->site_b, k * 4))) out->site_b = (uint32_t *)p[1];
+        if (p[1] && (p[2] = realloc(out->d, k * 4))) out->d = (float *)p[2];
+        if (p[2] && (p[3] = realloc(out->d_prime, k * 4))) out->d_prime = (float *)p[3];
+        if (p[3] && (p[4] = realloc(out->r2, k * 4))) out->r2 = (float *)p[4];
+        if (!p[4]) return fail(WLD_E_OOM, "host allocation of %llu rows failed", (unsigned long long)k);
+        cap = k;
+        return WLD_OK;
+    };
+    int st = grow(1);
+    for (uint32_t b = 0; st == WLD_OK && b < m;) {
+        uint32_t e = b;
+        uint64_t pairs = 0;
+        while (e < m) {
+            const uint64_t p1 = pairs_in_chunks(c->L, e, e + 1);
+            if (e > b && pairs + p1 > limit) break;
+            pairs += p1;
+            ++e;
+        }
+        uint64_t rows = 0;
+        if ((st = run_chunks(c, r2_threshold, b, e, &rows)) != WLD_OK) break;
+        if ((st = grow(done + rows)) != WLD_OK) break;
+        if (rows &&
+            (st = wld_rows_copy(c, out->site_a + done, out->site_b + done, out->d + done, out->d_prime + done,
+                                out->r2 + done)) != WLD_OK)
+            break;
+        done += rows;
+        pairs_done += pairs;
+        if (progress) progress(pairs_done, user);
+        b = e;
+    }
+    if (st != WLD_OK) {
+        wld_pairs_free(out);
+        return st;
+    }
+    out->n = done;
+    c->stats.pairs = pairs_done;
+    c->stats.rows = done;
+    return WLD_OK;
+}
+
 int wld_all_weighted_ld_pairs(wld_ctx *c, const uint8_t *sites, size_t n_sites, size_t n_seqs,
                               const uint64_t *site_map, const float *weights, float r2_threshold,
                               wld_progress_fn progress, void *user, wld_pairs *out) {
@@ -837,26 +894,7 @@ int wld_all_weighted_ld_pairs(wld_ctx *c, const uint8_t *sites, size_t n_sites, 
     memset(out, 0, sizeof(*out));
     if (progress) progress(0, user);  // lib.rs:584
     WLD_TRY(wld_load(c, sites, n_sites, n_seqs, site_map, weights));
-    uint64_t rows = 0;
-    WLD_TRY(wld_run(c, r2_threshold, 0, 0, &rows));
-    const size_t k = std::max<uint64_t>(rows, 1);
-    out->site_a = (uint32_t *)malloc(k * 4);
-    out->site_b = (uint32_t *)malloc(k * 4);
-    out->d = (float *)malloc(k * 4);
-    out->d_prime = (float *)malloc(k * 4);
-    out->r2 = (float *)malloc(k * 4);
-    if (!out->site_a || !out->site_b || !out->d || !out->d_prime || !out->r2) {
-        wld_pairs_free(out);
-        return fail(WLD_E_OOM, "host allocation of %llu rows failed", (unsigned long long)rows);
-    }
-    int st = wld_rows_copy(c, out->site_a, out->site_b, out->d, out->d_prime, out->r2);
-    if (st != WLD_OK) {
-        wld_pairs_free(out);
-        return st;
-    }
-    out->n = rows;
-    if (progress) progress(c->stats.pairs, user);
-    return WLD_OK;
+    return wld_run_host(c, r2_threshold, progress, user, out);
 }
 
 int wld_single_weighted_ld_pair(wld_ctx *c, const uint8_t *a, const uint8_t *b, const float *weights, size_t n_seqs,

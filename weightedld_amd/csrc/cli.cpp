@@ -383,19 +383,9 @@ int run_gpu_prepass(const Opt &opt, wld_siteset *siteset, wld_ctx *ctx) {
     INFO("Beginning pairwise weighted LD computation");
     sw = clk::now();
     const uint64_t total_pairs = ((uint64_t)L - 1) * ((uint64_t)L - 2) / 2;  // main.rs:168 (sic, wraps)
-    uint64_t n = 0;
-    if ((st = wld_run(ctx, opt.r2_threshold, 0, 0, &n)) != WLD_OK) die(st, "all_weighted_ld_pairs");
-    wld_pairs pairs;
-    pairs.n = n;
-    const size_t m = std::max<uint64_t>(n, 1);
-    pairs.site_a = (uint32_t *)malloc(m * 4);
-    pairs.site_b = (uint32_t *)malloc(m * 4);
-    pairs.d = (float *)malloc(m * 4);
-    pairs.d_prime = (float *)malloc(m * 4);
-    pairs.r2 = (float *)malloc(m * 4);
-    if (!pairs.site_a || !pairs.site_b || !pairs.d || !pairs.d_prime || !pairs.r2) die(WLD_E_OOM, "rows");
-    if (n && (st = wld_rows_copy(ctx, pairs.site_a, pairs.site_b, pairs.d, pairs.d_prime, pairs.r2)) != WLD_OK)
-        die(st, "rows_copy");
+    wld_pairs pairs;  // any L: batches of <= 2^31 pairs, rows appended in reference order
+    if ((st = wld_run_host(ctx, opt.r2_threshold, nullptr, nullptr, &pairs)) != WLD_OK)
+        die(st, "all_weighted_ld_pairs");
     return finish(opt, ctx, pairs, clk::now() - sw, total_pairs);
 }
 
