@@ -195,13 +195,8 @@ __device__ __forceinline__ void mfma_block_sel16(v4i (&acc)[4][2][NPL][2], v4i c
     for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-#ifdef WLD_EXP_NOBPERM  // diagnostic: B operands taken as loaded (wrong sums, same MFMAs)
-            b_in[n][e] = cb[n][e];
-            b_maj[n][e] = cb[n][e] ^ (int)kOnes;
-#else
             b_in[n][e] = (int)__builtin_amdgcn_perm(kOnes, kOnes, (unsigned)cb[n][e]);
             b_maj[n][e] = (int)__builtin_amdgcn_perm(kOnes, 0u, (unsigned)cb[n][e]);
-#endif
         }
 #pragma unroll
     for (int p = 0; p < NPL; ++p) {
