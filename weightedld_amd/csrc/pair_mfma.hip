@@ -526,9 +526,11 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
     const uint32_t offA = lrow + (wave >> 1) * 1024 + (wave & 1) * 256;
     const uint32_t offB = lrow + 2048;  // + (n >> 1) * 1024 + (n & 1) * 256
     const uint32_t offD = kGroup * kStageCodes + so * kDigStage + hh * 16;
-    uint32_t offP[NPL];  // the active planes' 32-byte rows of a stage's digit record
+    // the active planes' 32-byte rows of a stage's digit record (all three:
+    // compile-time offsets, so the reads keep immediate offsets)
+    uint32_t offP[NPL];
 #pragma unroll
-    for (int j = 0; j < NPL; ++j) offP[j] = offD + 32 * ((plane_idx >> (2 * j)) & 3);
+    for (int j = 0; j < NPL; ++j) offP[j] = NPL == 3 ? offD + 32 * j : offD + 32 * ((plane_idx >> (2 * j)) & 3);
     zero_acc(acc);
     uint32_t buf = 0;
 #ifdef WLD_EXP_PRIO
@@ -556,7 +558,8 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
                                *reinterpret_cast<const v4i *>(sc + offB + 1280)};
             v4i dp[NPL];
 #pragma unroll
-            for (int j = 0; j < NPL; ++j) dp[j] = *reinterpret_cast<const v4i *>(sd + offP[j]);
+            for (int j = 0; j < NPL; ++j)
+                dp[j] = *reinterpret_cast<const v4i *>(NPL == 3 ? sd + offD + 32 * j : sd + offP[j]);
             mfma_block_sel16<NPL>(acc.v, ca, cb, dp);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
