@@ -90,6 +90,7 @@ struct wld_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
     RunPending pend;                      // the run between run_enqueue and run_complete
+    bool run_dirty = true;                // run state (cursor, chunk totals) may be nonzero: re-initialise
     unsigned long long *h_cnt = nullptr;  // mapped pinned {cursor, rows} written by chunk_scan_kernel
     unsigned long long *d_hcnt = nullptr;
     int kernel_pref = WLD_KERNEL_AUTO;
@@ -601,11 +602,17 @@ int grow_staging(wld_ctx *c, uint64_t cap) {
 // the caller's device word, if given).
 int enqueue_pass(wld_ctx *c) {
     const RunPending &r = c->pend;
-    const uint32_t T = (uint32_t)(c->LP / kTile);
     const uint32_t lin_count = r.lin_end - r.lin_begin;
-    launch_run_init(ptr<unsigned long long>(c->counters), ptr<uint32_t>(c->chunk_total), r.lin_begin, lin_count,
-                    ptr<uint32_t>(c->seg_cnt), c->LP * T / 4, c->stream);
-    HIP_TRY(hipGetLastError());
+    // The chunk scan of every completed run leaves the cursor and its chunk
+    // totals at 0, and every computed tile writes all of its segment counts,
+    // so the init kernel runs only after (re)allocation or a failed run.
+    if (c->run_dirty) {
+        const uint32_t n = chunk_rows_of(c->L);
+        launch_run_init(ptr<unsigned long long>(c->counters), ptr<uint32_t>(c->chunk_total), n * (n + 1) / 2,
+                        c->stream);
+        HIP_TRY(hipGetLastError());
+    }
+    c->run_dirty = true;  // until run_complete has seen this pass's scan
     const OrderArgs o = order_args(c);
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     if (c->n_tiles) WLD_TRY(launch_pairs(c, r.thr, o, nullptr));
@@ -644,9 +651,11 @@ int run_enqueue(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uns
     WLD_TRY(grow_staging(c, std::min<uint64_t>(pairs, init_rows)));
     WLD_TRY(ensure(c->seg_cnt, c->LP * T));
     WLD_TRY(ensure(c->seg_off, c->LP * T * sizeof(uint32_t)));
+    const size_t ct_bytes = c->chunk_total.bytes, cn_bytes = c->counters.bytes;
     WLD_TRY(ensure(c->chunk_total, std::max<size_t>(n_chunks, 1) * sizeof(uint32_t)));
     WLD_TRY(ensure(c->chunk_base, std::max<size_t>(n_chunks, 1) * sizeof(uint32_t)));
     WLD_TRY(ensure(c->counters, 4 * sizeof(unsigned long long)));
+    if (c->chunk_total.bytes != ct_bytes || c->counters.bytes != cn_bytes) c->run_dirty = true;  // fresh memory
     c->pend = RunPending{true, thr, lin_begin, lin_end, pairs, count_out};
     return enqueue_pass(c);
 }
@@ -662,6 +671,7 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     unsigned long long h[2] = {0, 0};
     for (int attempt = 0; attempt < 2; ++attempt) {
         HIP_TRY(hipStreamSynchronize(c->stream));
+        c->run_dirty = false;  // the pass completed: its scan cleaned the run state
         h[0] = __atomic_load_n(&c->h_cnt[0], __ATOMIC_ACQUIRE);
         h[1] = __atomic_load_n(&c->h_cnt[1], __ATOMIC_ACQUIRE);
         if (h[0] <= c->st_capacity) break;

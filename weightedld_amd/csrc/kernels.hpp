@@ -74,11 +74,11 @@ void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const int8_t *w
 unsigned mfma_plane_mask(const int8_t *wplanes, size_t LP, size_t NP, hipStream_t s);
 
 // order.hip
-void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t lin_begin, uint32_t lin_count,
-                     uint32_t *seg_cnt_words, size_t n_words, hipStream_t s);
+// zeroes the run state (staging cursor, row total, every chunk total)
+void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t n_chunks, hipStream_t s);
 // count_out (device, may be null): also receives the run's row total
-void launch_chunk_scan(const uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
-                       unsigned long long *total, const unsigned long long *cursor, unsigned long long *host_out,
+void launch_chunk_scan(uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
+                       unsigned long long *total, unsigned long long *cursor, unsigned long long *host_out,
                        unsigned long long *count_out, hipStream_t s);
 void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,
                    uint32_t n_chunk_rows, uint32_t L, const uint32_t *site_map, uint32_t *out_a, uint32_t *out_b,

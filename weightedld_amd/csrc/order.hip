@@ -19,21 +19,20 @@ namespace wld {
 // Zeroes a run's counters, its chunk totals and the segment counts (one launch
 // instead of three memsets).
 __global__ __launch_bounds__(256) void run_init_kernel(unsigned long long *__restrict__ counters,
-                                                        uint32_t *__restrict__ chunk_total, uint32_t lin_begin,
-                                                        uint32_t lin_count, uint32_t *__restrict__ seg_cnt_words,
-                                                        uint32_t n_words) {
+                                                        uint32_t *__restrict__ chunk_total, uint32_t n_chunks) {
     const uint32_t i0 = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
     if (i0 < 4) counters[i0] = 0;
-    for (uint32_t i = i0; i < lin_count; i += stride) chunk_total[lin_begin + i] = 0;
-    for (uint32_t i = i0; i < n_words; i += stride) seg_cnt_words[i] = 0;
+    for (uint32_t i = i0; i < n_chunks; i += stride) chunk_total[i] = 0;
 }
 
 // host_out (mapped pinned host memory) receives {staging cursor, row total}:
-// the run's only device-to-host transfer, without a copy command.
-__global__ __launch_bounds__(1024) void chunk_scan_kernel(const uint32_t *__restrict__ chunk_total, uint32_t lin_begin,
+// the run's only device-to-host transfer, without a copy command.  The scan
+// also leaves the run state clean for the next run (the staging cursor and
+// the range's chunk totals back to 0), so a run needs no initialising kernel.
+__global__ __launch_bounds__(1024) void chunk_scan_kernel(uint32_t *__restrict__ chunk_total, uint32_t lin_begin,
                                                            uint32_t count, uint32_t *__restrict__ chunk_base,
                                                            unsigned long long *__restrict__ total,
-                                                           const unsigned long long *__restrict__ cursor,
+                                                           unsigned long long *__restrict__ cursor,
                                                            unsigned long long *host_out,
                                                            unsigned long long *__restrict__ count_out) {
     __shared__ unsigned long long sw[16];
@@ -61,8 +60,10 @@ __global__ __launch_bounds__(1024) void chunk_scan_kernel(const uint32_t *__rest
         }
         *total = run;
         if (count_out) *count_out = run;  // e.g. the caller's tensor for the RCCL count exchange
+        const unsigned long long cur = *cursor;
+        *cursor = 0;
         if (host_out) {
-            host_out[0] = *cursor;
+            host_out[0] = cur;
             host_out[1] = run;
             __threadfence_system();
         }
@@ -70,8 +71,10 @@ __global__ __launch_bounds__(1024) void chunk_scan_kernel(const uint32_t *__rest
     __syncthreads();
     unsigned long long base = sw[wv] + v - s;
     for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t t = chunk_total[lin_begin + i];
+        chunk_total[lin_begin + i] = 0;
         chunk_base[i] = (uint32_t)base;
-        base += chunk_total[lin_begin + i];
+        base += t;
     }
 }
 
@@ -110,7 +113,9 @@ __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t
 #pragma unroll
     for (int s = 0; s < kTilesPerChunk; ++s) {
         const uint32_t tb = col * kTilesPerChunk + s;
-        cnt[s] = (a < L && tb < o.T) ? o.seg_cnt[(size_t)a * o.T + tb] : 0u;
+        // the tiles the pair kernel computed (b tile >= a tile, inside L) each
+        // wrote their 64 counts; the rest of the chunk holds no rows
+        cnt[s] = (a < L && tb * kTile < L && tb >= a / kTile) ? o.seg_cnt[(size_t)a * o.T + tb] : 0u;
         rowtot += cnt[s];
     }
     const uint32_t incl = wave_inclusive_scan(rowtot);
@@ -146,16 +151,13 @@ __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t
     }
 }
 
-void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t lin_begin, uint32_t lin_count,
-                     uint32_t *seg_cnt_words, size_t n_words, hipStream_t s) {
-    const size_t n = std::max<size_t>(std::max<size_t>(n_words, lin_count), 4);
-    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 2048);
-    hipLaunchKernelGGL(run_init_kernel, dim3(blocks), dim3(256), 0, s, counters, chunk_total, lin_begin, lin_count,
-                       seg_cnt_words, (uint32_t)n_words);
+void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t n_chunks, hipStream_t s) {
+    const unsigned blocks = (unsigned)std::min<size_t>((std::max<size_t>(n_chunks, 4) + 255) / 256, 2048);
+    hipLaunchKernelGGL(run_init_kernel, dim3(blocks), dim3(256), 0, s, counters, chunk_total, n_chunks);
 }
 
-void launch_chunk_scan(const uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
-                       unsigned long long *total, const unsigned long long *cursor, unsigned long long *host_out,
+void launch_chunk_scan(uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
+                       unsigned long long *total, unsigned long long *cursor, unsigned long long *host_out,
                        unsigned long long *count_out, hipStream_t s) {
     hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(1024), 0, s, chunk_total, lin_begin, count, chunk_base, total,
                        cursor, host_out, count_out);

@@ -424,9 +424,12 @@ __device__ __forceinline__ void tile_epilogue(const Acc &acc, uint32_t ta, uint3
 
     // ---- compaction: a 64x64 pass-bit matrix in LDS, rows in b order ----------
     // A tile with no passing pair (every tile at the bench threshold on random
-    // data) leaves nothing to write: seg_cnt was zeroed before the launch and
-    // seg_off is read only where seg_cnt > 0.  One barrier decides it.
-    if (!__syncthreads_or(pass != 0)) return;
+    // data) writes only its 64 zero counts (seg_off is read only where
+    // seg_cnt > 0).  One barrier decides it.
+    if (!__syncthreads_or(pass != 0)) {
+        if (tid < kTile) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
+        return;
+    }
     if (tid < kTile) sBits[tid] = 0ull;
     __syncthreads();
     if (pass) {
