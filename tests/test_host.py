@@ -67,6 +67,26 @@ def test_read_fasta_matches_oracle(name):
         assert np.array_equal(ss.site_histogram(i).data, O.histogram(ref[i]))
 
 
+@pytest.mark.parametrize("n_seqs,n_sites", [(1, 1), (63, 65), (130, 257), (200, 1000)])
+def test_read_fasta_blocked_transpose_vs_oracle(tmp_path, n_seqs, n_sites):
+    # ragged 64x64 blocks, every byte class (upper/lower ACGT, '-', others, a
+    # header-like '>' inside no line), histograms fused into the transpose
+    rng = np.random.default_rng(n_seqs * 7 + n_sites)
+    alphabet = np.frombuffer(b"ACGTacgt-NnXx*.?", dtype=np.uint8)
+    lines = []
+    for q in range(n_seqs):
+        lines.append(b">seq%d description\n" % q)
+        lines.append(alphabet[rng.integers(0, len(alphabet), n_sites)].tobytes() + b"\n")
+    p = tmp_path / "r.fasta"
+    p.write_bytes(b"".join(lines))
+    ss = W.read_fasta(str(p))
+    ref = O.read_fasta(str(p))
+    assert (ss.n_sites(), ss.n_seqs()) == ref.shape
+    assert np.array_equal(ss.buffer, ref)
+    for i in range(0, ref.shape[0], max(1, ref.shape[0] // 50)):
+        assert np.array_equal(ss.site_histogram(i).data, O.histogram(ref[i]))
+
+
 def test_read_fasta_panic_cases(tmp_path):
     with pytest.raises(W.WldError) as e:
         W.read_fasta(os.path.join(FIXTURES, "t1_henikoff_paper.fasta"))

@@ -5,6 +5,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <memory>
 #include <vector>
 
 #include "weightedld.h"
@@ -18,11 +19,33 @@ void clear_error();
 // Returns status after recording a message.
 int fail(int status, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 
+// std::allocator that leaves trivially constructible elements uninitialised on
+// resize: buffers that are written in full right after sizing skip a serial
+// zero fill and get their first touch in the threads that write them.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U> &) noexcept {}
+    template <class U>
+    void construct(U *p) noexcept {
+        ::new ((void *)p) U;
+    }
+    template <class U, class... A>
+    void construct(U *p, A &&...a) {
+        ::new ((void *)p) U(std::forward<A>(a)...);
+    }
+};
+
 // lib.rs:158-173 — SiteSet: site-major symbols, optional site_map, histograms.
 struct SiteSet {
     size_t n_sites = 0;
     size_t n_seqs = 0;
-    std::vector<uint8_t> buffer;      // buffer[site * n_seqs + seq]
+    std::vector<uint8_t, NoInitAlloc<uint8_t>> buffer;  // buffer[site * n_seqs + seq] (resize leaves it unset)
     bool has_map = false;
     std::vector<uint64_t> site_map;   // filtered -> parent index (lib.rs:165-169)
     std::vector<uint64_t> hist;       // 6 per site (lib.rs:171-172)

@@ -17,6 +17,11 @@
 #include <cstring>
 #include <fstream>
 #include <sstream>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <array>
 #include <thread>
 
 #include "common.hpp"
@@ -46,11 +51,24 @@ int fail(int status, const char *fmt, ...) {
     return status;
 }
 
-// lib.rs:98-104
+// lib.rs:98-104 (bytes >= 6 count as Unknown, 5).  One vectorisable compare-
+// and-count pass per symbol value over blocks of 255 bytes (u8 counters).
 void histogram(const uint8_t *sym, size_t n, uint64_t out[6]) {
-    uint64_t h[6] = {0, 0, 0, 0, 0, 0};
-    for (size_t i = 0; i < n; ++i) h[sym[i] < 6 ? sym[i] : 5] += 1;
-    for (int s = 0; s < 6; ++s) out[s] = h[s];
+    uint64_t h[5] = {0, 0, 0, 0, 0};
+    for (size_t i0 = 0; i0 < n; i0 += 255) {
+        const size_t m = std::min<size_t>(255, n - i0);
+        for (int v = 0; v < 5; ++v) {
+            uint8_t c = 0;
+            for (size_t i = 0; i < m; ++i) c += sym[i0 + i] == v;
+            h[v] += c;
+        }
+    }
+    uint64_t known = 0;
+    for (int s = 0; s < 5; ++s) {
+        out[s] = h[s];
+        known += h[s];
+    }
+    out[5] = n - known;
 }
 
 // lib.rs:126-140: strict '>' keeps the earlier of A,C,G,T,- on ties.
@@ -69,10 +87,11 @@ void major_minor(const uint64_t h[6], int *maj, int *mnr) {
     *mnr = b;
 }
 
+// f(lo, hi) over [0, n) split across the host threads; serial below min_n items.
 template <class F>
-static void parallel_for(size_t n, F &&f) {
+static void parallel_for(size_t n, F &&f, size_t min_n = 4096) {
     unsigned nt = std::max(1u, std::min(std::thread::hardware_concurrency(), 64u));
-    if (n < 4096 || nt == 1) {
+    if (n < min_n || nt == 1) {
         f(size_t(0), n);
         return;
     }
@@ -93,6 +112,18 @@ void compute_histograms(SiteSet &s) {
     });
 }
 
+// lib.rs:53-64, as a table for the FASTA transpose
+static const std::array<uint8_t, 256> kSymbolOfByte = [] {
+    std::array<uint8_t, 256> t{};
+    for (int c = 0; c < 256; ++c) t[c] = WLD_SYM_UNKNOWN;
+    t['a'] = t['A'] = WLD_SYM_A;
+    t['c'] = t['C'] = WLD_SYM_C;
+    t['g'] = t['G'] = WLD_SYM_G;
+    t['t'] = t['T'] = WLD_SYM_T;
+    t['-'] = WLD_SYM_MISSING;
+    return t;
+}();
+
 // lib.rs:53-64
 static inline uint8_t symbol_from_byte(unsigned char c) {
     switch (c) {
@@ -103,6 +134,41 @@ static inline uint8_t symbol_from_byte(unsigned char c) {
     case '-': return WLD_SYM_MISSING;
     default: return WLD_SYM_UNKNOWN;
     }
+}
+
+// The whole file, memory-mapped read-only (falls back to read_file).
+struct FileView {
+    const unsigned char *p = nullptr;
+    size_t n = 0;
+    void *map = nullptr;
+    std::string copy;
+    ~FileView() {
+        if (map) munmap(map, n);
+    }
+};
+
+static bool read_file(const char *path, std::string &data);
+
+static bool view_file(const char *path, FileView &v) {
+    const int fd = open(path, O_RDONLY);
+    if (fd >= 0) {
+        struct stat st;
+        if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0) {
+            void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+            if (m != MAP_FAILED) {
+                close(fd);
+                v.map = m;
+                v.p = (const unsigned char *)m;
+                v.n = (size_t)st.st_size;
+                return true;
+            }
+        }
+        close(fd);
+    }
+    if (!read_file(path, v.copy)) return false;
+    v.p = (const unsigned char *)v.copy.data();
+    v.n = v.copy.size();
+    return true;
 }
 
 static bool read_file(const char *path, std::string &data) {
@@ -163,10 +229,10 @@ int wld_major_minor(const uint64_t hist[6], int *major, int *minor) {
 // lib.rs:277-307 then SiteSet::from_multiseq (lib.rs:176-206).
 int wld_read_fasta(const char *path, wld_siteset **out) {
     if (!path || !out) return fail(WLD_E_ARG, "wld_read_fasta: null pointer");
-    std::string data;
-    if (!read_file(path, data)) return fail(WLD_E_IO, "cannot read %s", path);
-    const unsigned char *p = (const unsigned char *)data.data();
-    const size_t n = data.size();
+    FileView view;
+    if (!view_file(path, view)) return fail(WLD_E_IO, "cannot read %s", path);
+    const unsigned char *p = view.p;
+    const size_t n = view.n;
     std::vector<size_t> start, bytes;
     bool any_high = false;
     for (size_t pos = 0; pos < n;) {
@@ -180,8 +246,16 @@ int wld_read_fasta(const char *path, wld_siteset **out) {
     }
     if (start.empty())
         return fail(WLD_E_FORMAT, "%s: no sequences (the reference indexes sequences[0] and panics)", path);
-    for (unsigned char c : data)
-        if (c >= 0x80) { any_high = true; break; }
+    {  // any byte >= 0x80 (then multi-byte UTF-8 chars count as one symbol each)
+        uint64_t acc = 0, w;
+        size_t i = 0;
+        for (; i + 8 <= n; i += 8) {
+            memcpy(&w, p + i, 8);
+            acc |= w;
+        }
+        for (; i < n; ++i) acc |= p[i];
+        any_high = (acc & 0x8080808080808080ull) != 0;
+    }
 
     auto *ss = new wld_siteset;
     SiteSet &s = ss->s;
@@ -196,20 +270,28 @@ int wld_read_fasta(const char *path, wld_siteset **out) {
                             "sequence 0 has %zu; lib.rs:180-182)", path, i, bytes[i], s.n_sites);
             }
         s.buffer.resize(s.n_sites * s.n_seqs);
-        // cache-blocked transpose into site-major order
-        const size_t B = 64;
-        parallel_for((s.n_seqs + B - 1) / B, [&](size_t lo, size_t hi) {
-            for (size_t sb = lo; sb < hi; ++sb) {
-                size_t q0 = sb * B, q1 = std::min(s.n_seqs, q0 + B);
-                for (size_t j0 = 0; j0 < s.n_sites; j0 += B) {
-                    size_t j1 = std::min(s.n_sites, j0 + B);
-                    for (size_t q = q0; q < q1; ++q) {
-                        const unsigned char *line = p + start[q];
-                        for (size_t j = j0; j < j1; ++j) s.buffer[j * s.n_seqs + q] = symbol_from_byte(line[j]);
+        s.hist.resize(s.n_sites * 6);
+        // cache-blocked transpose into site-major order, threads over 64-site
+        // blocks: each 64x64 tile is gathered from 64 lines into a local tile,
+        // then written as 64 contiguous runs of the site-major rows; the
+        // block's histograms are taken while its rows are still in cache
+        const size_t B = 64, N = s.n_seqs;
+        uint8_t *dst = s.buffer.data();
+        parallel_for((s.n_sites + B - 1) / B, [&](size_t lo, size_t hi) {
+            alignas(64) uint8_t tile[B][B];
+            for (size_t jb = lo; jb < hi; ++jb) {
+                const size_t j0 = jb * B, nj = std::min(s.n_sites, j0 + B) - j0;
+                for (size_t q0 = 0; q0 < N; q0 += B) {
+                    const size_t nq = std::min(N, q0 + B) - q0;
+                    for (size_t q = 0; q < nq; ++q) {
+                        const unsigned char *line = p + start[q0 + q] + j0;
+                        for (size_t j = 0; j < nj; ++j) tile[j][q] = kSymbolOfByte[line[j]];
                     }
+                    for (size_t j = 0; j < nj; ++j) memcpy(dst + (j0 + j) * N + q0, tile[j], nq);
                 }
+                for (size_t j = 0; j < nj; ++j) histogram(dst + (j0 + j) * N, N, &s.hist[(j0 + j) * 6]);
             }
-        });
+        }, 2);
     } else {
         // Slow path: multi-byte UTF-8 chars are one (Unknown) symbol each.
         std::vector<size_t> chars(start.size());
@@ -229,8 +311,8 @@ int wld_read_fasta(const char *path, wld_siteset **out) {
                 s.buffer[j++ * s.n_seqs + q] = symbol_from_byte(c);
             }
         }
+        compute_histograms(s);
     }
-    compute_histograms(s);
     *out = ss;
     return WLD_OK;
 }
@@ -312,11 +394,13 @@ int wld_siteset_filter_sites_of_interest(const wld_siteset *in, float min_acgt_f
     t.n_sites = t.site_map.size();
     t.buffer.resize(t.n_sites * t.n_seqs);
     t.hist.resize(t.n_sites * 6);
-    for (size_t k = 0; k < t.n_sites; ++k) {
-        size_t i = t.site_map[k];
-        memcpy(&t.buffer[k * t.n_seqs], &s.buffer[i * s.n_seqs], s.n_seqs);
-        memcpy(&t.hist[k * 6], &s.hist[i * 6], 6 * sizeof(uint64_t));
-    }
+    parallel_for(t.n_sites, [&](size_t lo, size_t hi) {
+        for (size_t k = lo; k < hi; ++k) {
+            size_t i = t.site_map[k];
+            memcpy(&t.buffer[k * t.n_seqs], &s.buffer[i * s.n_seqs], s.n_seqs);
+            memcpy(&t.hist[k * 6], &s.hist[i * 6], 6 * sizeof(uint64_t));
+        }
+    }, 256);
     *out = o;
     return WLD_OK;
 }
@@ -340,10 +424,13 @@ int wld_henikoff_weights(const wld_siteset *in, float *out) {
             float df = (float)distinct;
             float c[6];
             for (int k = 0; k <= WLD_SYM_MISSING; ++k) c[k] = 1.0f / (df * (float)h[k]);
+            // the Unknown fill is read only by sequences that are Unknown here
             float total = 0.0f;
-            const uint8_t *site = &s.buffer[i * N];
-            for (size_t q = 0; q < N; ++q)
-                if (site[q] <= WLD_SYM_MISSING) total += c[site[q]];
+            if (h[5]) {
+                const uint8_t *site = &s.buffer[i * N];
+                for (size_t q = 0; q < N; ++q)
+                    if (site[q] <= WLD_SYM_MISSING) total += c[site[q]];
+            }
             c[5] = total / df;
             for (int k = 0; k < 6; ++k) tab[i * 6 + k] = c[k];
         }
@@ -355,7 +442,7 @@ int wld_henikoff_weights(const wld_siteset *in, float *out) {
             const float *c = &tab[i * 6];
             for (size_t q = lo; q < hi; ++q) w[q] = w[q] + c[site[q]];
         }
-    });
+    }, 64);
     float mx = 0.0f;
     for (size_t q = 0; q < N; ++q) mx = std::fmax(mx, w[q]);
     for (size_t q = 0; q < N; ++q) out[q] = w[q] / mx;
