@@ -168,6 +168,21 @@ def test_dense_vs_oracle_awkward_sites(ctxs, kern):
     dense_check(ctx, buf, w)
 
 
+@pytest.mark.parametrize("kern", KERNELS)
+@pytest.mark.parametrize("N", [1, 2, 3])
+def test_dense_vs_oracle_few_sequences(ctxs, kern, N):
+    # one to three sequences (63 padding lanes of the 64-sequence step): masks
+    # of one or two sequences, T = a single weight, 0/0 NaN rows
+    ctx = _ctx(ctxs, kern)
+    rng = np.random.default_rng(N)
+    buf = rng.choice(5, size=(40, N)).astype(np.uint8)
+    w = (0.3 + rng.random(N)).astype(np.float32)
+    ctx.load(buf, w)
+    dense_check(ctx, buf, w)
+    ctx.run(0.0)
+    compare_rows(ctx.rows(), O.all_pairs(buf, w, 0.0), 0.0, buf=buf, w=w)
+
+
 def test_dense_nonfinite_weights_valu(ctxs):
     # non-finite weights force the SAFE select variant (0*inf must not appear)
     ctx = ctxs["valu"]
