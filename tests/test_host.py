@@ -91,6 +91,13 @@ def test_read_fasta_panic_cases(tmp_path):
     with pytest.raises(W.WldError) as e:
         W.read_fasta(os.path.join(FIXTURES, "t1_henikoff_paper.fasta"))
     assert e.value.name == "WLD_E_FORMAT"
+    # the message reads the lengths before the half-built set is freed (a
+    # use-after-free here once printed garbage and corrupted the heap)
+    assert "sequence 4 has 7, sequence 0 has 8" in str(e.value)
+    for _ in range(3):
+        r = subprocess.run([CLI, "--fasta-input", os.path.join(FIXTURES, "t1_henikoff_paper.fasta"), "--pair-output",
+                            str(tmp_path / "p.tsv")], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 101 and "sequence 0 has 8;" in r.stderr, r.stderr
     p = tmp_path / "empty.fasta"
     p.write_text(">only a header\n")
     with pytest.raises(W.WldError):

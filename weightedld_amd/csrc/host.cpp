@@ -264,10 +264,11 @@ int wld_read_fasta(const char *path, wld_siteset **out) {
         s.n_sites = bytes[0];
         for (size_t i = 0; i < start.size(); ++i)
             if (bytes[i] != s.n_sites) {
+                const size_t n0 = s.n_sites;  // s lives in ss
                 delete ss;
                 return fail(WLD_E_FORMAT,
                             "%s: Not all sequences have the same number of symbols (sequence %zu has %zu, "
-                            "sequence 0 has %zu; lib.rs:180-182)", path, i, bytes[i], s.n_sites);
+                            "sequence 0 has %zu; lib.rs:180-182)", path, i, bytes[i], n0);
             }
         s.buffer.resize(s.n_sites * s.n_seqs);
         s.hist.resize(s.n_sites * 6);
