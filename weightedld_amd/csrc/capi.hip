@@ -205,7 +205,9 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
         const char *lay = getenv("WLD_MFMA_LAYOUT");
         c->use_frag = !(lay && std::string(lay) == "rows");
         if (c->use_frag) {
-            WLD_TRY(ensure(c->frag, c->LP * c->NP));
+            // two copies: the selector-coded one (A operands, and B in the
+            // v_perm build) and the 0/1/2-coded one the B side reads raw
+            WLD_TRY(ensure(c->frag, 2 * c->LP * c->NP));
             launch_frag(ptr<uint8_t>(c->codes), c->LP, c->NP, ptr<uint8_t>(c->frag), c->stream);
             HIP_TRY(hipGetLastError());
         }
@@ -337,6 +339,7 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         // anything; WLD_NO_PREFILTER=1 disables it (A/B experiments)
         const bool prefilter = thr > 0.0f && !getenv("WLD_NO_PREFILTER");
         launch_pair_mfma(ptr<uint8_t>(c->codes), c->use_frag ? ptr<uint8_t>(c->frag) : nullptr,
+                         c->use_frag ? ptr<uint8_t>(c->frag) + c->LP * c->NP : nullptr,
                          ptr<int8_t>(c->planes), ptr<uint32_t>(c->tiles), c->n_tiles, (uint32_t)c->L,
                          (uint32_t)c->NP, n, thr, c->shift, c->plane_mask, prefilter, o, dense, c->stream);
     } else

@@ -61,12 +61,13 @@ bool mfma_supported();
 size_t mfma_planes_bytes(size_t LP, size_t NP);
 void launch_mfma_prep(const uint8_t *site_ok, const float *w_pad, size_t L, size_t LP, size_t NP, int shift,
                       int8_t *planes, hipStream_t s);
+// frag holds 2 LP NP bytes: selector-coded, then 0/1/2-coded (B operands)
 void launch_frag(const uint8_t *codes, size_t LP, size_t NP, uint8_t *frag, hipStream_t s);
 // frag != nullptr: LDS-streaming kernel on the fragment-major copy; else the
 // site-major kernel
 // plane_mask: the weight-digit planes with a nonzero digit (mfma_plane_mask);
 // the LDS kernel runs 4 MFMA products per active plane
-void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const int8_t *wplanes, const uint32_t *tiles,
+void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const uint8_t *frag_b, const int8_t *wplanes, const uint32_t *tiles,
                       uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
                       unsigned plane_mask, bool prefilter, const OrderArgs &o, const DenseArgs *dense,
                       hipStream_t s);

@@ -124,19 +124,23 @@ __global__ __launch_bounds__(256) void frag_kernel(const uint8_t *__restrict__ c
     const uint32_t kb = t % NKB;
     const size_t g = t / NKB;
     const uint4 v = *reinterpret_cast<const uint4 *>(codes + (g * 32 + (l & 31)) * NP + kb * 32 + (l >> 5) * 16);
-    uint32_t in[4] = {v.x, v.y, v.z, v.w}, out[4];
+    uint32_t in[4] = {v.x, v.y, v.z, v.w}, out[4], raw[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-        uint32_t o = 0;
+        uint32_t o = 0, r = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t c = (in[e] >> (8 * j)) & 0xFF;
             const uint32_t sel = (c & kCodeIn) ? ((c & kCodeMaj) ? 4u + j : (uint32_t)j) : 12u;
             o |= sel << (8 * j);
+            r |= ((c & kCodeIn) ? ((c & kCodeMaj) ? 2u : 1u) : 0u) << (8 * j);
         }
         out[e] = o;
+        raw[e] = r;
     }
     *reinterpret_cast<uint4 *>(frag + idx * 16) = make_uint4(out[0], out[1], out[2], out[3]);
+    // the B-side copy: 0 (not major/minor), 1 (minor), 2 (major) = minor + 2 major
+    *reinterpret_cast<uint4 *>(frag + (size_t)LP * NP + idx * 16) = make_uint4(raw[0], raw[1], raw[2], raw[3]);
 }
 
 __device__ __forceinline__ v16i mfma_i8(v4i a, v4i b, v16i c) {
@@ -170,7 +174,17 @@ template <int NPL>
 struct Acc16 {
     static constexpr int kPlanes = NPL;
     v4i v[4][2][NPL][2];  // [n][channel_a][plane][channel_b]
+#ifdef WLD_BPERM
     __device__ __forceinline__ int get(int x, int p, int y, int i) const { return v[i >> 2][x][p][y][i & 3]; }
+#else
+    // channel_b slots hold X = S(raw) = S(minor) + 2 S(major) and Y = S(minor)
+    // (mfma_block_sel16): S(in) = (X + Y) / 2, S(major) = (X - Y) / 2, both
+    // exact (X - Y is even) and in int32 range (|X| + |Y| <= 3 * 128 NP)
+    __device__ __forceinline__ int get(int x, int p, int y, int i) const {
+        const int X = v[i >> 2][x][p][0][i & 3], Y = v[i >> 2][x][p][1][i & 3];
+        return (y ? X - Y : X + Y) >> 1;
+    }
+#endif
     static __device__ __forceinline__ uint32_t a_local(int i, uint32_t wave, uint32_t lane) {
         return 16 * wave + 4 * (lane >> 4) + (i & 3);
     }
@@ -195,8 +209,13 @@ __device__ __forceinline__ void mfma_block_sel16(v4i (&acc)[4][2][NPL][2], v4i c
     for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
+#ifdef WLD_BPERM  // selector-coded B: in / major indicators, two v_perm per dword
             b_in[n][e] = (int)__builtin_amdgcn_perm(kOnes, kOnes, (unsigned)cb[n][e]);
             b_maj[n][e] = (int)__builtin_amdgcn_perm(kOnes, 0u, (unsigned)cb[n][e]);
+#else  // 0/1/2-coded B: the raw bytes (minor + 2 major) and the minor bit, one v_and per dword
+            b_in[n][e] = cb[n][e];
+            b_maj[n][e] = cb[n][e] & (int)kOnes;
+#endif
         }
 #pragma unroll
     for (int p = 0; p < NPL; ++p) {
@@ -480,6 +499,7 @@ __device__ __forceinline__ void tile_epilogue(const Acc &acc, uint32_t ta, uint3
 // the 41 MB code copy of BASELINE config 4 is served from L2/MALL either way.)
 template <bool DENSE, bool PREFILTER, int NPL>
 __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__restrict__ frag,
+                                                            const uint8_t *__restrict__ frag_b,
                                                             const int8_t *__restrict__ planes,
                                                             const uint64_t *__restrict__ ok_bits,
                                                             const uint32_t *__restrict__ tiles, uint32_t L,
@@ -502,7 +522,12 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
 
     // this wave's 1 KB code block per stage: A0/A1 (a sites), B0/B1 (b sites)
     const uint32_t g = wave < 2 ? 2 * ta + wave : 2 * tb + (wave - 2);
+#ifdef WLD_BPERM
+    (void)frag_b;
     const uint8_t *src = frag + (size_t)g * NKB * 1024;  // wave-uniform
+#else
+    const uint8_t *src = (wave < 2 ? frag : frag_b) + (size_t)g * NKB * 1024;  // wave-uniform
+#endif
     const int8_t *digf = planes + digf_offset(NP);
     const uint32_t smem_lds = lds_addr(smem);
     auto issue = [&](uint32_t grp, uint32_t buf) {
@@ -640,19 +665,19 @@ void launch_frag(const uint8_t *codes, size_t LP, size_t NP, uint8_t *frag, hipS
 }
 
 template <int NPL>
-void launch_lds(const uint8_t *frag, const int8_t *wplanes, const uint64_t *ok_bits, const uint32_t *tiles,
+void launch_lds(const uint8_t *frag, const uint8_t *frag_b, const int8_t *wplanes, const uint64_t *ok_bits, const uint32_t *tiles,
                 uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
                 uint32_t plane_idx, bool prefilter, const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
     const DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
     const dim3 g(n_tiles), b(256);
     if (dense)
-        hipLaunchKernelGGL((pair_mfma_kernel<true, false, NPL>), g, b, 0, s, frag, wplanes, ok_bits, tiles, L,
+        hipLaunchKernelGGL((pair_mfma_kernel<true, false, NPL>), g, b, 0, s, frag, frag_b, wplanes, ok_bits, tiles, L,
                            NP, n_chunk_rows, thr, shift, plane_idx, o, dn);
     else if (prefilter)
-        hipLaunchKernelGGL((pair_mfma_kernel<false, true, NPL>), g, b, 0, s, frag, wplanes, ok_bits, tiles, L,
+        hipLaunchKernelGGL((pair_mfma_kernel<false, true, NPL>), g, b, 0, s, frag, frag_b, wplanes, ok_bits, tiles, L,
                            NP, n_chunk_rows, thr, shift, plane_idx, o, dn);
     else
-        hipLaunchKernelGGL((pair_mfma_kernel<false, false, NPL>), g, b, 0, s, frag, wplanes, ok_bits, tiles, L,
+        hipLaunchKernelGGL((pair_mfma_kernel<false, false, NPL>), g, b, 0, s, frag, frag_b, wplanes, ok_bits, tiles, L,
                            NP, n_chunk_rows, thr, shift, plane_idx, o, dn);
 }
 
@@ -664,7 +689,7 @@ unsigned mfma_plane_mask(const int8_t *wplanes, size_t LP, size_t NP, hipStream_
     return m & 7;
 }
 
-void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const int8_t *wplanes, const uint32_t *tiles,
+void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const uint8_t *frag_b, const int8_t *wplanes, const uint32_t *tiles,
                       uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
                       unsigned plane_mask, bool prefilter, const OrderArgs &o, const DenseArgs *dense,
                       hipStream_t s) {
@@ -680,13 +705,13 @@ void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const int8_t *w
         for (uint32_t p = 0; p < 3; ++p)
             if (plane_mask >> p & 1) idx |= p << (2 * n++);
         if (n == 3)
-            launch_lds<3>(frag, wplanes, ok_bits, tiles, n_tiles, L, NP, n_chunk_rows, thr, shift, idx, prefilter, o,
+            launch_lds<3>(frag, frag_b, wplanes, ok_bits, tiles, n_tiles, L, NP, n_chunk_rows, thr, shift, idx, prefilter, o,
                           dense, s);
         else if (n == 2)
-            launch_lds<2>(frag, wplanes, ok_bits, tiles, n_tiles, L, NP, n_chunk_rows, thr, shift, idx, prefilter, o,
+            launch_lds<2>(frag, frag_b, wplanes, ok_bits, tiles, n_tiles, L, NP, n_chunk_rows, thr, shift, idx, prefilter, o,
                           dense, s);
         else
-            launch_lds<1>(frag, wplanes, ok_bits, tiles, n_tiles, L, NP, n_chunk_rows, thr, shift, idx, prefilter, o,
+            launch_lds<1>(frag, frag_b, wplanes, ok_bits, tiles, n_tiles, L, NP, n_chunk_rows, thr, shift, idx, prefilter, o,
                           dense, s);
     } else {
         if (dense)
