@@ -185,11 +185,19 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     const float maxabs = ws[0], minabs = ws[1];
     // MFMA planes hold w * 2^shift in 24-bit fixed point; AUTO keeps the f32
     // VALU kernel when that could lose precision ("Kernel choice").
-    const bool mfma_ok = mfma_supported() && finite && maxabs > 0.0f && minabs >= maxabs * 0x1p-10f;
+    // The int32 accumulators hold X = S(minor) + 2 S(major) and Y = S(minor)
+    // with |X| + |Y| <= 3 * 128 * NP (pair_mfma.hip, Acc16::get): NP < 2^31 / 384.
+    constexpr size_t kMfmaMaxNP = 5592320;
+    const bool mfma_fits = c->NP <= kMfmaMaxNP;
+    const bool mfma_ok =
+        mfma_supported() && mfma_fits && finite && maxabs > 0.0f && minabs >= maxabs * 0x1p-10f;
     int k = c->kernel_pref;
     if (k == WLD_KERNEL_AUTO) k = mfma_ok ? WLD_KERNEL_MFMA : WLD_KERNEL_VALU;
     if (k == WLD_KERNEL_MFMA && !(mfma_supported() && finite && maxabs > 0.0f))
         return fail(WLD_E_ARG, "MFMA kernel requested but weights are not finite/nonzero");
+    if (k == WLD_KERNEL_MFMA && !mfma_fits)
+        return fail(WLD_E_ARG, "MFMA kernel requested but %zu sequences exceed its int32 sums (max %zu)", N,
+                    kMfmaMaxNP);
     c->kernel = k;
     c->safe = !finite;
     c->shift = 0;
