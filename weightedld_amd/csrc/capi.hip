@@ -298,6 +298,42 @@ void rows_to_linear(uint32_t n, uint32_t rb, uint32_t re, uint32_t &lb, uint32_t
     le = re > rb ? chunk_linear(n, rb, rb) + (n - rb) : 0;
 }
 
+// L2-aware launch order (default; WLD_TILE_ORDER=rows keeps plain (ta, tb)
+// order): workgroups are dealt to the 8
+// XCDs round-robin by launch index, so position 8i + x is XCD x's i-th tile.
+// Each XCD gets whole 8x8-tile super-blocks (greedy, least-loaded first), so
+// the ~64 tiles resident on its 32 CUs read 8 A and 8 B tile columns (2 MB at
+// C4) that fit its 4 MB L2.  Short queues are padded with kNoTile entries,
+// which the pair kernels skip.
+std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t) {
+    constexpr uint32_t kX = 8, kS = 8;
+    std::vector<std::vector<uint32_t>> blocks;
+    uint64_t last = ~0ull;
+    std::vector<uint32_t> sorted(t);
+    std::sort(sorted.begin(), sorted.end(), [](uint32_t x, uint32_t y) {
+        const uint32_t bx = ((x >> 16) / kS) << 16 | ((x & 0xFFFFu) / kS), by = ((y >> 16) / kS) << 16 | ((y & 0xFFFFu) / kS);
+        return bx != by ? bx < by : x < y;
+    });
+    for (uint32_t v : sorted) {
+        const uint64_t key = ((v >> 16) / kS) << 16 | ((v & 0xFFFFu) / kS);
+        if (key != last) blocks.emplace_back(), last = key;
+        blocks.back().push_back(v);
+    }
+    std::vector<std::vector<uint32_t>> q(kX);
+    for (auto &b : blocks) {
+        size_t x = 0;
+        for (size_t k = 1; k < kX; ++k)
+            if (q[k].size() < q[x].size()) x = k;
+        q[x].insert(q[x].end(), b.begin(), b.end());
+    }
+    size_t len = 0;
+    for (auto &v : q) len = std::max(len, v.size());
+    std::vector<uint32_t> out(len * kX, kNoTile);
+    for (size_t x = 0; x < kX; ++x)
+        for (size_t i = 0; i < q[x].size(); ++i) out[i * kX + x] = q[x][i];
+    return out;
+}
+
 // 64x64 tiles (tb >= ta) of the chunks [lb, le), sorted (ta, tb) so a row of
 // tiles shares its A columns in L2 as in a whole-row run
 int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
@@ -314,6 +350,8 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
                 t.push_back((ta << 16) | tb);
     }
     std::sort(t.begin(), t.end());
+    const char *ord = getenv("WLD_TILE_ORDER");
+    if (!(ord && std::string(ord) == "rows") && t.size() > 512 && T_used < 65535) t = xcd_order(t);
     c->n_tiles = (uint32_t)t.size();
     WLD_TRY(ensure(c->tiles, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));
     if (!t.empty())

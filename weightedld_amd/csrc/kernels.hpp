@@ -12,6 +12,8 @@ constexpr int kChunk = 256;      // reference chunk side, lib.rs:615
 constexpr int kTile = 64;        // pair-kernel tile side (sites); 4 tiles per chunk side
 constexpr int kSeqPad = 64;      // sequences padded to a multiple of this
 constexpr int kTilesPerChunk = kChunk / kTile;
+// an empty slot of a reordered tile list (never a real tile: T_used < 65535 there)
+constexpr uint32_t kNoTile = 0xFFFFFFFFu;
 
 // Code byte per (site, sequence): bit0 = sequence is major or minor at the site
 // ("in" the pair mask, lib.rs:435), bit1 = sequence is major (lib.rs:430,432).

@@ -518,6 +518,7 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
     const unsigned long long ts0 = stamp();
 #endif
     const uint32_t tile = tiles[blockIdx.x];
+    if (tile == kNoTile) return;  // padding of an XCD-ordered list (whole workgroup)
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
 
     // this wave's 1 KB code block per stage: A0/A1 (a sites), B0/B1 (b sites)
@@ -628,6 +629,7 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_rows_kernel(const uint8_t *_
     __shared__ unsigned long long sBits[kTile];
     __shared__ uint32_t sRowBase[kTile];
     const uint32_t tile = tiles[blockIdx.x];
+    if (tile == kNoTile) return;  // padding of an XCD-ordered list (whole workgroup)
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t wa = wave >> 1, wb = wave & 1, r = lane & 31, h = lane >> 5;

@@ -36,6 +36,7 @@ __global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__rest
     __shared__ __attribute__((aligned(16))) float sW[64];
 
     const uint32_t tile = tiles[blockIdx.x];
+    if (tile == kNoTile) return;  // padding of an XCD-ordered list (whole workgroup)
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
     const uint32_t a0 = ta * kTile, b0 = tb * kTile;
     const uint32_t tid = threadIdx.x;
