@@ -57,7 +57,18 @@ constexpr int kGroup = 8;                           // 32-sequence stages per LD
 constexpr int kStageCodes = 4096;                   // A0 A1 B0 B1, 1 KB each
 constexpr int kDigStage = 128;                      // digit bytes per stage: [plane][half][16] + 32 pad
 constexpr int kDigGroup = 1024;                     // digit records of one group: one full-wave DMA
-constexpr int kGroupBytes = kGroup * kStageCodes + kDigGroup;  // two groups in LDS
+// stages per LDS group of the kernel with NPL active digit planes: one plane
+// (equal weights) uses 4-stage groups, 34 KB of LDS per workgroup and 108
+// VGPRs, so four workgroups (4 waves per SIMD) share a CU
+#ifndef WLD_KG1
+#define WLD_KG1 4
+#endif
+template <int NPL>
+struct GroupShape {
+    static constexpr int kStages = NPL == 1 ? WLD_KG1 : kGroup;
+    static constexpr int kBytes = kStages * kStageCodes + kDigGroup;
+    static constexpr int kWgPerCu = NPL == 1 && WLD_KG1 <= 4 ? 4 : 2;
+};
 
 __host__ __device__ inline size_t digf_offset(size_t NP) { return 3 * NP; }
 __host__ __device__ inline size_t okbits_offset(size_t NP) {
@@ -76,7 +87,8 @@ __host__ __device__ inline size_t digf_stage(uint32_t kb) { return (size_t)(kb /
 //   ok_bits[g] bit i = site 64g+i passes  (site_ok, lib.rs:400-408)
 //   plane_mask (u32 after the bits)       bit p = some digit of plane p is nonzero
 __host__ __device__ inline size_t planemask_offset(size_t LP, size_t NP) { return okbits_offset(NP) + LP / 64 * 8; }
-size_t mfma_planes_bytes(size_t LP, size_t NP) { return planemask_offset(LP, NP) + 16; }
+// + 1 KB: a half-group (kg < kGroup) digit DMA copies 1 KB from a 512-B offset
+size_t mfma_planes_bytes(size_t LP, size_t NP) { return planemask_offset(LP, NP) + 16 + kDigGroup; }
 
 __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict__ w_pad, uint32_t NP, int shift,
                                                          int8_t *__restrict__ planes, int8_t *__restrict__ digf,
@@ -498,21 +510,22 @@ __device__ __forceinline__ void tile_epilogue(const Acc &acc, uint32_t ta, uint3
 // tile per workgroup.  (An XCD-contiguous block->tile remap measured no gain:
 // the 41 MB code copy of BASELINE config 4 is served from L2/MALL either way.)
 template <bool DENSE, bool PREFILTER, int NPL>
-__global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__restrict__ frag,
+__global__ __launch_bounds__(256, GroupShape<NPL>::kWgPerCu) void pair_mfma_kernel(const uint8_t *__restrict__ frag,
                                                             const uint8_t *__restrict__ frag_b,
                                                             const int8_t *__restrict__ planes,
                                                             const uint64_t *__restrict__ ok_bits,
                                                             const uint32_t *__restrict__ tiles, uint32_t L,
                                                             uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
                                                             uint32_t plane_idx, OrderArgs o, DenseArgs dn) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kGroupBytes];  // operand groups (DMA targets)
+    constexpr int KG = GroupShape<NPL>::kStages, KGB = GroupShape<NPL>::kBytes;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * KGB];  // operand groups (DMA targets)
     __shared__ unsigned long long sBits[kTile];                              // compaction (never a DMA target)
     __shared__ uint32_t sRowBase[kTile];
 
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const uint32_t NKB = NP / 32;
-    const uint32_t n_groups = (NKB + kGroup - 1) / kGroup;
+    const uint32_t n_groups = (NKB + KG - 1) / KG;
 
 #ifdef WLD_EXP_STAMPS
     const unsigned long long ts0 = stamp();
@@ -532,15 +545,17 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
     const int8_t *digf = planes + digf_offset(NP);
     const uint32_t smem_lds = lds_addr(smem);
     auto issue = [&](uint32_t grp, uint32_t buf) {
-        const uint32_t gb = smem_lds + buf * kGroupBytes;
-        const uint32_t kb0 = grp * kGroup;
+        const uint32_t gb = smem_lds + buf * KGB;
+        const uint32_t kb0 = grp * KG;
         const uint8_t *base = src + (size_t)kb0 * 1024;
         const uint32_t lane16 = lane * 16;
 #pragma unroll
-        for (int st = 0; st < kGroup; ++st)
+        for (int st = 0; st < KG; ++st)
             if (kb0 + st < NKB) glds16(base + (uint32_t)(st * 1024) + lane16, gb + st * kStageCodes + wave * 1024);
-        if (wave == 0)  // digit records of the group = 1 KB (allocation padded to whole groups)
-            glds16(digf + (size_t)grp * kDigGroup + lane16, gb + kGroup * kStageCodes);
+        // digit records of the group's stages (128 B each, contiguous from
+        // digf_stage(kb0)): one 1 KB full-wave copy (allocation padded past
+        // the last group)
+        if (wave == 0) glds16(digf + digf_stage(kb0) + lane16, gb + KG * kStageCodes);
     };
 
     issue(0, 0);
@@ -554,7 +569,7 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
     const uint32_t lrow = so * kStageCodes + (32 * hh + (lane & 15)) * 16;
     const uint32_t offA = lrow + (wave >> 1) * 1024 + (wave & 1) * 256;
     const uint32_t offB = lrow + 2048;  // + (n >> 1) * 1024 + (n & 1) * 256
-    const uint32_t offD = kGroup * kStageCodes + so * kDigStage + hh * 16;
+    const uint32_t offD = KG * kStageCodes + so * kDigStage + hh * 16;
     // the active planes' 32-byte rows of a stage's digit record (all three:
     // compile-time offsets, so the reads keep immediate offsets)
     uint32_t offP[NPL];
@@ -576,8 +591,8 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_kernel(const uint8_t *__rest
         if (grp == 0) tsg = stamp();
 #endif
         if (grp + 1 < n_groups) issue(grp + 1, buf ^ 1);
-        const uint8_t *gb = smem + buf * kGroupBytes;
-        const uint32_t n_st = min((uint32_t)kGroup, NKB - grp * kGroup);
+        const uint8_t *gb = smem + buf * KGB;
+        const uint32_t n_st = min((uint32_t)KG, NKB - grp * KG);
         for (uint32_t st = 0; st < n_st; st += 2) {  // n_st is even: NP is a multiple of 64
             const uint8_t *sc = gb + st * kStageCodes;
             const uint8_t *sd = gb + st * kDigStage;
