@@ -63,11 +63,14 @@ constexpr int kDigGroup = 1024;                     // digit records of one grou
 #ifndef WLD_KG1
 #define WLD_KG1 4
 #endif
+#ifndef WLD_WG1
+#define WLD_WG1 (WLD_KG1 <= 4 ? 4 : 2)
+#endif
 template <int NPL>
 struct GroupShape {
     static constexpr int kStages = NPL == 1 ? WLD_KG1 : kGroup;
     static constexpr int kBytes = kStages * kStageCodes + kDigGroup;
-    static constexpr int kWgPerCu = NPL == 1 && WLD_KG1 <= 4 ? 4 : 2;
+    static constexpr int kWgPerCu = NPL == 1 ? WLD_WG1 : 2;
 };
 
 __host__ __device__ inline size_t digf_offset(size_t NP) { return 3 * NP; }
