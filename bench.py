@@ -32,7 +32,7 @@ CONFIGS = {
 }
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 I8_MFMA_PEAK_TOPS = 5000.0  # dense i8 MFMA = 2x bf16 dense 2.5 PF (MI355X_MICROARCH.md Matrix cores)
-F32_VALU_PEAK_TFLOPS = 157.3  # FP32 vector peak (spec)
+F32_VALU_PEAK_TFLOPS = 157.3  # FP32 vector peak (spec) = f32-input MFMA peak
 
 
 def synth(L, N, seed=0x5EED, block=4096):
@@ -252,8 +252,10 @@ def main():
     else:
         ops = shard_pairs * 8.0 * N  # 4 masked f32 sums x N seqs x 2 flops/FMA
         achieved = ops / (kernel_ms * 1e-3) / 1e12
-        roof = {"bound": "valu", "achieved": achieved, "peak": F32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": achieved / F32_VALU_PEAK_TFLOPS}
+        # finite weights: f32-input MFMA (v_mfma_f32_16x16x4_f32), whose peak is the
+        # f32 vector peak (MI355X_MICROARCH.md, Matrix cores: F32 row)
+        roof = {"bound": "mfma", "achieved": achieved, "peak": F32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / F32_VALU_PEAK_TFLOPS, "path": "f32 MFMA 16x16x4"}
     roof["kernel"] = "pair_%s_kernel" % kern_name
     roof["kernel_ms"] = kernel_ms
     tr = load_traffic(args.config + ("-unweighted" if args.unweighted else ""), kern_name)

@@ -1,5 +1,8 @@
-// f32 VALU pair kernel: the exact-f32 path (and the fallback for weights the
-// MFMA kernel's fixed-point planes cannot hold exactly).
+// f32 pair kernel: the exact-f32 path (and the fallback for weights the
+// integer MFMA kernel's fixed-point planes cannot hold exactly).  For finite
+// weights the products and sums run on f32-input MFMA (MF below); the VALU
+// loop described next is the SAFE (non-finite weights) path and the
+// WLD_VALU_PLAIN=1 variant.
 //
 // Replaces the inner loop of single_weighted_ld_pair (lib.rs:416-480) for a
 // 64x64 tile of site pairs per 256-thread workgroup.  Each thread owns a 4x4
@@ -24,7 +27,19 @@ namespace {
 constexpr int kStride = 68;  // LDS row stride in bytes (17 dwords: conflict-free b reads)
 }
 
-template <bool DENSE, bool SAFE>
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+// MF = true: the products and f32 sums of the non-SAFE path on the matrix
+// cores, v_mfma_f32_16x16x4_f32 (f32 inputs, exact products, an f32 fma chain
+// over k: the same terms in the same sequence order as the VALU loop).  Wave w
+// owns a rows 16w..16w+15 against the tile's 64 b columns in four 16x16
+// blocks; lane l = 16g + r carries a row r (A) / b column r (B) at sequence
+// kk + g, and holds the sums of pairs (a = 16w + 4g + e, b = 16n + r) — the
+// same thread -> (4 a rows, 4 b columns) shape as the VALU mapping (a = ty +
+// 16i), so the epilogue and compaction only change how a row slot maps to a.
+// The VALU's code extraction then overlaps the matrix pipe instead of
+// competing with the FMAs for VALU issue.
+template <bool DENSE, bool SAFE, bool MF>
 __global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__restrict__ codes,
                                                          const float *__restrict__ w,
                                                          const uint8_t *__restrict__ site_ok,
@@ -49,6 +64,9 @@ __global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__rest
     // sums (lib.rs:418-445) lose N/8*2^-24; blocks of ~sqrt(N) sequences
     // (flush = round(sqrt(NP)/64), launch_pair_valu) leave ~2 sqrt(N)*2^-24.
     float acc[4][4][4], tot[4][4][4];
+    v4f accM[4][4];  // MF: [b block n][sum q], element e = a row slot
+    // a row of the tile for row slot i of this thread (b = tx + 16 j either way)
+    auto arow = [&](int i) -> uint32_t { return MF ? 4 * ty + i : ty + 16 * i; };
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -79,8 +97,33 @@ __global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__rest
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) acc[i][j][q] = 0.0f;
+                    for (int q = 0; q < 4; ++q) {
+                        acc[i][j][q] = 0.0f;
+                        accM[j][q][i] = 0.0f;
+                    }
         }
+
+        if constexpr (MF) {
+            const uint32_t lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+            const uint8_t *rowA = sA + (16 * wave + r) * kStride + g;
+            const uint8_t *rowB = sB + r * kStride + g;
+#pragma unroll 4
+            for (int kk = 0; kk < 64; kk += 4) {
+                const float we = sW[kk + g];
+                const uint32_t ca = rowA[kk];
+                const float u = (ca & kCodeIn) ? we : 0.0f;
+                const float v = (ca & kCodeMaj) ? we : 0.0f;
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const uint32_t cb = rowB[16 * n * kStride + kk];
+                    const float fi = (float)(cb & 1u), fm = (float)(cb >> 1);
+                    accM[n][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fi, accM[n][0], 0, 0, 0);
+                    accM[n][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fi, accM[n][1], 0, 0, 0);
+                    accM[n][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fm, accM[n][2], 0, 0, 0);
+                    accM[n][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fm, accM[n][3], 0, 0, 0);
+                }
+            }
+        } else
 
 #pragma unroll 2
         for (int kk = 0; kk < 64; kk += 4) {
@@ -141,7 +184,7 @@ __global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__rest
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) tot[i][j][q] += acc[i][j][q];
+                    for (int q = 0; q < 4; ++q) tot[i][j][q] += MF ? accM[j][q][i] : acc[i][j][q];
         }
     }
 
@@ -150,7 +193,7 @@ __global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__rest
     float res[4][4][3];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const uint32_t a = a0 + ty + 16 * i;
+        const uint32_t a = a0 + arow(i);
         const bool oka = a < L && site_ok[a];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -182,7 +225,7 @@ __global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__rest
     __shared__ uint16_t sRowP[kTile][4];
     __shared__ uint32_t sRowBase[kTile];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sMask[ty + 16 * i][tx] = (uint8_t)passmask[i];
+    for (int i = 0; i < 4; ++i) sMask[arow(i)][tx] = (uint8_t)passmask[i];
     __syncthreads();
     if (tid < kTile) {
         const uint32_t r = tid;
@@ -217,7 +260,7 @@ __global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__rest
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         if (!passmask[i]) continue;
-        const uint32_t r = ty + 16 * i;
+        const uint32_t r = arow(i);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (!(passmask[i] & (1u << j))) continue;
@@ -238,20 +281,30 @@ void launch_pair_valu(const uint8_t *codes, const float *w, const uint8_t *site_
                       const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
     DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
     const uint32_t flush = (uint32_t)std::max(1.0, std::floor(std::sqrt((double)NP) / 64.0 + 0.5));
+    // finite weights: products and sums on the matrix cores (WLD_VALU_PLAIN=1:
+    // the VALU loop, for A/B); non-finite weights keep the select loop
+    static const bool plain = getenv("WLD_VALU_PLAIN") != nullptr;
+    const dim3 g(n_tiles), b(256);
     if (dense) {
         if (safe)
-            hipLaunchKernelGGL((pair_valu_kernel<true, true>), dim3(n_tiles), dim3(256), 0, s, codes, w, site_ok, tiles,
-                               L, NP, flush, n_chunk_rows, thr, o, dn);
+            hipLaunchKernelGGL((pair_valu_kernel<true, true, false>), g, b, 0, s, codes, w, site_ok, tiles, L, NP,
+                               flush, n_chunk_rows, thr, o, dn);
+        else if (plain)
+            hipLaunchKernelGGL((pair_valu_kernel<true, false, false>), g, b, 0, s, codes, w, site_ok, tiles, L, NP,
+                               flush, n_chunk_rows, thr, o, dn);
         else
-            hipLaunchKernelGGL((pair_valu_kernel<true, false>), dim3(n_tiles), dim3(256), 0, s, codes, w, site_ok,
-                               tiles, L, NP, flush, n_chunk_rows, thr, o, dn);
+            hipLaunchKernelGGL((pair_valu_kernel<true, false, true>), g, b, 0, s, codes, w, site_ok, tiles, L, NP,
+                               flush, n_chunk_rows, thr, o, dn);
     } else {
         if (safe)
-            hipLaunchKernelGGL((pair_valu_kernel<false, true>), dim3(n_tiles), dim3(256), 0, s, codes, w, site_ok,
-                               tiles, L, NP, flush, n_chunk_rows, thr, o, dn);
+            hipLaunchKernelGGL((pair_valu_kernel<false, true, false>), g, b, 0, s, codes, w, site_ok, tiles, L, NP,
+                               flush, n_chunk_rows, thr, o, dn);
+        else if (plain)
+            hipLaunchKernelGGL((pair_valu_kernel<false, false, false>), g, b, 0, s, codes, w, site_ok, tiles, L, NP,
+                               flush, n_chunk_rows, thr, o, dn);
         else
-            hipLaunchKernelGGL((pair_valu_kernel<false, false>), dim3(n_tiles), dim3(256), 0, s, codes, w, site_ok,
-                               tiles, L, NP, flush, n_chunk_rows, thr, o, dn);
+            hipLaunchKernelGGL((pair_valu_kernel<false, false, true>), g, b, 0, s, codes, w, site_ok, tiles, L, NP,
+                               flush, n_chunk_rows, thr, o, dn);
     }
 }
 
