@@ -351,7 +351,9 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
     }
     std::sort(t.begin(), t.end());
     const char *ord = getenv("WLD_TILE_ORDER");
-    if (!(ord && std::string(ord) == "rows") && t.size() > 512 && T_used < 65535) t = xcd_order(t);
+    // only with many rounds of resident tiles: whole super-blocks per XCD
+    // leave up to one super-block of imbalance (C2's 528 tiles: +14%)
+    if (!(ord && std::string(ord) == "rows") && t.size() >= 4096 && T_used < 65535) t = xcd_order(t);
     c->n_tiles = (uint32_t)t.size();
     WLD_TRY(ensure(c->tiles, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));
     if (!t.empty())
