@@ -128,6 +128,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--unweighted", action="store_true", help="unit weights (main.rs:150-153 --unweighted)")
     ap.add_argument("--thr", type=float, help="override the config's r2 threshold (non-headline lines)")
+    ap.add_argument("--rehearse-dist", action="store_true",
+                    help="at N=1: run the N>1 step path (RCCL group of one, ShardStep/pipelined steps)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="N>1: one ShardStep at a time (no overlap of a step's count exchange with the next kernel)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -141,7 +145,12 @@ def main():
 
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    if world > 1:
+    dist_on = world > 1 or args.rehearse_dist  # the N>1 step path (a group of one when rehearsing)
+    if dist_on:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29571")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=device)
 
     sys.path.insert(0, REPO)
@@ -192,24 +201,42 @@ def main():
     # rows (if any) then gathered to rank 0 in reference order (shards
     # concatenate in descending rank order: chunk rows descend)
     shard_step = wdist.ShardStep(ctx, rank, world, device)
+    # N>1 timed steps: two contexts on the same resident inputs, step i's
+    # kernel queued on the device behind step i-1's while step i-1's count
+    # exchange / host read / row gather complete (PipelinedShardStep)
+    pipe = None
+    if dist_on and not args.no_pipeline:
+        ctx2 = W.Context(local_rank, kernel)
+        ctx2.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
+        pipe = wdist.PipelinedShardStep([ctx, ctx2], rank, world, device)
+
+    def nrows(res):
+        return int(res[1].shape[1]) if res is not None and res[1] is not None else 0
 
     def step():
-        if world == 1:
+        if not dist_on:
             return ctx.run_chunks(thr, cb, ce)
         _, rows = shard_step(thr, cb, ce)
         return int(rows.shape[1]) if rows is not None else 0
 
-    for _ in range(args.warmup):
-        step()
-    if world > 1:
+    def run_steps(k):
+        if pipe is None:
+            r = 0
+            for _ in range(k):
+                r = step()
+            return r
+        for _ in range(k):
+            pipe.submit(thr, cb, ce)
+        return nrows(pipe.drain())
+
+    run_steps(args.warmup)
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    rows = 0
-    for _ in range(args.steps):
-        rows = step()
+    rows = run_steps(args.steps)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     # per-launch HIP-event times of the same steps, sampled after the timed
@@ -222,7 +249,7 @@ def main():
         kms.append(st["pair_kernel_ms"])
         oms.append(st["order_ms"])
         gms.append((time.perf_counter() - tg) * 1e3 - st["pair_kernel_ms"])
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -236,7 +263,7 @@ def main():
     planes = st["mfma_planes"]
 
     if rank != 0:
-        if world > 1:
+        if dist_on:
             dist.destroy_process_group()
         return
 
@@ -277,7 +304,8 @@ def main():
             "unit (--unweighted)" if args.unweighted else "Henikoff"),
         "config": {"workload": desc, "n_seqs": N, "n_sites": L, "r2_threshold": thr, "pairs": total_pairs,
                    "rows_passing": rows, "kernel": kern_name, "mfma_planes": planes,
-                   "parallelism": "chunk-range shard x%d%s" % (world, " + RCCL gather" if world > 1 else "")},
+                   "parallelism": "chunk-range shard x%d%s" % (
+                       world, (" + RCCL gather" + (", pipelined steps" if pipe is not None else "")) if dist_on else "")},
         "roofline": roof,
         "north_star_hbm_view": {"algorithmic_bytes_per_pair": 2 * N, "achieved_GBps": hbm_alg,
                                 "peak_GBps": HBM_PEAK_GBPS, "frac": hbm_alg / HBM_PEAK_GBPS},
@@ -291,7 +319,7 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(buf, weights, thr, args.cpu_seconds)
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -624,6 +624,51 @@ def test_shard_step_world1_rccl(W, ctxs):
         dist.destroy_process_group()
 
 
+def test_pipelined_shard_step_world1_rccl(W):
+    # PipelinedShardStep (the bench's N>1 timed loop): two contexts on the same
+    # inputs, step i's kernel queued behind step i-1's on the device while
+    # step i-1 completes.  Every step's rows equal the oracle's, in order,
+    # across threshold changes, steps with and without rows, and a drain.
+    import torch
+    import torch.distributed as dist
+    from weightedld_amd import dist as wdist
+
+    L, N = 700, 256
+    buf = synth(L, N, 79)
+    w = np.random.default_rng(8).random(N).astype(np.float32) + 0.1
+    ctxs2 = [W.Context(0, W.KERNEL_MFMA), W.Context(0, W.KERNEL_MFMA)]
+    for c in ctxs2:
+        c.load(buf, w)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = "29562"
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        pipe = wdist.PipelinedShardStep(ctxs2, 0, 1, dev)
+        thrs = [0.0, 0.02, 2.0, 0.02, 0.0, 2.0, 2.0, 0.01]
+        refs = {t: O.all_pairs(buf, w, t) for t in set(thrs)}
+        results = []
+        for i, t in enumerate(thrs):
+            r = pipe.submit(t, 0, 0)
+            assert (r is None) == (i == 0)
+            if r is not None:
+                results.append(r)
+        results.append(pipe.drain())
+        assert pipe.drain() is None
+        assert len(results) == len(thrs)
+        for t, (n, rows) in zip(thrs, results):
+            ref = refs[t]
+            got = wdist.unpack_rows(rows)
+            assert n == rows.shape[1] == len(ref["site_a"])
+            assert list(zip(got["site_a"].tolist(), got["site_b"].tolist())) == \
+                list(zip(ref["site_a"].tolist(), ref["site_b"].tolist()))
+            assert np.abs(got["r2"].astype(np.float64) - ref["r2"]).max(initial=0.0) < 1e-5
+    finally:
+        dist.destroy_process_group()
+        for c in ctxs2:
+            c.close()
+
+
 def test_run_host_batches_concatenate(W, ctxs, monkeypatch):
     # wld_run_host / wld_all_weighted_ld_pairs split the chunk sequence into
     # batches (<= 2^31 pairs; forced small here) and append their rows: the

@@ -111,20 +111,72 @@ class ShardStep:
         self.gather = RowGather(rank, world, device, group)
         self.stream = torch.cuda.ExternalStream(ctx.stream_ptr(), device=device)
 
-    def __call__(self, thr, chunk_begin, chunk_end):
+    def enqueue(self, thr, chunk_begin, chunk_end, kernel_done=None):
+        """The pair kernel, its row count and the count all_gather, on the
+        context's stream; no host wait.  kernel_done (a torch.cuda.Event) is
+        recorded after the kernel, before the collective."""
         import torch
         import torch.distributed as dist
 
         g = self.gather
         with torch.cuda.stream(self.stream):
             self.ctx.run_chunks_async(thr, chunk_begin, chunk_end, g.cnt.data_ptr())
+            if kernel_done is not None:
+                kernel_done.record(self.stream)
             dist.all_gather_into_tensor(g.cnts, g.cnt, group=g.group)
+
+    def finish(self):
+        """Completes an enqueued step: (rows on this rank, gathered rows on rank 0 / None)."""
+        import torch
+
+        g = self.gather
+        with torch.cuda.stream(self.stream):
             counts = g.cnts.tolist()  # the step's one host wait when no rank has rows
         n = self.ctx.run_wait()  # returns at once: the stream is idle
         if max(counts) == 0:
             return n, (g.cnt.new_zeros((5, 0), dtype=torch.int32) if g.rank == 0 else None)
         packed = pack_rows_device(self.ctx, n, g.device)
         return n, (packed if g.world == 1 else g(packed, counts))
+
+    def __call__(self, thr, chunk_begin, chunk_end):
+        self.enqueue(thr, chunk_begin, chunk_end)
+        return self.finish()
+
+
+class PipelinedShardStep:
+    """Back-to-back ShardSteps on two contexts loaded with the same inputs
+    (double-buffered staging and counts).  Step i runs on context i % 2; its
+    pair kernel waits on the device (an event, no host wait) for step i-1's
+    kernel, so kernels still run one at a time, while step i-1's count
+    exchange, host read and (if any rank has rows) row gather overlap step i's
+    kernel.  submit() returns step i-1's result (None for the first step);
+    drain() completes the last one.  Collectives are issued in step order on
+    every rank."""
+
+    def __init__(self, ctxs, rank, world, device, group=None):
+        import torch
+
+        assert len(ctxs) == 2
+        self.steps = [ShardStep(c, rank, world, device, group) for c in ctxs]
+        self.done = [torch.cuda.Event(), torch.cuda.Event()]
+        self.i = 0
+        self.pending = None
+
+    def submit(self, thr, chunk_begin, chunk_end):
+        k = self.i & 1
+        prev = self.pending
+        if prev is not None:
+            self.steps[k].stream.wait_event(self.done[prev])
+        self.steps[k].enqueue(thr, chunk_begin, chunk_end, self.done[k])
+        self.i += 1
+        self.pending = k
+        return self.steps[prev].finish() if prev is not None else None
+
+    def drain(self):
+        if self.pending is None:
+            return None
+        k, self.pending = self.pending, None
+        return self.steps[k].finish()
 
 
 def gather_rows(packed, rank, world, group=None):
