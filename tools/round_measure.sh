@@ -12,6 +12,7 @@ tools/gpu_step.sh 300 $out/bench_c4_valu.log python bench.py --kernel valu --ste
 tools/gpu_step.sh 300 $out/bench_c2.log python bench.py --config c2 --no-cpu-baseline || exit $?
 tools/gpu_step.sh 300 $out/bench_c4_unweighted.log python bench.py --unweighted --no-cpu-baseline || exit $?
 tools/gpu_step.sh 300 $out/bench_c5.log python bench.py --config c5 --steps 5 --warmup 3 --no-cpu-baseline || exit $?
+tools/gpu_step.sh 300 $out/bench_c4_rehearse.log python bench.py --rehearse-dist --no-cpu-baseline || exit $?
 timeout -k 10 600 tools/cli_e2e.sh > $out/cli_e2e.log 2>&1 || { echo "cli_e2e failed $?"; exit 1; }
 cp -r gpurun_out/cli_e2e $out/
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o c4 -- \
