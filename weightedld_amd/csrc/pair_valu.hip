@@ -39,8 +39,11 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 // 16i), so the epilogue and compaction only change how a row slot maps to a.
 // The VALU's code extraction then overlaps the matrix pipe instead of
 // competing with the FMAs for VALU issue.
+#ifndef WLD_VALU_MF_WG
+#define WLD_VALU_MF_WG 2  // MF: 164 VGPRs would fit 3 per CU; measured equal
+#endif
 template <bool DENSE, bool SAFE, bool MF>
-__global__ __launch_bounds__(256, 2) void pair_valu_kernel(const uint8_t *__restrict__ codes,
+__global__ __launch_bounds__(256, MF ? WLD_VALU_MF_WG : 2) void pair_valu_kernel(const uint8_t *__restrict__ codes,
                                                          const float *__restrict__ w,
                                                          const uint8_t *__restrict__ site_ok,
                                                          const uint32_t *__restrict__ tiles, uint32_t L, uint32_t NP,
