@@ -118,8 +118,12 @@ int wld_create(int device, wld_ctx **out);
 void wld_destroy(wld_ctx *ctx);
 
 /* Kernel selection.  AUTO (default): the exact-integer MFMA kernel when the
- * weights are finite and their dynamic range fits its fixed-point weight
- * planes, else the f32 VALU kernel.  Both run on the GPU; there is no CPU path. */
+ * weights are finite, their dynamic range fits its fixed-point weight planes
+ * (min nonzero |w| >= 2^-10 max |w|) and n_seqs <= 5,592,320 (int32 sums),
+ * else the exact-product f32 kernel (WLD_KERNEL_VALU: f32-input MFMA for
+ * finite weights, a VALU loop otherwise).  An explicit WLD_KERNEL_MFMA outside
+ * those bounds fails with WLD_E_ARG at load.  Both run on the GPU; there is no
+ * CPU path. */
 #define WLD_KERNEL_AUTO 0
 #define WLD_KERNEL_VALU 1
 #define WLD_KERNEL_MFMA 2
