@@ -121,9 +121,10 @@ void wld_destroy(wld_ctx *ctx);
  * weights are finite, their dynamic range fits its fixed-point weight planes
  * (min nonzero |w| >= 2^-10 max |w|) and n_seqs <= 5,592,320 (int32 sums),
  * else the exact-product f32 kernel (WLD_KERNEL_VALU: f32-input MFMA for
- * finite weights, a VALU loop otherwise).  An explicit WLD_KERNEL_MFMA outside
- * those bounds fails with WLD_E_ARG at load.  Both run on the GPU; there is no
- * CPU path. */
+ * finite weights, a VALU loop otherwise).  An explicit WLD_KERNEL_MFMA with
+ * non-finite or all-zero weights, or more sequences, fails with WLD_E_ARG at
+ * load (a wide dynamic range is allowed: small weights lose precision).  Both
+ * run on the GPU; there is no CPU path. */
 #define WLD_KERNEL_AUTO 0
 #define WLD_KERNEL_VALU 1
 #define WLD_KERNEL_MFMA 2
