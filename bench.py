@@ -208,7 +208,8 @@ def main():
     if dist_on and not args.no_pipeline:
         ctx2 = W.Context(local_rank, kernel)
         ctx2.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
-        pipe = wdist.PipelinedShardStep([ctx, ctx2], rank, world, device)
+        pipe = wdist.PipelinedShardStep([ctx, ctx2], rank, world, device,
+                                        serialize_kernels=bool(os.environ.get("WLD_PIPE_SERIALIZE")))
 
     def nrows(res):
         return int(res[1].shape[1]) if res is not None and res[1] is not None else 0

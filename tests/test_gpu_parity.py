@@ -624,7 +624,8 @@ def test_shard_step_world1_rccl(W, ctxs):
         dist.destroy_process_group()
 
 
-def test_pipelined_shard_step_world1_rccl(W):
+@pytest.mark.parametrize("serialize", [False, True])
+def test_pipelined_shard_step_world1_rccl(W, serialize):
     # PipelinedShardStep (the bench's N>1 timed loop): two contexts on the same
     # inputs, step i's kernel queued behind step i-1's on the device while
     # step i-1 completes.  Every step's rows equal the oracle's, in order,
@@ -644,7 +645,7 @@ def test_pipelined_shard_step_world1_rccl(W):
     dev = torch.device("cuda", 0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     try:
-        pipe = wdist.PipelinedShardStep(ctxs2, 0, 1, dev)
+        pipe = wdist.PipelinedShardStep(ctxs2, 0, 1, dev, serialize_kernels=serialize)
         thrs = [0.0, 0.02, 2.0, 0.02, 0.0, 2.0, 2.0, 0.01]
         refs = {t: O.all_pairs(buf, w, t) for t in set(thrs)}
         results = []

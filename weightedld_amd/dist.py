@@ -110,6 +110,7 @@ class ShardStep:
         self.ctx = ctx
         self.gather = RowGather(rank, world, device, group)
         self.stream = torch.cuda.ExternalStream(ctx.stream_ptr(), device=device)
+        self.rows_seen = False  # some rank had rows in the last finished step
 
     def enqueue(self, thr, chunk_begin, chunk_end, kernel_done=None):
         """The pair kernel, its row count and the count all_gather, on the
@@ -132,6 +133,7 @@ class ShardStep:
         g = self.gather
         with torch.cuda.stream(self.stream):
             counts = g.cnts.tolist()  # the step's one host wait when no rank has rows
+        self.rows_seen = max(counts) > 0
         n = self.ctx.run_wait()  # returns at once: the stream is idle
         if max(counts) == 0:
             return n, (g.cnt.new_zeros((5, 0), dtype=torch.int32) if g.rank == 0 else None)
@@ -145,27 +147,31 @@ class ShardStep:
 
 class PipelinedShardStep:
     """Back-to-back ShardSteps on two contexts loaded with the same inputs
-    (double-buffered staging and counts).  Step i runs on context i % 2; its
-    pair kernel waits on the device (an event, no host wait) for step i-1's
-    kernel, so kernels still run one at a time, while step i-1's count
-    exchange, host read and (if any rank has rows) row gather overlap step i's
-    kernel.  submit() returns step i-1's result (None for the first step);
+    (double-buffered staging and counts).  Step i runs on context i % 2, so
+    step i-1's count exchange, host read and (if any rank has rows) row gather
+    overlap step i's kernel, and step i's kernel may start in the tail of step
+    i-1's (the contexts share nothing the kernels write).  serialize_kernels=True
+    makes step i's kernel wait on the device (an event, no host wait) for step
+    i-1's, so kernels run one at a time; that is also done while the last
+    finished step had rows, so a step's row copies and gather do not compete
+    with two kernels.  submit() returns step i-1's result (None for the first step);
     drain() completes the last one.  Collectives are issued in step order on
     every rank."""
 
-    def __init__(self, ctxs, rank, world, device, group=None):
+    def __init__(self, ctxs, rank, world, device, group=None, serialize_kernels=False):
         import torch
 
         assert len(ctxs) == 2
         self.steps = [ShardStep(c, rank, world, device, group) for c in ctxs]
         self.done = [torch.cuda.Event(), torch.cuda.Event()]
+        self.serialize = serialize_kernels  # False: step i's kernel may start in step i-1's tail
         self.i = 0
         self.pending = None
 
     def submit(self, thr, chunk_begin, chunk_end):
         k = self.i & 1
         prev = self.pending
-        if prev is not None:
+        if prev is not None and (self.serialize or any(st.rows_seen for st in self.steps)):
             self.steps[k].stream.wait_event(self.done[prev])
         self.steps[k].enqueue(thr, chunk_begin, chunk_end, self.done[k])
         self.i += 1
