@@ -205,6 +205,10 @@ def main():
     # kernel queued on the device behind step i-1's while step i-1's count
     # exchange / host read / row gather complete (PipelinedShardStep)
     pipe = None
+    ctx1b = None  # N=1: the second context of the pipelined loop
+    if not dist_on and not args.no_pipeline:
+        ctx1b = W.Context(local_rank, kernel)
+        ctx1b.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
     if dist_on and not args.no_pipeline:
         ctx2 = W.Context(local_rank, kernel)
         ctx2.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
@@ -221,6 +225,21 @@ def main():
         return int(rows.shape[1]) if rows is not None else 0
 
     def run_steps(k):
+        if ctx1b is not None:
+            # N=1 pipelined: step i on context i % 2 (double-buffered rows), the
+            # host completes step i-1 (wld_run_wait) while step i's kernel runs
+            # (after a step with rows, one at a time: its row assembly then does
+            # not compete with the next kernel)
+            cs, r, prev = (ctx, ctx1b), 0, None
+            for i in range(k):
+                c = cs[i & 1]
+                if prev is not None and r > 0:
+                    r, prev = prev.run_wait(), None
+                c.run_chunks_async(thr, cb, ce)
+                if prev is not None:
+                    r = prev.run_wait()
+                prev = c
+            return prev.run_wait() if prev is not None else r
         if pipe is None:
             r = 0
             for _ in range(k):
@@ -305,8 +324,9 @@ def main():
             "unit (--unweighted)" if args.unweighted else "Henikoff"),
         "config": {"workload": desc, "n_seqs": N, "n_sites": L, "r2_threshold": thr, "pairs": total_pairs,
                    "rows_passing": rows, "kernel": kern_name, "mfma_planes": planes,
-                   "parallelism": "chunk-range shard x%d%s" % (
-                       world, (" + RCCL gather" + (", pipelined steps" if pipe is not None else "")) if dist_on else "")},
+                   "parallelism": "chunk-range shard x%d%s%s" % (
+                       world, (" + RCCL gather" if dist_on else ""),
+                       ", pipelined steps" if (pipe is not None or ctx1b is not None) else "")},
         "roofline": roof,
         "north_star_hbm_view": {"algorithmic_bytes_per_pair": 2 * N, "achieved_GBps": hbm_alg,
                                 "peak_GBps": HBM_PEAK_GBPS, "frac": hbm_alg / HBM_PEAK_GBPS},
