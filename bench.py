@@ -204,12 +204,17 @@ def main():
     # N>1 timed steps: two contexts on the same resident inputs, step i's
     # kernel queued on the device behind step i-1's while step i-1's count
     # exchange / host read / row gather complete (PipelinedShardStep)
+    # Pipelining doubles the contexts' operand footprint (two fragment copies of
+    # 2 LP NP bytes each): only when both fit the 256 MB Infinity Cache (C4:
+    # 2 x 81 MB); at C5 (2 x 500 MB) the alternating contexts measured 2% slower
+    LP, NP = -(-L // 256) * 256, -(-N // 64) * 64
+    pipelined = not args.no_pipeline and 2 * LP * NP <= 128 << 20
     pipe = None
     ctx1b = None  # N=1: the second context of the pipelined loop
-    if not dist_on and not args.no_pipeline:
+    if not dist_on and pipelined:
         ctx1b = W.Context(local_rank, kernel)
         ctx1b.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
-    if dist_on and not args.no_pipeline:
+    if dist_on and pipelined:
         ctx2 = W.Context(local_rank, kernel)
         ctx2.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
         pipe = wdist.PipelinedShardStep([ctx, ctx2], rank, world, device,
