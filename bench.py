@@ -75,6 +75,7 @@ def cpu_baseline(buf, w, thr, target_s=15.0, max_s=30.0):
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import _oracle as O  # checker / baseline only
 
+    O.use_native()  # gcc -O3 -march=native on the measuring host
     threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
     L = buf.shape[0]
     n = (L + 255) // 256
@@ -104,7 +105,7 @@ def cpu_baseline(buf, w, thr, target_s=15.0, max_s=30.0):
     p, t = run(k2)
     return {"value": p / t, "unit": "site-pairs/s", "cores": threads, "kind": "port",
             "sample": "%s = %d pairs in %.1f s; C restatement of the lib.rs simd path (8-lane f32, rayon-style "
-                      "chunk scheduling), gcc -O3 -march=x86-64-v3" % (what, p, t)}
+                      "chunk scheduling), gcc -O3 -march=native" % (what, p, t)}
 
 
 def load_traffic(config, kernel):
@@ -127,11 +128,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--unweighted", action="store_true", help="unit weights (main.rs:150-153 --unweighted)")
+    ap.add_argument("--wide-weights", action="store_true",
+                    help="Henikoff weights with every 10th scaled by 2^-8 (range ~2^-8: the 4-plane kernel)")
     ap.add_argument("--thr", type=float, help="override the config's r2 threshold (non-headline lines)")
     ap.add_argument("--rehearse-dist", action="store_true",
                     help="at N=1: run the N>1 step path (RCCL group of one, ShardStep/pipelined steps)")
     ap.add_argument("--no-pipeline", action="store_true",
-                    help="N>1: one ShardStep at a time (no overlap of a step's count exchange with the next kernel)")
+                    help="one step at a time (N=1: no second context; N>1: one ShardStep at a time)")
+    ap.add_argument("--no-screen", action="store_true",
+                    help="every tile with every weight-digit plane (WLD_OPT_SCREEN 0; same rows)")
+    ap.add_argument("--no-prefilter", action="store_true",
+                    help="every pair through the f32 epilogue (WLD_OPT_PREFILTER 0, implies --no-screen; same rows)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -167,6 +174,9 @@ def main():
     weights = W.henikoff_weights(kept)  # host pre-pass (lib.rs:340-380)
     if args.unweighted:
         weights = np.ones(N, dtype=np.float32)
+    if args.wide_weights:
+        weights = weights.copy()
+        weights[::10] *= np.float32(2.0 ** -8)
     prepass_ms = (time.perf_counter() - t0) * 1e3
     assert kept.n_sites() == L  # the synthetic distribution keeps every site
     torch.ones(1024, device=device).sum().item()  # CUDA context + allocator up before timing H2D
@@ -185,10 +195,19 @@ def main():
     for _ in range(3):
         assert pre.load_filtered_device(d_buf.data_ptr(), L, N, unweighted=args.unweighted) == L
         dev_ms.append(pre.stats()["load_ms"])
-    assert np.array_equal(pre.weights().view(np.uint32), weights.view(np.uint32))
+    if not args.wide_weights:
+        assert np.array_equal(pre.weights().view(np.uint32), weights.view(np.uint32))
     pre.close()
-    ctx = W.Context(local_rank, kernel)
-    ctx.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
+    def new_ctx():
+        c = W.Context(local_rank, kernel)
+        if args.no_screen or args.no_prefilter:
+            c.set_option("screen", 0)
+        if args.no_prefilter:
+            c.set_option("prefilter", 0)
+        c.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
+        return c
+
+    ctx = new_ctx()
     load_ms = ctx.stats()["load_ms"]
     # contiguous run of the reference chunk sequence, balanced by pairs (weightedld_amd/dist.py)
     cb, ce = ctx.shard_chunks(L, world, rank)
@@ -212,11 +231,9 @@ def main():
     pipe = None
     ctx1b = None  # N=1: the second context of the pipelined loop
     if not dist_on and pipelined:
-        ctx1b = W.Context(local_rank, kernel)
-        ctx1b.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
+        ctx1b = new_ctx()
     if dist_on and pipelined:
-        ctx2 = W.Context(local_rank, kernel)
-        ctx2.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
+        ctx2 = new_ctx()
         pipe = wdist.PipelinedShardStep([ctx, ctx2], rank, world, device,
                                         serialize_kernels=bool(os.environ.get("WLD_PIPE_SERIALIZE")))
 
@@ -266,23 +283,38 @@ def main():
     elapsed = time.perf_counter() - t0
     # per-launch HIP-event times of the same steps, sampled after the timed
     # region so that reading them adds nothing to it
-    kms, oms = [], []
+    kms, oms, sms, cand = [], [], [], []
     for _ in range(min(args.steps, 20)):
         tg = time.perf_counter()
         step()
         st = ctx.stats()
         kms.append(st["pair_kernel_ms"])
         oms.append(st["order_ms"])
+        sms.append(st["screen_ms"])
+        cand.append(st["candidate_tiles"])
         gms.append((time.perf_counter() - tg) * 1e3 - st["pair_kernel_ms"])
+    screened = bool(ctx.stats()["screened"])
+    n_tiles = ctx.stats()["tiles"]
+    # the same steps without the screen (every tile, every plane; same rows),
+    # reported alongside: a few sequential runs after the timed region
+    unscreened_ms = None
+    if screened:
+        ctx.set_option("screen", 0)
+        ums = []
+        for _ in range(5):
+            step()
+            ums.append(ctx.stats()["pair_kernel_ms"])
+        ctx.set_option("screen", 1)
+        unscreened_ms = float(np.mean(ums[1:]))
     if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        km = torch.tensor([float(np.mean(kms))], dtype=torch.float64, device=device)
+        km = torch.tensor([float(np.mean(kms)), float(np.mean(sms))], dtype=torch.float64, device=device)
         dist.all_reduce(km, op=dist.ReduceOp.MAX)
-        kernel_ms = float(km.item())
+        kernel_ms, screen_ms = float(km[0].item()), float(km[1].item())
     else:
-        kernel_ms = float(np.mean(kms))
+        kernel_ms, screen_ms = float(np.mean(kms)), float(np.mean(sms))
     st = ctx.stats()
     kern_name = "mfma" if st["kernel"] == W.KERNEL_MFMA else "valu"
     planes = st["mfma_planes"]
@@ -295,24 +327,47 @@ def main():
     total_pairs = L * (L - 1) // 2
     value = total_pairs * args.steps / elapsed
     shard_pairs = ctx.pairs_in_chunks(L, cb, ce)
-    # dominant kernel roofline (DESIGN.md "Roofline"): per-launch algorithmic work / HIP-event time
+    # Roofline of the dominant kernel: ALGORITHMIC work per
+    # launch, SURVEY 8(d)'s 4 masked multiply-adds per (pair, sequence) =
+    # 8 N ops per pair, over the launch's HIP-event time.  Screened runs: the
+    # dominant kernel is the one-plane screen, which evaluates every pair of
+    # the shard (its bound, from one digit plane of every sequence); the
+    # candidate launch recomputes the few tiles it cannot reject.
+    alg_ops = shard_pairs * 8.0 * N
     if kern_name == "mfma":
-        ops = shard_pairs * 8.0 * planes * N  # active weight planes x 4 masked products x N seqs x 2 ops/MAC
-        achieved = ops / (kernel_ms * 1e-3) / 1e12
-        roof = {"bound": "mfma", "achieved": achieved, "peak": I8_MFMA_PEAK_TOPS, "unit": "TFLOP/s",
-                "frac": achieved / I8_MFMA_PEAK_TOPS}
+        peak, unit = I8_MFMA_PEAK_TOPS, "TFLOP/s"  # int8 TOPS, dense (no sparsity)
+        dom_ms = screen_ms if screened else kernel_ms
+        achieved = alg_ops / (dom_ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak,
+                "work": "algorithmic: 8*N int8 ops per site pair (4 masked weighted sums)",
+                "kernel": "pair_mfma_kernel<screen,1 plane>" if screened else "pair_mfma_kernel<%d planes>" % planes,
+                "kernel_ms": dom_ms}
+        # what the matrix cores executed: P digit planes x 8 N per pair
+        ex_planes = 1 if screened else planes
+        roof["executed_frac"] = shard_pairs * 8.0 * ex_planes * N / (dom_ms * 1e-3) / 1e12 / peak
+        roof["executed_work"] = "%d digit plane(s) x 8*N int8 ops per pair" % ex_planes
     else:
-        ops = shard_pairs * 8.0 * N  # 4 masked f32 sums x N seqs x 2 flops/FMA
-        achieved = ops / (kernel_ms * 1e-3) / 1e12
+        achieved = alg_ops / (kernel_ms * 1e-3) / 1e12
         # finite weights: f32-input MFMA (v_mfma_f32_16x16x4_f32), whose peak is the
         # f32 vector peak (MI355X_MICROARCH.md, Matrix cores: F32 row)
         roof = {"bound": "mfma", "achieved": achieved, "peak": F32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": achieved / F32_VALU_PEAK_TFLOPS, "path": "f32 MFMA 16x16x4"}
-    roof["kernel"] = "pair_%s_kernel" % kern_name
-    roof["kernel_ms"] = kernel_ms
+                "frac": achieved / F32_VALU_PEAK_TFLOPS, "path": "f32 MFMA 16x16x4",
+                "work": "algorithmic: 8*N f32 flops per site pair", "kernel": "pair_valu_kernel",
+                "kernel_ms": kernel_ms}
+    roof["pair_phase_ms"] = kernel_ms
+    roof["pair_phase_frac"] = alg_ops / (kernel_ms * 1e-3) / 1e12 / roof["peak"]
+    if screened:
+        roof["screen"] = {"tiles": n_tiles, "candidate_tiles": float(np.mean(cand)),
+                          "candidate_launch_ms": kernel_ms - screen_ms, "unscreened_pair_kernel_ms": unscreened_ms,
+                          "unscreened_frac": alg_ops / (unscreened_ms * 1e-3) / 1e12 / roof["peak"]}
     tr = load_traffic(args.config + ("-unweighted" if args.unweighted else ""), kern_name)
     roof["traffic"] = tr.get("hbm_bytes_per_launch") if tr else None
     hbm_alg = shard_pairs * 2.0 * N / (kernel_ms * 1e-3) / 1e9  # 2N bytes per pair
+    if kern_name == "mfma":
+        dtype = ("i8 digit planes of 24-bit fixed-point weights (%d plane%s), exact i32 sums, f32 epilogue"
+                 % (planes, "s" if planes > 1 else ""))
+    else:
+        dtype = "f32"
     out = {
         "metric": METRIC,
         "value": value,
@@ -324,22 +379,26 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "i8" if kern_name == "mfma" else "f32",
+        "dtype": dtype,
         "data": "synthetic (seeded bench_weighted_pair_ld.rs distribution, %s weights)" % (
-            "unit (--unweighted)" if args.unweighted else "Henikoff"),
+            "unit (--unweighted)" if args.unweighted else
+            "Henikoff, every 10th x 2^-8 (--wide-weights)" if args.wide_weights else "Henikoff"),
         "config": {"workload": desc, "n_seqs": N, "n_sites": L, "r2_threshold": thr, "pairs": total_pairs,
                    "rows_passing": rows, "kernel": kern_name, "mfma_planes": planes,
                    "parallelism": "chunk-range shard x%d%s%s" % (
                        world, (" + RCCL gather" if dist_on else ""),
                        ", pipelined steps" if (pipe is not None or ctx1b is not None) else "")},
         "roofline": roof,
-        "north_star_hbm_view": {"algorithmic_bytes_per_pair": 2 * N, "achieved_GBps": hbm_alg,
-                                "peak_GBps": HBM_PEAK_GBPS, "frac": hbm_alg / HBM_PEAK_GBPS},
+        # SURVEY 8(d)'s no-reuse byte MODEL (2N bytes per pair as if every pair
+        # re-read both site columns from HBM) — not a roofline: the kernel
+        # stages columns through LDS/L2 and reads each far fewer times
+        "north_star_hbm_model": {"model_bytes_per_pair": 2 * N, "model_GBps": hbm_alg,
+                                 "hbm_peak_GBps": HBM_PEAK_GBPS, "model_over_peak": hbm_alg / HBM_PEAK_GBPS},
         "order_ms": float(np.mean(oms)),
         # SURVEY 8(d) timing window: phases outside `value`'s step are reported, not timed in it
         "phases_ms": {"host_prepass_filter_henikoff": prepass_ms,
                       "device_prepass_filter_henikoff_encode": float(min(dev_ms)), "h2d_inputs": h2d_ms,
-                      "device_encode_prep": load_ms, "pair_kernel": kernel_ms, "order_assembly": float(np.mean(oms)),
+                      "device_encode_prep": load_ms, "pair_phase": kernel_ms, "order_assembly": float(np.mean(oms)),
                       "step_minus_kernel_rank0": float(np.median(gms))},
     }
     if world == 1 and not args.no_cpu_baseline:

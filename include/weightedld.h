@@ -130,6 +130,40 @@ void wld_destroy(wld_ctx *ctx);
 #define WLD_KERNEL_MFMA 2
 int wld_set_kernel(wld_ctx *ctx, int kernel);
 
+/* Per-context options (the library reads no environment variables).  None
+ * changes a result: every setting gives bit-identical rows; they exist for
+ * A/B measurements and tests.  Set between runs; WLD_E_ARG for an unknown
+ * option or a bad value.
+ *   WLD_OPT_PREFILTER  1 (default): with r2_threshold > 0 the MFMA kernel
+ *                      skips the f32 epilogue of pairs that a rigorous bound
+ *                      proves cannot pass; 0: every pair.
+ *   WLD_OPT_SCREEN     1 (default): with the prefilter on and >= 2 nonzero
+ *                      weight-digit planes, a one-plane screen launch bounds
+ *                      every pair's r2 and only candidate 64x64 tiles are
+ *                      recomputed with every plane; 0: every tile, every plane.
+ *   WLD_OPT_TILE_ORDER 0 (default): L2/XCD-aware tile launch order; 1: plain
+ *                      (a-tile, b-tile) order.
+ *   WLD_OPT_ALL_PLANES 0 (default): all-zero digit planes are skipped; 1: the
+ *                      MFMA kernel multiplies all three.
+ *   WLD_OPT_MFMA_LAYOUT 0 (default): LDS-streaming fragment-major kernel; 1:
+ *                      the site-major register kernel (takes effect at the
+ *                      next load).
+ *   WLD_OPT_VALU_PLAIN 0 (default): the f32 fallback multiplies on f32-input
+ *                      MFMA; 1: a VALU fmaf loop (same sums, same order).
+ *   WLD_OPT_STAGING_ROWS   initial staging capacity in rows (default 2^25;
+ *                      grown on overflow by a re-run).
+ *   WLD_OPT_HOST_BATCH_PAIRS  pairs per batch of wld_run_host (default 2^31). */
+#define WLD_OPT_PREFILTER 1
+#define WLD_OPT_SCREEN 2
+#define WLD_OPT_TILE_ORDER 3
+#define WLD_OPT_ALL_PLANES 4
+#define WLD_OPT_MFMA_LAYOUT 5
+#define WLD_OPT_VALU_PLAIN 6
+#define WLD_OPT_STAGING_ROWS 7
+#define WLD_OPT_HOST_BATCH_PAIRS 8
+int wld_set_option(wld_ctx *ctx, int option, int64_t value);
+int wld_get_option(wld_ctx *ctx, int option, int64_t *value);
+
 /* Rows of PairStore<LdStats> (lib.rs:523-576) as structure-of-arrays, in the
  * reference's order: 256x256 chunks in triu_index order (lib.rs:623-635:
  * chunk rows descending, columns ascending), then site_a, then site_b
@@ -265,12 +299,17 @@ typedef struct {
     int kernel;              /* WLD_KERNEL_VALU or WLD_KERNEL_MFMA actually used   */
     uint64_t pairs;          /* pairs evaluated (a<b) in the last run              */
     uint64_t rows;           /* rows that passed the threshold                     */
-    double pair_kernel_ms;   /* HIP-event time of the pair kernel (last run)       */
+    double pair_kernel_ms;   /* HIP-event time of the pair phase (last run): the pair
+                                kernel, or screen + candidate launch           */
     double order_ms;         /* HIP-event time of the ordering kernels (last run)  */
     double load_ms;          /* HIP-event time of the encode kernel (last load)    */
-    uint64_t pair_kernel_launches;
+    uint64_t pair_kernel_launches; /* 2 when screened: screen + candidate tiles */
     int weight_shift;        /* fixed-point exponent of the MFMA weight planes     */
     int mfma_planes;         /* weight-digit planes the MFMA kernel multiplies (1-3; all-zero planes skipped) */
+    uint64_t tiles;          /* 64x64 site tiles of the last run                   */
+    uint64_t candidate_tiles;/* tiles computed with every plane (= tiles unless screened) */
+    double screen_ms;        /* HIP-event time of the screen launch (0 if none)    */
+    int screened;            /* 1 if the last run ran the one-plane screen          */
 } wld_run_stats;
 int wld_last_stats(wld_ctx *ctx, wld_run_stats *out);
 

@@ -28,6 +28,18 @@ class _Rows(ctypes.Structure):
 _lib = None
 
 
+def use_native():
+    """Builds the oracle for THIS host (-march=native, into oracle/build_native)
+    and makes lib() load that build: bench.py's CPU baseline, on the measuring
+    host (the test build is -march=x86-64-v3 so it runs on any x86-64 host)."""
+    global ORACLE_SO, _lib
+    out = os.path.join(ORACLE_DIR, "build_native")
+    subprocess.run(["make", "-s", "-B", "-C", ORACLE_DIR, "MARCH=native", "OUT=" + out], check=True)
+    ORACLE_SO = os.path.join(out, "libwld_oracle.so")
+    _lib = None
+    return ORACLE_SO
+
+
 def lib():
     global _lib
     if _lib is not None:
@@ -189,6 +201,24 @@ def all_pairs_dense_f64(buf, weights):
                                _p(d, ctypes.c_double), _p(dp, ctypes.c_double), _p(r2, ctypes.c_double),
                                _p(valid, ctypes.c_uint8))
     return d, dp, r2, valid
+
+
+def pair_sums_f64(buf, weights):
+    """The four masked sums of lib.rs:416-480 for every pair (L x L f64 each:
+    T, SA, SB, SAB), with the f32 weights summed in f64 (numpy restatement,
+    for conditioning diagnostics)."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    L = buf.shape[0]
+    w = np.asarray(weights, dtype=np.float32).astype(np.float64)
+    inm = np.zeros(buf.shape, dtype=np.float64)
+    mj = np.zeros(buf.shape, dtype=np.float64)
+    for s in range(L):
+        a, b = major_minor(histogram(buf[s]))
+        if a is None or b is None:
+            continue
+        inm[s] = (buf[s] == a) | (buf[s] == b)
+        mj[s] = buf[s] == a
+    return (inm * w) @ inm.T, (mj * w) @ inm.T, (inm * w) @ mj.T, (mj * w) @ mj.T
 
 
 def triu_index(n, i):

@@ -16,6 +16,35 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: larger CPU cases")
 
 
+class ParityReport:
+    """Per-field tallies of the GPU-vs-oracle comparisons (test_gpu_parity.agree):
+    values compared, max |GPU - reference| among strictly agreeing values, and
+    the count and max |GPU - reference| of D' values accepted only because they
+    are at least as close to the exact f64 value as the f32 reference."""
+
+    def __init__(self):
+        self.f = {}
+
+    def record(self, field, n, max_strict, n_esc, max_esc):
+        t = self.f.setdefault(field, [0, 0.0, 0, 0.0])
+        t[0] += n
+        t[1] = max(t[1], max_strict)
+        t[2] += n_esc
+        t[3] = max(t[3], max_esc)
+
+
+PARITY = ParityReport()
+
+
+def pytest_terminal_summary(terminalreporter):
+    if not PARITY.f:
+        return
+    terminalreporter.write_line("parity report (GPU vs oracle, tolerance 1e-5):")
+    for field, (n, ms, ne, me) in sorted(PARITY.f.items()):
+        terminalreporter.write_line("  %-8s %12d values  max|diff| strict %.3g  escaped via f64 truth: %d (max|diff| %.3g)"
+                                    % (field, n, ms, ne, me))
+
+
 GOLDEN = os.path.join(TESTS, "golden")
 FIXTURES = os.path.join(GOLDEN, "fixtures")
 SYNTH = os.path.join(GOLDEN, "synthetic")

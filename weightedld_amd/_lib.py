@@ -8,8 +8,7 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-# WLD_LIB points the tests at an experimental in-tree build (tools/build_variant.sh)
-LIB_PATH = os.environ.get("WLD_LIB") or os.path.join(PKG_DIR, "libweightedld.so")
+LIB_PATH = os.path.join(PKG_DIR, "libweightedld.so")
 
 WLD_OK = 0
 STATUS = {
@@ -22,6 +21,9 @@ STATUS = {
     -7: "WLD_E_STATE",
 }
 KERNEL_AUTO, KERNEL_VALU, KERNEL_MFMA = 0, 1, 2
+# wld_set_option ids (include/weightedld.h)
+OPTIONS = {"prefilter": 1, "screen": 2, "tile_order": 3, "all_planes": 4, "mfma_layout": 5, "valu_plain": 6,
+           "staging_rows": 7, "host_batch_pairs": 8}
 
 
 class WldError(RuntimeError):
@@ -53,6 +55,10 @@ class RunStats(ctypes.Structure):
         ("pair_kernel_launches", ctypes.c_uint64),
         ("weight_shift", ctypes.c_int),
         ("mfma_planes", ctypes.c_int),
+        ("tiles", ctypes.c_uint64),
+        ("candidate_tiles", ctypes.c_uint64),
+        ("screen_ms", ctypes.c_double),
+        ("screened", ctypes.c_int),
     ]
 
 
@@ -89,6 +95,8 @@ SIGNATURES = {
     "wld_create": (_int, [_int, ctypes.POINTER(_vp)]),
     "wld_destroy": (None, [_vp]),
     "wld_set_kernel": (_int, [_vp, _int]),
+    "wld_set_option": (_int, [_vp, _int, ctypes.c_int64]),
+    "wld_get_option": (_int, [_vp, _int, ctypes.POINTER(ctypes.c_int64)]),
     "wld_pairs_free": (None, [ctypes.POINTER(Pairs)]),
     "wld_all_weighted_ld_pairs": (_int, [_vp, _u8p, _sz, _sz, _u64p, _f32p, ctypes.c_float, PROGRESS_FN, _vp,
                                          ctypes.POINTER(Pairs)]),
@@ -141,8 +149,6 @@ def lib():
     _preload_torch()
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
-        if os.environ.get("WLD_LIB") and not hasattr(L, name):
-            continue  # an older experimental build (A/B against a previous commit)
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

@@ -11,12 +11,13 @@ from collections import namedtuple
 
 import numpy as np
 
-from ._lib import (KERNEL_AUTO, KERNEL_MFMA, KERNEL_VALU, PROGRESS_FN, Pairs, RunStats, WldError, check, lib)
+from ._lib import (KERNEL_AUTO, KERNEL_MFMA, KERNEL_VALU, OPTIONS, PROGRESS_FN, Pairs, RunStats, WldError, check,
+                   lib)
 
 __all__ = [
     "Symbol", "SymbolHistogram", "SiteSet", "LdStats", "PairStore", "read_fasta", "read_vcf",
     "is_site_of_interest", "henikoff_weights", "single_weighted_ld_pair", "all_weighted_ld_pairs",
-    "Context", "default_context", "KERNEL_AUTO", "KERNEL_VALU", "KERNEL_MFMA", "WldError",
+    "Context", "default_context", "KERNEL_AUTO", "KERNEL_VALU", "KERNEL_MFMA", "OPTIONS", "WldError",
 ]
 
 
@@ -218,6 +219,17 @@ class Context:
 
     def set_kernel(self, kernel):
         check(lib().wld_set_kernel(self._h, kernel), "wld_set_kernel")
+
+    def set_option(self, name, value):
+        """wld_set_option: name is a key of OPTIONS ("prefilter", "screen",
+        "tile_order", "all_planes", "mfma_layout", "valu_plain", "staging_rows",
+        "host_batch_pairs"); no option changes a result."""
+        check(lib().wld_set_option(self._h, OPTIONS[name], int(value)), "wld_set_option")
+
+    def get_option(self, name):
+        v = ctypes.c_int64()
+        check(lib().wld_get_option(self._h, OPTIONS[name], ctypes.byref(v)), "wld_get_option")
+        return int(v.value)
 
     def load(self, site_major, weights, site_map=None):
         buf = np.ascontiguousarray(site_major, dtype=np.uint8)

@@ -88,12 +88,16 @@ struct RunPending {
 struct wld_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[6] = {};
+    hipEvent_t ev[7] = {};  // 2..3 pair phase (6: after the screen), 3..4/5 order phase
     RunPending pend;                      // the run between run_enqueue and run_complete
     bool run_dirty = true;                // run state (cursor, chunk totals) may be nonzero: re-initialise
     unsigned long long *h_cnt = nullptr;  // mapped pinned {cursor, rows} written by chunk_scan_kernel
     unsigned long long *d_hcnt = nullptr;
     int kernel_pref = WLD_KERNEL_AUTO;
+    // wld_set_option (include/weightedld.h)
+    bool opt_prefilter = true, opt_screen = true, opt_tile_rows = false, opt_all_planes = false;
+    bool opt_site_major = false, opt_valu_plain = false;
+    uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
 
     // loaded SiteSet
     bool loaded = false;
@@ -107,22 +111,25 @@ struct wld_ctx {
     int kernel = WLD_KERNEL_VALU;
     bool safe = false;
     int shift = 0;
-    unsigned plane_mask = 7;  // weight-digit planes with a nonzero digit (MFMA)
+    int fixed_planes = 3;      // digit planes of the fixed-point weights (3: 23 bits, 4: 31 bits)
+    unsigned plane_mask = 7;   // weight-digit planes with a nonzero digit (MFMA)
+    MfmaWeightStats wst{7, 1, {0, 0, 0}};  // digit-plane statistics of the load (MFMA)
 
     // run state
-    DevBuf tiles, seg_cnt, seg_off, chunk_total, chunk_base, counters;
+    DevBuf tiles, cand, seg_cnt, seg_off, chunk_total, chunk_base, counters;
     DevBuf st_a, st_b, st_d, st_dp, st_r2;
     DevBuf out_a, out_b, out_d, out_dp, out_r2;
     uint64_t st_capacity = 0;
     uint32_t tiles_lb = ~0u, tiles_le = ~0u;  // linear chunk range the tile list covers
     uint32_t n_tiles = 0;
     bool have_rows = false;
+    bool screened = false;  // the last pass ran the one-plane screen
     uint64_t rows = 0;
     wld_run_stats stats{};
 
     ~wld_ctx() {
         (void)hipSetDevice(device);
-        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &tiles,
+        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &tiles, &cand,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
@@ -151,12 +158,12 @@ float event_ms(hipEvent_t a, hipEvent_t b) {
 }
 
 // fixed-point exponent for the MFMA weight planes: max|w| * 2^shift must fit
-// three balanced base-256 digits (|q| <= 127 * 65793 = 8,355,711 + 256).
-int weight_shift(float maxabs) {
-    const double lim = 127.0 * (1.0 + 256.0 + 65536.0);
+// `planes` balanced base-256 digits (|q| <= 127 * (1 + 2^8 + 2^16 [+ 2^24])).
+int weight_shift(float maxabs, int planes) {
+    const double lim = 127.0 * (1.0 + 256.0 + 65536.0 + (planes == 4 ? 16777216.0 : 0.0));
     int e = 0;
     std::frexp((double)maxabs, &e);  // maxabs = m * 2^e, m in [0.5, 1)
-    int shift = 22 - e;              // maxabs * 2^shift < 2^22 < lim
+    int shift = (planes == 4 ? 30 : 22) - e;  // maxabs * 2^shift < 2^22 (2^30) < lim
     while (std::ldexp((double)maxabs, shift + 1) <= lim) ++shift;
     while (std::ldexp((double)maxabs, shift) > lim) --shift;
     return shift;
@@ -183,14 +190,20 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
 
     const bool finite = ws[2] == 0.0f;
     const float maxabs = ws[0], minabs = ws[1];
-    // MFMA planes hold w * 2^shift in 24-bit fixed point; AUTO keeps the f32
-    // VALU kernel when that could lose precision ("Kernel choice").
+    // MFMA planes hold w * 2^shift in fixed point: 3 digit planes (q < 2^23) or
+    // 4 (q < 2^31).  Each weight is then within 0.5 / q_min relative of its f32
+    // value; AUTO requires that to be <= 2^-19 (sums of nonnegative weights,
+    // any cell of the 2x2 table included, keep that relative error, so d and
+    // r2 move by ~1e-6 at most: DESIGN.md §5), i.e. min|w| >= 2^-4 max|w| for
+    // 3 planes and >= 2^-12 max|w| for 4; wider ranges take the f32 kernel.
     // The int32 accumulators hold X = S(minor) + 2 S(major) and Y = S(minor)
-    // with |X| + |Y| <= 3 * 128 * NP (pair_mfma.hip, Acc16::get): NP < 2^31 / 384.
-    constexpr size_t kMfmaMaxNP = 5592320;
+    // with |X| + |Y| <= 3 * 128 * NP (pair_mfma.hip, Acc16::get): NP < 2^31 / 384;
+    // 4 planes fold two planes into int32 (NP <= 65024).
+    constexpr size_t kMfmaMaxNP = 5592320, kMfma4MaxNP = 65024;
     const bool mfma_fits = c->NP <= kMfmaMaxNP;
-    const bool mfma_ok =
-        mfma_supported() && mfma_fits && finite && maxabs > 0.0f && minabs >= maxabs * 0x1p-10f;
+    const bool range3 = minabs >= maxabs * 0x1p-4f, range4 = minabs >= maxabs * 0x1p-12f;
+    const bool mfma_ok = mfma_supported() && mfma_fits && finite && maxabs > 0.0f &&
+                         (range3 || (range4 && c->NP <= kMfma4MaxNP));
     int k = c->kernel_pref;
     if (k == WLD_KERNEL_AUTO) k = mfma_ok ? WLD_KERNEL_MFMA : WLD_KERNEL_VALU;
     if (k == WLD_KERNEL_MFMA && !(mfma_supported() && finite && maxabs > 0.0f))
@@ -203,15 +216,21 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     c->shift = 0;
     c->use_frag = false;
     if (k == WLD_KERNEL_MFMA) {
-        c->shift = weight_shift(maxabs);
+        // 3 planes when they hold every weight to 2^-19; else 4 (an explicit
+        // MFMA request beyond 2^-12 keeps 4 planes and loses precision on the
+        // smallest weights)
+        c->fixed_planes = range3 || c->NP > kMfma4MaxNP ? 3 : 4;
+        if (c->fixed_planes == 4 && c->opt_site_major)
+            return fail(WLD_E_ARG, "the site-major MFMA kernel (WLD_OPT_MFMA_LAYOUT) multiplies 3 digit planes; "
+                                   "these weights need 4");
+        c->shift = weight_shift(maxabs, c->fixed_planes);
         WLD_TRY(ensure(c->planes, mfma_planes_bytes(c->LP, c->NP)));
         launch_mfma_prep(ptr<uint8_t>(c->site_ok), ptr<float>(c->w_pad), L, c->LP, c->NP, c->shift,
                          ptr<int8_t>(c->planes), c->stream);
         HIP_TRY(hipGetLastError());
         // fragment-major copy of the codes (1 KB contiguous per wave operand load);
-        // WLD_MFMA_LAYOUT=rows keeps the site-major reads (A/B experiments)
-        const char *lay = getenv("WLD_MFMA_LAYOUT");
-        c->use_frag = !(lay && std::string(lay) == "rows");
+        // WLD_OPT_MFMA_LAYOUT = 1 keeps the site-major reads (tests)
+        c->use_frag = !c->opt_site_major;
         if (c->use_frag) {
             // two copies: the selector-coded one (A operands, and B in the
             // v_perm build) and the 0/1/2-coded one the B side reads raw
@@ -233,9 +252,11 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
         if (L) HIP_TRY(hipMemcpyAsync(c->site_map.p, m.data(), L * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
-    c->plane_mask = c->kernel == WLD_KERNEL_MFMA && !getenv("WLD_ALL_PLANES")
-                        ? mfma_plane_mask(ptr<int8_t>(c->planes), c->LP, c->NP, c->stream)
-                        : 7u;
+    c->wst = MfmaWeightStats{7, 1, {0, 0, 0}};
+    if (c->kernel == WLD_KERNEL_MFMA && mfma_weight_stats(ptr<int8_t>(c->planes), c->LP, c->NP, c->stream, &c->wst))
+        return fail(WLD_E_HIP, "reading the weight-plane statistics failed");
+    const unsigned all_planes = (1u << c->fixed_planes) - 1;
+    c->plane_mask = c->kernel == WLD_KERNEL_MFMA && !c->opt_all_planes ? c->wst.plane_mask : all_planes;
     c->stats.load_ms = event_ms(c->ev[0], c->ev[1]);
     c->stats.mfma_planes = c->kernel == WLD_KERNEL_MFMA ? __builtin_popcount(c->plane_mask) : 0;
     c->stats.kernel = c->kernel;
@@ -350,12 +371,12 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
                 t.push_back((ta << 16) | tb);
     }
     std::sort(t.begin(), t.end());
-    const char *ord = getenv("WLD_TILE_ORDER");
     // only with many rounds of resident tiles: whole super-blocks per XCD
     // leave up to one super-block of imbalance (C2's 528 tiles: +14%)
-    if (!(ord && std::string(ord) == "rows") && t.size() >= 4096 && T_used < 65535) t = xcd_order(t);
+    if (!c->opt_tile_rows && t.size() >= 4096 && T_used < 65535) t = xcd_order(t);
     c->n_tiles = (uint32_t)t.size();
     WLD_TRY(ensure(c->tiles, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));
+    WLD_TRY(ensure(c->cand, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));  // screen candidates
     if (!t.empty())
         HIP_TRY(hipMemcpyAsync(c->tiles.p, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -380,21 +401,39 @@ OrderArgs order_args(wld_ctx *c) {
     return o;
 }
 
-int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *dense) {
+// Enqueues the pair kernel(s) of a pass; *screened tells whether the MFMA
+// screen ran (then ev[6] separates it from the candidate launch).
+int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *dense, bool *screened = nullptr) {
     const uint32_t n = chunk_rows_of(c->L);
+    bool sc = false;
     if (c->kernel == WLD_KERNEL_MFMA) {
-        // the exact-integer r2 prefilter needs a positive threshold to reject
-        // anything; WLD_NO_PREFILTER=1 disables it (A/B experiments)
-        const bool prefilter = thr > 0.0f && !getenv("WLD_NO_PREFILTER");
-        launch_pair_mfma(ptr<uint8_t>(c->codes), c->use_frag ? ptr<uint8_t>(c->frag) : nullptr,
-                         c->use_frag ? ptr<uint8_t>(c->frag) + c->LP * c->NP : nullptr,
-                         ptr<int8_t>(c->planes), ptr<uint32_t>(c->tiles), c->n_tiles, (uint32_t)c->L,
-                         (uint32_t)c->NP, n, thr, c->shift, c->plane_mask, prefilter, o, dense, c->stream);
+        MfmaLaunch m{};
+        m.codes = ptr<uint8_t>(c->codes);
+        m.frag = c->use_frag ? ptr<uint8_t>(c->frag) : nullptr;
+        m.frag_b = c->use_frag ? ptr<uint8_t>(c->frag) + c->LP * c->NP : nullptr;
+        m.wplanes = ptr<int8_t>(c->planes);
+        m.tiles = ptr<uint32_t>(c->tiles);
+        m.n_tiles = c->n_tiles;
+        m.L = (uint32_t)c->L;
+        m.NP = (uint32_t)c->NP;
+        m.n_chunk_rows = n;
+        m.thr = thr;
+        m.shift = c->shift;
+        m.plane_mask = c->plane_mask;
+        m.nonneg = c->wst.nonneg;
+        // both need a positive threshold to reject anything
+        m.prefilter = c->opt_prefilter && thr > 0.0f;
+        m.screen = m.prefilter && c->opt_screen;
+        for (int t = 0; t < 3; ++t) m.resid[t] = c->wst.resid[t];
+        m.cand_list = ptr<uint32_t>(c->cand);
+        m.cand_count = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 2);
+        sc = launch_pair_mfma(m, o, dense, c->stream, c->ev[6]);
     } else
         launch_pair_valu(ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), ptr<uint8_t>(c->site_ok),
-                         ptr<uint32_t>(c->tiles), c->n_tiles, (uint32_t)c->L, (uint32_t)c->NP, n, thr, c->safe, o,
-                         dense, c->stream);
+                         ptr<uint32_t>(c->tiles), c->n_tiles, (uint32_t)c->L, (uint32_t)c->NP, n, thr, c->safe,
+                         c->opt_valu_plain, o, dense, c->stream);
     HIP_TRY(hipGetLastError());
+    if (screened) *screened = sc;
     return WLD_OK;
 }
 
@@ -450,6 +489,53 @@ int wld_set_kernel(wld_ctx *ctx, int kernel) {
     if (kernel < WLD_KERNEL_AUTO || kernel > WLD_KERNEL_MFMA) return fail(WLD_E_ARG, "bad kernel id %d", kernel);
     if (kernel == WLD_KERNEL_MFMA && !mfma_supported()) return fail(WLD_E_ARG, "MFMA kernel not built");
     ctx->kernel_pref = kernel;
+    return WLD_OK;
+}
+
+int wld_set_option(wld_ctx *c, int option, int64_t value) {
+    if (!c) return fail(WLD_E_ARG, "null context");
+    if (c->pend.active) return fail(WLD_E_STATE, "wld_set_option during a run");
+    switch (option) {
+        case WLD_OPT_PREFILTER: c->opt_prefilter = value != 0; break;
+        case WLD_OPT_SCREEN: c->opt_screen = value != 0; break;
+        case WLD_OPT_TILE_ORDER:
+            c->opt_tile_rows = value != 0;
+            c->tiles_lb = c->tiles_le = ~0u;  // rebuild the list at the next run
+            break;
+        case WLD_OPT_ALL_PLANES:
+            c->opt_all_planes = value != 0;
+            if (c->loaded && c->kernel == WLD_KERNEL_MFMA)
+                c->plane_mask = c->opt_all_planes ? (1u << c->fixed_planes) - 1 : c->wst.plane_mask;
+            if (c->loaded) c->stats.mfma_planes = c->kernel == WLD_KERNEL_MFMA ? __builtin_popcount(c->plane_mask) : 0;
+            break;
+        case WLD_OPT_MFMA_LAYOUT: c->opt_site_major = value != 0; break;
+        case WLD_OPT_VALU_PLAIN: c->opt_valu_plain = value != 0; break;
+        case WLD_OPT_STAGING_ROWS:
+            if (value < 1) return fail(WLD_E_ARG, "WLD_OPT_STAGING_ROWS must be >= 1");
+            c->opt_staging_rows = (uint64_t)value;
+            break;
+        case WLD_OPT_HOST_BATCH_PAIRS:
+            if (value < 1) return fail(WLD_E_ARG, "WLD_OPT_HOST_BATCH_PAIRS must be >= 1");
+            c->opt_host_batch_pairs = (uint64_t)value;
+            break;
+        default: return fail(WLD_E_ARG, "unknown option %d", option);
+    }
+    return WLD_OK;
+}
+
+int wld_get_option(wld_ctx *c, int option, int64_t *value) {
+    if (!c || !value) return fail(WLD_E_ARG, "null argument");
+    switch (option) {
+        case WLD_OPT_PREFILTER: *value = c->opt_prefilter; break;
+        case WLD_OPT_SCREEN: *value = c->opt_screen; break;
+        case WLD_OPT_TILE_ORDER: *value = c->opt_tile_rows; break;
+        case WLD_OPT_ALL_PLANES: *value = c->opt_all_planes; break;
+        case WLD_OPT_MFMA_LAYOUT: *value = c->opt_site_major; break;
+        case WLD_OPT_VALU_PLAIN: *value = c->opt_valu_plain; break;
+        case WLD_OPT_STAGING_ROWS: *value = (int64_t)c->opt_staging_rows; break;
+        case WLD_OPT_HOST_BATCH_PAIRS: *value = (int64_t)c->opt_host_batch_pairs; break;
+        default: return fail(WLD_E_ARG, "unknown option %d", option);
+    }
     return WLD_OK;
 }
 
@@ -666,13 +752,16 @@ int enqueue_pass(wld_ctx *c) {
     c->run_dirty = true;  // until run_complete has seen this pass's scan
     const OrderArgs o = order_args(c);
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-    if (c->n_tiles) WLD_TRY(launch_pairs(c, r.thr, o, nullptr));
+    c->screened = false;
+    if (c->n_tiles) WLD_TRY(launch_pairs(c, r.thr, o, nullptr, &c->screened));
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     c->h_cnt[0] = c->h_cnt[1] = lin_count ? ~0ull : 0ull;
+    c->h_cnt[2] = 0;
     if (lin_count) {
         launch_chunk_scan(ptr<uint32_t>(c->chunk_total), r.lin_begin, lin_count, ptr<uint32_t>(c->chunk_base),
                           ptr<unsigned long long>(c->counters) + 1, ptr<unsigned long long>(c->counters), c->d_hcnt,
-                          r.count_out, c->stream);
+                          r.count_out, reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 2),
+                          c->stream);
         HIP_TRY(hipGetLastError());
     } else if (r.count_out) {
         HIP_TRY(hipMemsetAsync(r.count_out, 0, sizeof(unsigned long long), c->stream));
@@ -697,9 +786,7 @@ int run_enqueue(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uns
     if (pairs > 0xFFFFFFFFull)
         return fail(WLD_E_ARG, "shard has %llu pairs; > 2^32 per device not supported (shard over more devices)",
                     (unsigned long long)pairs);
-    uint64_t init_rows = 1ull << 25;
-    if (const char *e = getenv("WLD_INITIAL_STAGING_ROWS")) init_rows = strtoull(e, nullptr, 10);  // tests
-    WLD_TRY(grow_staging(c, std::min<uint64_t>(pairs, init_rows)));
+    WLD_TRY(grow_staging(c, std::min<uint64_t>(pairs, c->opt_staging_rows)));
     WLD_TRY(ensure(c->seg_cnt, c->LP * T));
     WLD_TRY(ensure(c->seg_off, c->LP * T * sizeof(uint32_t)));
     const size_t ct_bytes = c->chunk_total.bytes, cn_bytes = c->counters.bytes;
@@ -719,12 +806,13 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     const RunPending r = c->pend;
     const uint32_t n = chunk_rows_of(c->L);
     const uint32_t lin_count = r.lin_end - r.lin_begin;
-    unsigned long long h[2] = {0, 0};
+    unsigned long long h[3] = {0, 0, 0};
     for (int attempt = 0; attempt < 2; ++attempt) {
         HIP_TRY(hipStreamSynchronize(c->stream));
         c->run_dirty = false;  // the pass completed: its scan cleaned the run state
         h[0] = __atomic_load_n(&c->h_cnt[0], __ATOMIC_ACQUIRE);
         h[1] = __atomic_load_n(&c->h_cnt[1], __ATOMIC_ACQUIRE);
+        h[2] = __atomic_load_n(&c->h_cnt[2], __ATOMIC_ACQUIRE);
         if (h[0] <= c->st_capacity) break;
         if (attempt == 1) return fail(WLD_E_HIP, "internal: staging overflow after resize");
         WLD_TRY(grow_staging(c, h[0]));
@@ -755,7 +843,11 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     c->stats.rows = rows;
     c->stats.pair_kernel_ms = event_ms(c->ev[2], c->ev[3]);
     c->stats.order_ms = event_ms(c->ev[3], c->ev[order_end]);
-    c->stats.pair_kernel_launches = c->n_tiles ? 1 : 0;
+    c->stats.pair_kernel_launches = c->n_tiles ? (c->screened ? 2 : 1) : 0;
+    c->stats.tiles = c->n_tiles;
+    c->stats.screened = c->screened ? 1 : 0;
+    c->stats.screen_ms = c->screened ? event_ms(c->ev[2], c->ev[6]) : 0.0;
+    c->stats.candidate_tiles = c->screened ? h[2] : c->n_tiles;
     if (n_rows) *n_rows = rows;
     return WLD_OK;
 }
@@ -899,8 +991,7 @@ int wld_run_host(wld_ctx *c, float r2_threshold, wld_progress_fn progress, void 
     // Batches of whole chunks, contiguous in the reference order, of at most
     // 2^31 pairs each (a run's staging positions are 32-bit); their rows
     // concatenate in order.  progress gets the running pair count per batch.
-    uint64_t limit = 1ull << 31;
-    if (const char *e = getenv("WLD_HOST_BATCH_PAIRS")) limit = std::max<uint64_t>(1, strtoull(e, nullptr, 10));  // tests
+    const uint64_t limit = std::max<uint64_t>(1, c->opt_host_batch_pairs);
     const uint32_t m = chunks_of(c->L);
     uint64_t cap = 0, done = 0, pairs_done = 0;
     auto grow = [&](uint64_t need) -> int {

@@ -21,6 +21,8 @@
 #include <condition_variable>
 #include <mutex>
 #include <thread>
+
+#include <unistd.h>
 #include <vector>
 
 #include "weightedld.h"
@@ -217,15 +219,25 @@ Opt parse(int argc, char **argv) {
     return o;
 }
 
+// Ends the process from any point after the device-context thread started:
+// streams are flushed, but no static destructor runs — the HIP runtime may
+// still be starting up on that thread, and tearing it down underneath it
+// crashes (SIGSEGV seen on the GPU box).  A Rust panic likewise just ends the
+// process with the other threads still running.
+[[noreturn]] void quit(int code) {
+    fflush(nullptr);
+    _exit(code);
+}
+
 // Rust's `main() -> Result<(), io::Error>` prints "Error: ..." and exits 1;
 // a panic prints the panic message and exits 101.
 [[noreturn]] void die(int st, const char *what) {
     if (st == WLD_E_FORMAT || st == WLD_E_ARG) {
         fprintf(stderr, "thread 'main' panicked at '%s: %s'\n", what, wld_last_error());
-        exit(101);
+        quit(101);
     }
     fprintf(stderr, "Error: %s: %s (%s)\n", what, wld_status_string(st), wld_last_error());
-    exit(1);
+    quit(1);
 }
 
 std::string debug_path(const std::string &p) { return "\"" + p + "\""; }
@@ -377,7 +389,7 @@ int run_gpu_prepass(const Opt &opt, wld_siteset *siteset, wld_ctx *ctx) {
         INFO("Writing weights to %s", debug_path(opt.weights_output).c_str());
         if (write_henikoff_weights(opt.weights_output, weights) != WLD_OK) {
             fprintf(stderr, "Error: cannot write %s\n", opt.weights_output.c_str());
-            return 1;
+            quit(1);  // the context thread may still be running
         }
     }
     INFO("Beginning pairwise weighted LD computation");
@@ -451,7 +463,7 @@ int main(int argc, char **argv) {
         INFO("Writing weights to %s", debug_path(opt.weights_output).c_str());
         if (write_henikoff_weights(opt.weights_output, weights) != WLD_OK) {
             fprintf(stderr, "Error: cannot write %s\n", opt.weights_output.c_str());
-            return 1;
+            quit(1);  // the context thread may still be running
         }
     }
 

@@ -55,7 +55,7 @@ void launch_fill_ones(float *w, size_t N, hipStream_t s);
 // pair_valu.hip
 void launch_pair_valu(const uint8_t *codes, const float *w, const uint8_t *site_ok, const uint32_t *tiles,
                       uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, bool safe,
-                      const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
+                      bool plain, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
 
 // pair_mfma.hip
 bool mfma_supported();
@@ -65,24 +65,50 @@ void launch_mfma_prep(const uint8_t *site_ok, const float *w_pad, size_t L, size
                       int8_t *planes, hipStream_t s);
 // frag holds 2 LP NP bytes: selector-coded, then 0/1/2-coded (B operands)
 void launch_frag(const uint8_t *codes, size_t LP, size_t NP, uint8_t *frag, hipStream_t s);
-// frag != nullptr: LDS-streaming kernel on the fragment-major copy; else the
-// site-major kernel
-// plane_mask: the weight-digit planes with a nonzero digit (mfma_plane_mask);
-// the LDS kernel runs 4 MFMA products per active plane
-void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const uint8_t *frag_b, const int8_t *wplanes, const uint32_t *tiles,
-                      uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
-                      unsigned plane_mask, bool prefilter, const OrderArgs &o, const DenseArgs *dense,
-                      hipStream_t s);
-// after launch_mfma_prep on stream s: bit p = plane p has a nonzero digit (synchronises s)
-unsigned mfma_plane_mask(const int8_t *wplanes, size_t LP, size_t NP, hipStream_t s);
+// weight-plane statistics written by launch_mfma_prep (read back once per load)
+struct MfmaWeightStats {
+    unsigned plane_mask;  // bit p = digit plane p (of 4) has a nonzero digit
+    int nonneg;           // every weight >= 0
+    uint64_t resid[3];    // resid[t-1] = sum_k |q_k - 2^(8t) d_t,k|: what top plane t alone leaves out
+};
+// synchronises s; returns 0, or -1 on a HIP error
+int mfma_weight_stats(const int8_t *wplanes, size_t LP, size_t NP, hipStream_t s, MfmaWeightStats *out);
+
+// workgroups of the candidate launch after a screen (it strides over a tile
+// list whose length is known only on the device): 4 rounds of 2 per CU
+constexpr uint32_t kCandidateGrid = 2048;
+
+struct MfmaLaunch {
+    const uint8_t *codes;   // site-major codes (used when frag is null)
+    const uint8_t *frag;    // fragment-major selector-coded copy (LDS kernel), or null
+    const uint8_t *frag_b;  // fragment-major 0/1/2-coded copy (B operands)
+    const int8_t *wplanes;
+    const uint32_t *tiles;
+    uint32_t n_tiles, L, NP, n_chunk_rows;
+    float thr;
+    int shift;
+    unsigned plane_mask;
+    int nonneg;
+    bool prefilter;  // thr > 0: skip pairs r2_bound_skip rejects
+    bool screen;     // thr > 0 and >= 2 planes: one-plane screen, then candidates
+    uint64_t resid[3];
+    uint32_t *cand_list;   // n_tiles entries
+    unsigned *cand_count;  // 0 before the launch (chunk_scan_kernel resets it)
+};
+// Enqueues the MFMA pair kernel(s) of one pass; returns true when the screen
+// ran (then screen_done, if given, is recorded between the two launches).
+bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *dense, hipStream_t s,
+                      hipEvent_t screen_done);
 
 // order.hip
 // zeroes the run state (staging cursor, row total, every chunk total)
 void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t n_chunks, hipStream_t s);
 // count_out (device, may be null): also receives the run's row total
+// host_out[2] receives the screen's candidate-tile count (cand_count, which
+// the scan resets to 0; may be null)
 void launch_chunk_scan(uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
                        unsigned long long *total, unsigned long long *cursor, unsigned long long *host_out,
-                       unsigned long long *count_out, hipStream_t s);
+                       unsigned long long *count_out, unsigned *cand_count, hipStream_t s);
 void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,
                    uint32_t n_chunk_rows, uint32_t L, const uint32_t *site_map, uint32_t *out_a, uint32_t *out_b,
                    float *out_d, float *out_dp, float *out_r2, hipStream_t s);

@@ -34,7 +34,8 @@ __global__ __launch_bounds__(1024) void chunk_scan_kernel(uint32_t *__restrict__
                                                            unsigned long long *__restrict__ total,
                                                            unsigned long long *__restrict__ cursor,
                                                            unsigned long long *host_out,
-                                                           unsigned long long *__restrict__ count_out) {
+                                                           unsigned long long *__restrict__ count_out,
+                                                           unsigned *__restrict__ cand_count) {
     __shared__ unsigned long long sw[16];
     const uint32_t tid = threadIdx.x;
     const uint32_t per = (count + 1023) / 1024;
@@ -62,9 +63,15 @@ __global__ __launch_bounds__(1024) void chunk_scan_kernel(uint32_t *__restrict__
         if (count_out) *count_out = run;  // e.g. the caller's tensor for the RCCL count exchange
         const unsigned long long cur = *cursor;
         *cursor = 0;
+        unsigned cand = 0;
+        if (cand_count) {
+            cand = *cand_count;
+            *cand_count = 0;
+        }
         if (host_out) {
             host_out[0] = cur;
             host_out[1] = run;
+            host_out[2] = cand;
             __threadfence_system();
         }
     }
@@ -158,9 +165,9 @@ void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32
 
 void launch_chunk_scan(uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
                        unsigned long long *total, unsigned long long *cursor, unsigned long long *host_out,
-                       unsigned long long *count_out, hipStream_t s) {
+                       unsigned long long *count_out, unsigned *cand_count, hipStream_t s) {
     hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(1024), 0, s, chunk_total, lin_begin, count, chunk_base, total,
-                       cursor, host_out, count_out);
+                       cursor, host_out, count_out, cand_count);
 }
 
 void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,

@@ -44,6 +44,39 @@ __device__ __forceinline__ void ld_epilogue(float total_weight, float PA, float 
     r2_out = d * d / (PA * Pa * PB * Pb);
 }
 
+// Rigorous skip test for the r2 > thr filter (thr > 0).  T, A, B, AB are
+// approximations of a pair's exact masked sums T, SA, SB, SAB (any common
+// unit) whose 2x2 cells n11 = AB, n10 = A-AB, n01 = B-AB, n00 = T-A-B+AB are
+// each within e_c of the exact cells, sum_c |e_c| <= R (R = 0: the sums are
+// exact).  Returns true only if ld_epilogue, run on the correctly rounded f32
+// values of the EXACT sums, cannot give r2 > thr — so skipping the pair never
+// changes the output.  Derivation ("Prefilter and screen"):
+//   * the f32 epilogue's d is within e_d = 16.25u (u = 2^-24) of the exact
+//     D = (SA SB - SAB T) / T^2 (all normalised quantities in [0, 1]), and its
+//     denominator PA Pa PB Pb is >= P (1 - 5u sum_i 1/f_i - 3u), f_i the four
+//     normalised marginals, so r2_f32 <= (|D| + e_d)^2 (1+u)^2 / (P (1 - rel));
+//   * with uncertain sums, |num - num^| <= R max_c |n^_c| + R^2/4, each
+//     marginal is within R, T within R.
+// Evaluated division-free in f64 with e_d = 24u, rel = 28u T/m + 8u, and a
+// 1e-12 relative allowance for the f64 evaluation itself.  Exact cells must be
+// >= 0 (normalised quantities in [0, 1]): guaranteed for nonnegative weights,
+// else checked as n^_c >= R.
+__device__ __forceinline__ bool r2_bound_skip(double T, double A, double B, double AB, double R, float thr,
+                                              bool nonneg) {
+    constexpr double u = 0x1p-24;
+    const double n10 = A - AB, n01 = B - AB, n00 = (T - A) - n01;
+    if (!nonneg && fmin(fmin(AB, n10), fmin(n01, n00)) < R) return false;
+    const double cmax = fmax(fmax(fabs(AB), fabs(n10)), fmax(fabs(n01), fabs(n00)));
+    const double m1 = A - R, m2 = (T - A) - R, m3 = B - R, m4 = (T - B) - R;
+    const double mlo = fmin(fmin(m1, m2), fmin(m3, m4));
+    if (!(mlo > 0.0)) return false;
+    const double Tub = T + R;
+    const double nub = fabs(A * B - AB * T) + R * cmax + 0.25 * R * R + (24.0 * u + 0x1p-40) * Tub * Tub;
+    const double lhs = nub * nub * ((1.0 + 4.0 * u) * (1.0 + 1e-12)) * mlo;
+    const double rhs = (double)thr * ((m1 * m2) * (m3 * m4)) * (mlo * (1.0 - 8.0 * u) - 28.0 * u * Tub);
+    return lhs <= rhs;
+}
+
 __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
     const int lane = threadIdx.x & 63;
 #pragma unroll

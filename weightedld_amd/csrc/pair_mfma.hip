@@ -42,6 +42,8 @@
 // issued right after the barrier and lands during this group's 4 x 48 MFMAs.
 // Passing rows are compacted per tile in LDS (order.hip assembles the
 // reference order).
+#include <algorithm>
+
 #include "pair_common.hpp"
 
 
@@ -55,61 +57,88 @@ bool mfma_supported() { return true; }
 namespace {
 constexpr int kGroup = 8;                           // 32-sequence stages per LDS group
 constexpr int kStageCodes = 4096;                   // A0 A1 B0 B1, 1 KB each
-constexpr int kDigStage = 128;                      // digit bytes per stage: [plane][half][16] + 32 pad
+constexpr int kDigStage = 128;                      // digit bytes per stage: [plane][half][16], 4 planes
+constexpr int kMaxPlanes = 4;                       // balanced base-256 digits of the fixed-point weights
+constexpr uint32_t kPlanes012 = 0 | (1 << 2) | (2 << 4);  // plane_idx of planes 0, 1, 2
 constexpr int kDigGroup = 1024;                     // digit records of one group: one full-wave DMA
-// stages per LDS group of the kernel with NPL active digit planes: one plane
-// (equal weights) uses 4-stage groups, 34 KB of LDS per workgroup and 108
-// VGPRs, so four workgroups (4 waves per SIMD) share a CU
-#ifndef WLD_KG1
-#define WLD_KG1 4
-#endif
-#ifndef WLD_WG1
-#define WLD_WG1 (WLD_KG1 <= 4 ? 4 : 2)
-#endif
+// Shape of the LDS kernel with NPL active digit planes.  One plane (equal
+// weights, and the screen) uses 4-stage groups, 34 KB of LDS per workgroup
+// and ~108 VGPRs, so four workgroups (4 waves per SIMD) share a CU.  Two or
+// three planes: 8-stage groups, four waves of 16 a rows x 64 b columns (NB = 4
+// column blocks each), 192 accumulators, two workgroups per CU.  Four planes
+// (31-bit fixed point): eight waves of 16 a rows x 32 b columns (NB = 2), so
+// the 4 x 32 products per wave fit the same 128 accumulators as two planes
+// and no partial sum has to be held across passes; one workgroup per CU,
+// still two waves per SIMD.
 template <int NPL>
 struct GroupShape {
-    static constexpr int kStages = NPL == 1 ? WLD_KG1 : kGroup;
+    static constexpr int kStages = NPL == 1 ? 4 : kGroup;
     static constexpr int kBytes = kStages * kStageCodes + kDigGroup;
-    static constexpr int kWgPerCu = NPL == 1 ? WLD_WG1 : 2;
+    static constexpr int kWaves = NPL == 4 ? 8 : 4;
+    static constexpr int kNB = NPL == 4 ? 2 : 4;  // 16-column b blocks per wave
+    static constexpr int kWgPerCu = NPL == 1 ? 4 : NPL == 4 ? 1 : 2;
 };
 
-__host__ __device__ inline size_t digf_offset(size_t NP) { return 3 * NP; }
+__host__ __device__ inline size_t digf_offset(size_t NP) { return kMaxPlanes * NP; }
 __host__ __device__ inline size_t okbits_offset(size_t NP) {
-    return 3 * NP + (NP / 32 + kGroup - 1) / kGroup * kDigGroup;
+    return kMaxPlanes * NP + (NP / 32 + kGroup - 1) / kGroup * kDigGroup;
 }
 // byte of the digit record of stage kb within digf
 __host__ __device__ inline size_t digf_stage(uint32_t kb) { return (size_t)(kb / kGroup) * kDigGroup + (kb % kGroup) * kDigStage; }
 }  // namespace
 
 // planes buffer (mfma_planes_bytes): the weight digits of q = rint(w * 2^shift)
-// in two layouts, then the site filter as bits:
+// (q = d0 + 2^8 d1 + 2^16 d2 + 2^24 d3, balanced digits in [-128, 127]; d3 = 0
+// for a 3-plane shift) in two layouts, then the site filter as bits:
 //   planes[p*NP + k]                      plane-major (site-major kernel path)
 //   digf[(kb/kGroup)*1024 + (kb%kGroup)*128 + (2p + h)*16 + j]
 //                                         per 32-sequence stage, 1 KB per group
 //                                         (LDS path; k = 32kb + 16h + j)
 //   ok_bits[g] bit i = site 64g+i passes  (site_ok, lib.rs:400-408)
-//   plane_mask (u32 after the bits)       bit p = some digit of plane p is nonzero
+//   stats (after the bits, 32 bytes):
+//     u32  bit p (p < 4) = some digit of plane p is nonzero; bit 8 = some weight < 0
+//     u64  resid[t-1] = sum_k |q_k - 2^(8t) d_t,k| for t = 1, 2, 3: what the top
+//          plane t alone leaves out (the screen's residual bound)
 __host__ __device__ inline size_t planemask_offset(size_t LP, size_t NP) { return okbits_offset(NP) + LP / 64 * 8; }
 // + 1 KB: a half-group (kg < kGroup) digit DMA copies 1 KB from a 512-B offset
-size_t mfma_planes_bytes(size_t LP, size_t NP) { return planemask_offset(LP, NP) + 16 + kDigGroup; }
+size_t mfma_planes_bytes(size_t LP, size_t NP) { return planemask_offset(LP, NP) + 32 + kDigGroup; }
 
 __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict__ w_pad, uint32_t NP, int shift,
                                                          int8_t *__restrict__ planes, int8_t *__restrict__ digf,
-                                                         unsigned *__restrict__ plane_mask) {
+                                                         unsigned *__restrict__ stats) {
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= NP) return;
-    unsigned used = 0;
-    long long q = llrint(ldexp((double)w_pad[k], shift));
-    const uint32_t kb = k >> 5, h = (k >> 4) & 1, j = k & 15;
+    unsigned used = 0, res[3] = {0, 0, 0};
+    if (k < NP) {
+        const float w = w_pad[k];
+        long long q = llrint(ldexp((double)w, shift));
+        const uint32_t kb = k >> 5, h = (k >> 4) & 1, j = k & 15;
+        int low = 0;  // q mod 2^(8p), balanced: what planes >= p leave out
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
-        const long long r = ((q + 128) & 255) - 128;  // balanced digit in [-128, 127]
-        q = (q - r) / 256;
-        planes[p * NP + k] = (int8_t)r;
-        digf[digf_stage(kb) + (2 * p + h) * 16 + j] = (int8_t)r;
-        used |= (r != 0) << p;
+        for (int p = 0; p < kMaxPlanes; ++p) {
+            if (p > 0) res[p - 1] = (unsigned)abs(low);
+            const long long r = ((q + 128) & 255) - 128;  // balanced digit in [-128, 127]
+            q = (q - r) / 256;
+            low += (int)r << (8 * p);
+            planes[p * NP + k] = (int8_t)r;
+            digf[digf_stage(kb) + (2 * p + h) * 16 + j] = (int8_t)r;
+            used |= (r != 0) << p;
+        }
+        used |= (w < 0.0f) << 8;
     }
-    if (used) atomicOr(plane_mask, used);
+    // per-wave sums (<= 64 * 2^23 < 2^32), one atomic each per wave
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        used |= __shfl_xor(used, off, 64);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) res[t] += __shfl_xor(res[t], off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (used) atomicOr(stats, used);
+        unsigned long long *acc = reinterpret_cast<unsigned long long *>(stats + 2);
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+            if (res[t]) atomicAdd(acc + t, (unsigned long long)res[t]);
+    }
 }
 
 // one wave per 64 sites
@@ -172,6 +201,7 @@ __device__ __forceinline__ v4i mfma_i8_16(v4i a, v4i b, v4i c) {
 template <int NPL>
 struct Acc32 {
     static constexpr int kPlanes = NPL;
+    static constexpr int kPairs = 16;
     v16i v[2][NPL][2];  // [channel_a][plane][channel_b]
     __device__ __forceinline__ int get(int x, int p, int y, int i) const { return v[x][p][y][i]; }
     static __device__ __forceinline__ uint32_t a_local(int i, uint32_t wave, uint32_t lane) {
@@ -181,17 +211,17 @@ struct Acc32 {
         return 32 * (wave & 1) + (lane & 31);
     }
 };
-// 16x16x64 shape, wave w owns a rows 16w..16w+15 against all 64 b columns as
-// four 16x16 blocks n (C/D col = lane & 15, row = 4 (lane >> 4) + e); register
-// i = 4n + e.  NPL = the weight-digit planes that are not all zero (3 for
-// general weights, 1 for equal weights, e.g. --unweighted).
-template <int NPL>
+// 16x16x64 shape, wave w owns a rows 16(w & 3)..+15 against NB 16x16 blocks
+// of b columns starting at block NB (w >> 2) (all 64 columns when NB = 4 with
+// four waves; 32 when NB = 2 with eight) (C/D col = lane & 15, row =
+// 4 (lane >> 4) + e); register i = 4n + e, kPairs = 4 NB per lane.  NPL = the
+// weight-digit planes that are not all zero (3 for general weights, 1 for
+// equal weights, e.g. --unweighted, 4 for weights spanning more than 2^4).
+template <int NPL, int NB = 4>
 struct Acc16 {
     static constexpr int kPlanes = NPL;
-    v4i v[4][2][NPL][2];  // [n][channel_a][plane][channel_b]
-#ifdef WLD_BPERM
-    __device__ __forceinline__ int get(int x, int p, int y, int i) const { return v[i >> 2][x][p][y][i & 3]; }
-#else
+    static constexpr int kPairs = 4 * NB;
+    v4i v[NB][2][NPL][2];  // [n][channel_a][plane][channel_b]
     // channel_b slots hold X = S(raw) = S(minor) + 2 S(major) and Y = S(minor)
     // (mfma_block_sel16): S(in) = (X + Y) / 2, S(major) = (X - Y) / 2, both
     // exact (X - Y is even) and in int32 range (|X| + |Y| <= 3 * 128 NP)
@@ -199,12 +229,11 @@ struct Acc16 {
         const int X = v[i >> 2][x][p][0][i & 3], Y = v[i >> 2][x][p][1][i & 3];
         return (y ? X - Y : X + Y) >> 1;
     }
-#endif
     static __device__ __forceinline__ uint32_t a_local(int i, uint32_t wave, uint32_t lane) {
-        return 16 * wave + 4 * (lane >> 4) + (i & 3);
+        return 16 * (wave & 3) + 4 * (lane >> 4) + (i & 3);
     }
     static __device__ __forceinline__ uint32_t b_local(int i, uint32_t wave, uint32_t lane) {
-        return 16 * (i >> 2) + (lane & 15);
+        return 16 * (NB * (wave >> 2) + (i >> 2)) + (lane & 15);
     }
 };
 
@@ -215,22 +244,18 @@ struct Acc16 {
 // the k order inside the instruction.  48 MFMAs of 16 cycles = the 24 of 32 of
 // two 32x32 stages; each A operand (digit x channel) feeds 8 MFMAs, so it
 // takes 56 v_perm per 48 MFMAs (64 with a 32x32 wave tile).
-template <int NPL>
-__device__ __forceinline__ void mfma_block_sel16(v4i (&acc)[4][2][NPL][2], v4i ca, const v4i (&cb)[4],
+template <int NPL, int NB>
+__device__ __forceinline__ void mfma_block_sel16(v4i (&acc)[NB][2][NPL][2], v4i ca, const v4i (&cb)[NB],
                                                  const v4i (&dp)[NPL]) {
     constexpr unsigned kOnes = 0x01010101u;
-    v4i b_in[4], b_maj[4];
+    v4i b_in[NB], b_maj[NB];
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < NB; ++n)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-#ifdef WLD_BPERM  // selector-coded B: in / major indicators, two v_perm per dword
-            b_in[n][e] = (int)__builtin_amdgcn_perm(kOnes, kOnes, (unsigned)cb[n][e]);
-            b_maj[n][e] = (int)__builtin_amdgcn_perm(kOnes, 0u, (unsigned)cb[n][e]);
-#else  // 0/1/2-coded B: the raw bytes (minor + 2 major) and the minor bit, one v_and per dword
+            // 0/1/2-coded B: the raw bytes (minor + 2 major) and the minor bit, one v_and per dword
             b_in[n][e] = cb[n][e];
             b_maj[n][e] = cb[n][e] & (int)kOnes;
-#endif
         }
 #pragma unroll
     for (int p = 0; p < NPL; ++p) {
@@ -241,7 +266,7 @@ __device__ __forceinline__ void mfma_block_sel16(v4i (&acc)[4][2][NPL][2], v4i c
             am[e] = (int)__builtin_amdgcn_perm((unsigned)dp[p][e], 0u, (unsigned)ca[e]);
         }
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
+        for (int n = 0; n < NB; ++n) {
             acc[n][0][p][0] = mfma_i8_16(ai, b_in[n], acc[n][0][p][0]);
             acc[n][0][p][1] = mfma_i8_16(ai, b_maj[n], acc[n][0][p][1]);
             acc[n][1][p][0] = mfma_i8_16(am, b_in[n], acc[n][1][p][0]);
@@ -309,22 +334,6 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
 }
 
-#ifdef WLD_EXP_STAMPS
-// diagnostic build only: per-tile cycle stamps of wave 0 (start, first group,
-// loop end, epilogue end) and where it ran (HW_ID | XCC_ID << 32)
-constexpr unsigned kStampWords = 5;
-__device__ unsigned long long g_stamps[kStampWords << 18];
-__device__ __forceinline__ unsigned long long stamp() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-extern "C" int wld_debug_stamps_copy(unsigned long long *out, unsigned n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), (size_t)n * kStampWords * 8) == hipSuccess ? 0 : -1;
-}
-#endif
 
 template <int NPL>
 __device__ __forceinline__ void zero_acc(Acc32<NPL> &acc) {
@@ -337,10 +346,10 @@ __device__ __forceinline__ void zero_acc(Acc32<NPL> &acc) {
 #pragma unroll
                 for (int e = 0; e < 16; ++e) acc.v[x][p][y][e] = 0;
 }
-template <int NPL>
-__device__ __forceinline__ void zero_acc(Acc16<NPL> &acc) {
+template <int NPL, int NB>
+__device__ __forceinline__ void zero_acc(Acc16<NPL, NB> &acc) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < NB; ++n)
 #pragma unroll
         for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -351,98 +360,97 @@ __device__ __forceinline__ void zero_acc(Acc16<NPL> &acc) {
                     for (int e = 0; e < 4; ++e) acc.v[n][x][p][y][e] = 0;
 }
 
+// What a pair-kernel launch does with each tile's sums (pair_eval /
+// tile_epilogue):
+//   kModeDense     every pair's stats to dense matrices (tests)
+//   kModeAll       reference epilogue for every valid pair, compaction
+//   kModePrefilter the same, skipping pairs that r2_bound_skip proves cannot
+//                  pass (exact sums, R = 0; threshold > 0)
+//   kModeScreen    one weight-digit plane only (the top one): every valid
+//                  pair's r2 is bounded with the plane's residual bound R; a
+//                  tile with any pair the bound cannot reject is appended to
+//                  the candidate list (recomputed with every plane by the
+//                  kModePrefilter launch), the others write their zero counts
+enum : int { kModeDense = 0, kModeAll = 1, kModePrefilter = 2, kModeScreen = 3 };
+
+// per-launch screen/candidate arguments
+struct ScreenArgs {
+    double R;               // kModeScreen: residual bound in top-digit units
+    int nonneg;             // all weights >= 0 (exact 2x2 cells are >= 0)
+    uint32_t *cand_list;    // kModeScreen: candidate tiles (packed ta << 16 | tb)
+    unsigned *cand_count;   // kModeScreen: appended to; candidate launch: tile count
+};
+
 // Reference epilogue of one pair from its exact sums (fixed-point units):
-// the optional exact-algebra prefilter, then lib.rs:482-520 in f32.  Returns
-// true when the pair passes (valid and r2 > thr, lib.rs:660); d/dp/r2 are
-// written when the f32 epilogue ran (always for DENSE).
-template <bool DENSE, bool PREFILTER>
+// the optional prefilter, then lib.rs:482-520 in f32.  Returns true when the
+// pair passes (valid and r2 > thr, lib.rs:660); d/dp/r2 are written when the
+// f32 epilogue ran (always for kModeDense).
+template <int MODE>
 __device__ __forceinline__ bool pair_eval(double T, double SA, double SB, double SAB, bool valid, float thr,
-                                          double scale, float &d, float &dp, float &r2) {
-    if constexpr (!DENSE) {
+                                          double scale, bool nonneg, float &d, float &dp, float &r2) {
+    if constexpr (MODE != kModeDense) {
         if (!valid) return false;
-        if constexpr (PREFILTER) {
-            // Exact algebra: d = PA*PB - P(AB) and r2 = d^2/(PA Pa PB Pb) become
-            // r2 = (SA*SB - SAB*T)^2 / (SA (T-SA) SB (T-SB)) on the exact sums.
-            // Evaluated in f64 (|err| ~1e-16 relative); pairs more than
-            // 1e-5 + 1e-4|thr| below the threshold cannot pass the f32 epilogue,
-            // so they skip it.  Everything else (and den <= 0, the NaN/inf
-            // cases) takes the full reference epilogue.
-            const double num = SA * SB - SAB * T;
-            const double den = SA * (T - SA) * SB * (T - SB);
-            const double cut = (double)thr - (1e-5 + 1e-4 * fabs((double)thr));
-            if (den > 0.0 && num * num < cut * den) return false;
-        }
+        // the f32 epilogue below provably gives r2 <= thr (pair_common.hpp)
+        if constexpr (MODE == kModePrefilter)
+            if (r2_bound_skip(T, SA, SB, SAB, 0.0, thr, nonneg)) return false;
     }
     ld_epilogue((float)(T * scale), (float)(SA * scale), (float)(SB * scale), (float)(SAB * scale), d, dp, r2);
     return valid && r2 > thr;
 }
 
-// Epilogue of one 64x64 tile.  The lane holds b = b0 + 32wb + r and 16 a rows
-// (MFMA C layout: row (i&3) + 8(i>>2) + 4h).  DENSE writes every pair's stats
-// (tests); otherwise passing pairs are compacted through the tile's 64x64
-// pass-bit matrix in LDS into staging, with per-(a, b-tile) segment counts and
-// offsets for order.hip.  PREFILTER (threshold > 0) skips the f32 epilogue for
-// pairs whose exact r2, evaluated in f64 from the exact sums, lies clearly
-// below the threshold.
-template <bool DENSE, bool PREFILTER, class Acc>
-__device__ __forceinline__ void tile_epilogue(const Acc &acc, uint32_t ta, uint32_t tb, uint32_t tid,
+// Epilogue of one 64x64 tile.  The lane holds 16 (a, b) pairs (Acc::a_local,
+// b_local).  kModeDense writes every pair's stats (tests); kModeAll and
+// kModePrefilter compact passing pairs through the tile's 64x64 pass-bit
+// matrix in LDS into staging, with per-(a, b-tile) segment counts and offsets
+// for order.hip; kModeScreen only decides whether the tile is a candidate.
+//
+// sum(x, y, i) returns the lane's i-th pair's sum over channel_a x (0 = in,
+// 1 = major) and channel_b y as an exact integer in f64: in fixed-point units
+// (S = sum_p 2^(8p) acc_p), or for kModeScreen in units of the screened plane.
+template <int MODE, class Acc, class SumFn>
+__device__ __forceinline__ void tile_epilogue(const SumFn &sum, uint32_t ta, uint32_t tb, uint32_t tid,
                                               uint64_t okA, uint64_t okB, uint32_t L, uint32_t n_chunk_rows,
-                                              float thr, int shift, bool narrow, uint32_t plane_idx,
-                                              const OrderArgs &o, const DenseArgs &dn, unsigned long long *sBits,
-                                              uint32_t *sRowBase) {
+                                              float thr, int shift, const OrderArgs &o, const DenseArgs &dn,
+                                              const ScreenArgs &sc, unsigned long long *sBits, uint32_t *sRowBase) {
     const uint32_t wave = tid >> 6, lane = tid & 63;
-    double pscale[Acc::kPlanes];  // 2^(8 idx_j) of the j-th active plane (plane_idx: 2 bits per plane)
-#pragma unroll
-    for (int j = 0; j < Acc::kPlanes; ++j) pscale[j] = (double)(1u << (8 * ((plane_idx >> (2 * j)) & 3)));
     const uint32_t a0 = ta * kTile, b0 = tb * kTile;
     const double scale = ldexp(1.0, -shift);
-    float res[16][3];
+    if constexpr (MODE == kModeScreen) {
+        // sums in units of the screened digit plane, within R of the exact
+        // sums scaled to that unit (cells: sum_c |e_c| <= R)
+        bool cand = false;
+#pragma unroll
+        for (int i = 0; i < Acc::kPairs; ++i) {
+            const uint32_t a_local = Acc::a_local(i, wave, lane);
+            const uint32_t b_local = Acc::b_local(i, wave, lane);
+            const bool valid = ((okB >> b_local) & 1) && a0 + a_local < b0 + b_local && ((okA >> a_local) & 1);
+            if (valid && !cand)
+                cand = !r2_bound_skip(sum(0, 0, i), sum(1, 0, i), sum(0, 1, i), sum(1, 1, i), sc.R, thr,
+                                      sc.nonneg != 0);
+        }
+        if (__syncthreads_or(cand)) {
+            if (tid == 0) sc.cand_list[atomicAdd(sc.cand_count, 1u)] = (ta << 16) | tb;
+        } else if (tid < kTile) {
+            o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
+        }
+        return;
+    }
+    float res[Acc::kPairs][3];
     uint32_t pass = 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < Acc::kPairs; ++i) {
         const uint32_t a_local = Acc::a_local(i, wave, lane);
         const uint32_t b_local = Acc::b_local(i, wave, lane);
         const uint32_t a = a0 + a_local, b = b0 + b_local;
         const bool valid = ((okB >> b_local) & 1) && a < b && ((okA >> a_local) & 1);
-#ifdef WLD_EXP_NOEPI
-        if constexpr (!DENSE) {  // diagnostic: accumulators consumed, no epilogue arithmetic
-            int x = 0;
-#pragma unroll
-            for (int c = 0; c < 4 * Acc::kPlanes; ++c)
-                x ^= acc.get(c / (2 * Acc::kPlanes), (c / 2) % Acc::kPlanes, c % 2, i);
-            if (valid && x == 0x7fffffff) pass |= 1u << i;
-            res[i][0] = res[i][1] = res[i][2] = 0.f;
-            continue;
-        }
-#endif
-        // S = acc_0 + 2^8 acc_1 + 2^16 acc_2: integers below 2^48, exact in f64.
-        // |acc_p| <= 128 NP, so acc_1 + 2^8 acc_2 is exact in int32 while
-        // 32896 NP < 2^31 (NP <= 65024): one int op, two conversions, one FMA.
-        // With fewer planes (all-zero digit planes skipped) S = sum_j 2^(8 idx_j) acc_j.
-        double S[2][2];
-#pragma unroll
-        for (int x = 0; x < 2; ++x)
-#pragma unroll
-            for (int y = 0; y < 2; ++y) {
-                if constexpr (Acc::kPlanes < 3) {
-                    double v = 0.0;
-#pragma unroll
-                    for (int j = 0; j < Acc::kPlanes; ++j) v = fma(pscale[j], (double)acc.get(x, j, y, i), v);
-                    S[x][y] = v;
-                } else if (narrow) {
-                    const int hi = acc.get(x, 1, y, i) + acc.get(x, 2, y, i) * 256;
-                    S[x][y] = fma(256.0, (double)hi, (double)acc.get(x, 0, y, i));
-                } else {
-                    S[x][y] = fma(65536.0, (double)acc.get(x, 2, y, i),
-                                  fma(256.0, (double)acc.get(x, 1, y, i), (double)acc.get(x, 0, y, i)));
-                }
-            }
         float d = 0.f, dp = 0.f, r2 = 0.f;
-        const bool ok = pair_eval<DENSE, PREFILTER>(S[0][0], S[1][0], S[0][1], S[1][1], valid, thr, scale, d, dp, r2);
+        const bool ok =
+            pair_eval<MODE>(sum(0, 0, i), sum(1, 0, i), sum(0, 1, i), sum(1, 1, i), valid, thr, scale, sc.nonneg != 0,
+                            d, dp, r2);
         res[i][0] = d;
         res[i][1] = dp;
         res[i][2] = r2;
-        if constexpr (DENSE) {
+        if constexpr (MODE == kModeDense) {
             if (a < b && b < L) {
                 const size_t k = (size_t)a * L + b;
                 dn.d[k] = d;
@@ -454,7 +462,7 @@ __device__ __forceinline__ void tile_epilogue(const Acc &acc, uint32_t ta, uint3
             if (ok) pass |= 1u << i;  // lib.rs:660 strict '>'
         }
     }
-    if constexpr (DENSE) return;
+    if constexpr (MODE == kModeDense) return;
 
     // ---- compaction: a 64x64 pass-bit matrix in LDS, rows in b order ----------
     // A tile with no passing pair (every tile at the bench threshold on random
@@ -468,7 +476,7 @@ __device__ __forceinline__ void tile_epilogue(const Acc &acc, uint32_t ta, uint3
     __syncthreads();
     if (pass) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
+        for (int i = 0; i < Acc::kPairs; ++i)
             if (pass & (1u << i))
                 atomicOr(&sBits[Acc::a_local(i, wave, lane)], 1ull << Acc::b_local(i, wave, lane));
     }
@@ -492,7 +500,7 @@ __device__ __forceinline__ void tile_epilogue(const Acc &acc, uint32_t ta, uint3
     __syncthreads();
     if (pass) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < Acc::kPairs; ++i) {
             if (!(pass & (1u << i))) continue;
             const uint32_t a_local = Acc::a_local(i, wave, lane);
             const uint32_t b_local = Acc::b_local(i, wave, lane);
@@ -509,141 +517,162 @@ __device__ __forceinline__ void tile_epilogue(const Acc &acc, uint32_t ta, uint3
     }
 }
 
-// LDS-streaming kernel over fragment-major, selector-coded codes: one 64x64
-// tile per workgroup.  (An XCD-contiguous block->tile remap measured no gain:
-// the 41 MB code copy of BASELINE config 4 is served from L2/MALL either way.)
-template <bool DENSE, bool PREFILTER, int NPL>
-__global__ __launch_bounds__(256, GroupShape<NPL>::kWgPerCu) void pair_mfma_kernel(const uint8_t *__restrict__ frag,
-                                                            const uint8_t *__restrict__ frag_b,
-                                                            const int8_t *__restrict__ planes,
-                                                            const uint64_t *__restrict__ ok_bits,
-                                                            const uint32_t *__restrict__ tiles, uint32_t L,
-                                                            uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
-                                                            uint32_t plane_idx, OrderArgs o, DenseArgs dn) {
+// LDS-streaming kernel over fragment-major, selector-coded codes, one 64x64
+// tile per workgroup; with LOOP (the candidate launch after a screen, whose
+// list length tile_count is only known on the device) workgroup i computes
+// tiles i, i + gridDim.x, ... (a separate instantiation: the loop costs
+// registers the one-tile kernel does not have to give up).  (An
+// XCD-contiguous block->tile remap measured no gain: the 41 MB code copy of
+// BASELINE config 4 is served from L2/MALL either way.)
+template <int MODE, int NPL, bool LOOP>
+__global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgPerCu) void pair_mfma_kernel(
+    const uint8_t *__restrict__ frag, const uint8_t *__restrict__ frag_b, const int8_t *__restrict__ planes,
+    const uint64_t *__restrict__ ok_bits, const uint32_t *__restrict__ tiles, uint32_t n_tiles,
+    const unsigned *tile_count, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
+    uint32_t plane_idx, OrderArgs o, DenseArgs dn, ScreenArgs sc) {
     constexpr int KG = GroupShape<NPL>::kStages, KGB = GroupShape<NPL>::kBytes;
+    constexpr int WAVES = GroupShape<NPL>::kWaves, NB = GroupShape<NPL>::kNB;
     __shared__ __attribute__((aligned(16))) uint8_t smem[2 * KGB];  // operand groups (DMA targets)
     __shared__ unsigned long long sBits[kTile];                              // compaction (never a DMA target)
     __shared__ uint32_t sRowBase[kTile];
 
-    const uint32_t tid = threadIdx.x;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const uint32_t NKB = NP / 32;
-    const uint32_t n_groups = (NKB + KG - 1) / KG;
+    auto compute_tile = [&](uint32_t tile, uint32_t tid) {
+        const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+        const uint32_t NKB = NP / 32;
+        const uint32_t n_groups = (NKB + KG - 1) / KG;
+        const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
 
-#ifdef WLD_EXP_STAMPS
-    const unsigned long long ts0 = stamp();
-#endif
-    const uint32_t tile = tiles[blockIdx.x];
-    if (tile == kNoTile) return;  // padding of an XCD-ordered list (whole workgroup)
-    const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
+        // this wave's 1 KB code block per stage: A0/A1 (a sites, selector-coded
+        // copy), B0/B1 (b sites, 0/1/2-coded copy); with eight waves, waves w
+        // and w + 4 copy the same block of alternate stages
+        const uint32_t wb = wave & 3;
+        const uint32_t g = wb < 2 ? 2 * ta + wb : 2 * tb + (wb - 2);
+        const uint8_t *src = (wb < 2 ? frag : frag_b) + (size_t)g * NKB * 1024;  // wave-uniform
+        const int8_t *digf = planes + digf_offset(NP);
+        const uint32_t smem_lds = lds_addr(smem);
+        auto issue = [&](uint32_t grp, uint32_t buf) {
+            const uint32_t gb = smem_lds + buf * KGB;
+            const uint32_t kb0 = grp * KG;
+            const uint8_t *base = src + (size_t)kb0 * 1024;
+            const uint32_t lane16 = lane * 16;
+#pragma unroll
+            for (int st = 0; st < KG; ++st)
+                if ((WAVES == 4 || (uint32_t)(st & 1) == (wave >> 2)) && kb0 + st < NKB)
+                    glds16(base + (uint32_t)(st * 1024) + lane16, gb + st * kStageCodes + wb * 1024);
+            // digit records of the group's stages (128 B each, contiguous from
+            // digf_stage(kb0)): one 1 KB full-wave copy (allocation padded past
+            // the last group)
+            if (wave == 0) glds16(digf + digf_stage(kb0) + lane16, gb + KG * kStageCodes);
+        };
 
-    // this wave's 1 KB code block per stage: A0/A1 (a sites), B0/B1 (b sites)
-    const uint32_t g = wave < 2 ? 2 * ta + wave : 2 * tb + (wave - 2);
-#ifdef WLD_BPERM
-    (void)frag_b;
-    const uint8_t *src = frag + (size_t)g * NKB * 1024;  // wave-uniform
-#else
-    const uint8_t *src = (wave < 2 ? frag : frag_b) + (size_t)g * NKB * 1024;  // wave-uniform
-#endif
-    const int8_t *digf = planes + digf_offset(NP);
-    const uint32_t smem_lds = lds_addr(smem);
-    auto issue = [&](uint32_t grp, uint32_t buf) {
-        const uint32_t gb = smem_lds + buf * KGB;
-        const uint32_t kb0 = grp * KG;
-        const uint8_t *base = src + (size_t)kb0 * 1024;
-        const uint32_t lane16 = lane * 16;
+        issue(0, 0);
+        const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
+        // lane group g = lane >> 4 reads stage 2s + (g >> 1), half g & 1, of each
+        // 64-sequence step (the 32-stage fragment layout, re-addressed): a sites
+        // 16w.. = rows 16(w & 1).. of 32-site block w >> 1 (w = wave & 3); b
+        // block nb = rows 16(nb & 1).. of B block nb >> 1
+        const uint32_t g4 = lane >> 4, so = g4 >> 1, hh = g4 & 1;
+        const uint32_t lrow = so * kStageCodes + (32 * hh + (lane & 15)) * 16;
+        const uint32_t offA = lrow + (wb >> 1) * 1024 + (wb & 1) * 256;
+        const uint32_t offB = lrow + 2048 + (WAVES == 8 ? (wave >> 2) * 1024 : 0);  // + (n >> 1) * 1024 + (n & 1) * 256
+        const uint32_t offD = KG * kStageCodes + so * kDigStage + hh * 16;
+        // the active planes' 32-byte rows of a stage's digit record (NPL 3 is
+        // always planes 0-2 and NPL 4 all four: compile-time offsets, kept as
+        // immediates)
+        uint32_t offP[NPL];
 #pragma unroll
-        for (int st = 0; st < KG; ++st)
-            if (kb0 + st < NKB) glds16(base + (uint32_t)(st * 1024) + lane16, gb + st * kStageCodes + wave * 1024);
-        // digit records of the group's stages (128 B each, contiguous from
-        // digf_stage(kb0)): one 1 KB full-wave copy (allocation padded past
-        // the last group)
-        if (wave == 0) glds16(digf + digf_stage(kb0) + lane16, gb + KG * kStageCodes);
-    };
+        for (int j = 0; j < NPL; ++j) offP[j] = offD + 32 * (NPL >= 3 ? j : ((plane_idx >> (2 * j)) & 3));
 
-    issue(0, 0);
-    const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
-    Acc16<NPL> acc;
-    // lane group g = lane >> 4 reads stage 2s + (g >> 1), half g & 1, of each
-    // 64-sequence step (the 32-stage fragment layout, re-addressed): a sites
-    // 16w.. = rows 16(w & 1).. of 32-site block w >> 1; b block n = rows
-    // 16(n & 1).. of B block n >> 1
-    const uint32_t g4 = lane >> 4, so = g4 >> 1, hh = g4 & 1;
-    const uint32_t lrow = so * kStageCodes + (32 * hh + (lane & 15)) * 16;
-    const uint32_t offA = lrow + (wave >> 1) * 1024 + (wave & 1) * 256;
-    const uint32_t offB = lrow + 2048;  // + (n >> 1) * 1024 + (n & 1) * 256
-    const uint32_t offD = KG * kStageCodes + so * kDigStage + hh * 16;
-    // the active planes' 32-byte rows of a stage's digit record (all three:
-    // compile-time offsets, so the reads keep immediate offsets)
-    uint32_t offP[NPL];
+        Acc16<NPL, NB> acc;
+        zero_acc(acc);
+        uint32_t buf = 0;
+        for (uint32_t grp = 0; grp < n_groups; ++grp) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this group landed
+            __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
+            asm volatile("" ::: "memory");
+            if (grp + 1 < n_groups) issue(grp + 1, buf ^ 1);
+            const uint8_t *gb = smem + buf * KGB;
+            const uint32_t n_st = min((uint32_t)KG, NKB - grp * KG);
+            for (uint32_t st = 0; st < n_st; st += 2) {  // n_st is even: NP is a multiple of 64
+                const uint8_t *sc_ = gb + st * kStageCodes;
+                const uint8_t *sd = gb + st * kDigStage;
+                const v4i ca = *reinterpret_cast<const v4i *>(sc_ + offA);
+                v4i cb[NB];
 #pragma unroll
-    for (int j = 0; j < NPL; ++j) offP[j] = NPL == 3 ? offD + 32 * j : offD + 32 * ((plane_idx >> (2 * j)) & 3);
-    zero_acc(acc);
-    uint32_t buf = 0;
-#ifdef WLD_EXP_PRIO
-    __builtin_amdgcn_s_setprio(WLD_EXP_PRIO);  // the matrix loop outranks a partner's epilogue VALU
-#endif
-#ifdef WLD_EXP_STAMPS
-    unsigned long long tsg = 0;
-#endif
-    for (uint32_t grp = 0; grp < n_groups; ++grp) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this group landed
-        __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
-        asm volatile("" ::: "memory");
-#ifdef WLD_EXP_STAMPS
-        if (grp == 0) tsg = stamp();
-#endif
-        if (grp + 1 < n_groups) issue(grp + 1, buf ^ 1);
-        const uint8_t *gb = smem + buf * KGB;
-        const uint32_t n_st = min((uint32_t)KG, NKB - grp * KG);
-        for (uint32_t st = 0; st < n_st; st += 2) {  // n_st is even: NP is a multiple of 64
-            const uint8_t *sc = gb + st * kStageCodes;
-            const uint8_t *sd = gb + st * kDigStage;
-            const v4i ca = *reinterpret_cast<const v4i *>(sc + offA);
-            const v4i cb[4] = {*reinterpret_cast<const v4i *>(sc + offB), *reinterpret_cast<const v4i *>(sc + offB + 256),
-                               *reinterpret_cast<const v4i *>(sc + offB + 1024),
-                               *reinterpret_cast<const v4i *>(sc + offB + 1280)};
-            v4i dp[NPL];
+                for (int n = 0; n < NB; ++n)
+                    cb[n] = *reinterpret_cast<const v4i *>(sc_ + offB + (n >> 1) * 1024 + (n & 1) * 256);
+                v4i dp[NPL];
 #pragma unroll
-            for (int j = 0; j < NPL; ++j)
-                dp[j] = *reinterpret_cast<const v4i *>(NPL == 3 ? sd + offD + 32 * j : sd + offP[j]);
-            mfma_block_sel16<NPL>(acc.v, ca, cb, dp);
+                for (int j = 0; j < NPL; ++j) dp[j] = *reinterpret_cast<const v4i *>(sd + offP[j]);
+                mfma_block_sel16<NPL, NB>(acc.v, ca, cb, dp);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
+            buf ^= 1;
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
-        buf ^= 1;
+        const bool narrow = NP <= 65024u;
+        auto sum = [&](int x, int y, int i) -> double {
+            if constexpr (MODE == kModeScreen) {
+                return (double)acc.get(x, 0, y, i);  // units of the screened plane
+            } else if constexpr (NPL >= 3) {
+                // S = sum_p 2^(8p) acc_p, integers below 2^53, exact in f64.
+                // |acc_p| <= 128 NP, so acc_1 + 2^8 acc_2 (and acc_2 + 2^8 acc_3)
+                // is exact in int32 while 32896 NP < 2^31 (NP <= 65024; the
+                // host keeps 4 planes within that).
+                if constexpr (NPL == 4) {
+                    if (narrow) {
+                        const int h23 = acc.get(x, 2, y, i) + acc.get(x, 3, y, i) * 256;
+                        const int lo = acc.get(x, 0, y, i) + acc.get(x, 1, y, i) * 256;
+                        return fma(65536.0, (double)h23, (double)lo);
+                    }
+                    return fma(16777216.0, (double)acc.get(x, 3, y, i),
+                               fma(65536.0, (double)acc.get(x, 2, y, i),
+                                   fma(256.0, (double)acc.get(x, 1, y, i), (double)acc.get(x, 0, y, i))));
+                } else {
+                    if (narrow) {
+                        const int h12 = acc.get(x, 1, y, i) + acc.get(x, 2, y, i) * 256;
+                        return fma(256.0, (double)h12, (double)acc.get(x, 0, y, i));
+                    }
+                    return fma(65536.0, (double)acc.get(x, 2, y, i),
+                               fma(256.0, (double)acc.get(x, 1, y, i), (double)acc.get(x, 0, y, i)));
+                }
+            } else {
+                // all-zero planes skipped: sum_j 2^(8 idx_j) acc_j, exact
+                double v = 0.0;
+#pragma unroll
+                for (int j = 0; j < NPL; ++j)
+                    v = fma((double)(1u << (8 * ((plane_idx >> (2 * j)) & 3))), (double)acc.get(x, j, y, i), v);
+                return v;
+            }
+        };
+        tile_epilogue<MODE, Acc16<NPL, NB>>(sum, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, shift, o, dn, sc, sBits,
+                                            sRowBase);
+    };
+    if constexpr (!LOOP) {
+        const uint32_t tile = tiles[blockIdx.x];
+        if (tile != kNoTile) compute_tile(tile, threadIdx.x);  // kNoTile: padding of an XCD-ordered list
+    } else {
+        const uint32_t nt = *tile_count;
+        for (uint32_t bi = blockIdx.x; bi < nt; bi += gridDim.x) {
+            // the thread id laundered per tile: nothing lane-derived is hoisted
+            // out of the loop and held live across the epilogue
+            uint32_t tid = threadIdx.x;
+            asm volatile("" : "+v"(tid));
+            compute_tile(tiles[bi], tid);
+            __syncthreads();  // the next tile's first DMA reuses buffer 0 and the compaction state
+        }
     }
-#ifdef WLD_EXP_STAMPS
-    const unsigned long long ts1 = stamp();
-#endif
-#ifdef WLD_EXP_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
-    tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, shift, NP <= 65024u,
-                                    plane_idx, o, dn, sBits, sRowBase);
-#ifdef WLD_EXP_STAMPS
-    const unsigned long long ts2 = stamp();
-    if (tid == 0 && blockIdx.x < (1u << 18)) {
-        const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
-        const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
-        g_stamps[kStampWords * blockIdx.x] = ts0;
-        g_stamps[kStampWords * blockIdx.x + 1] = tsg;
-        g_stamps[kStampWords * blockIdx.x + 2] = ts1;
-        g_stamps[kStampWords * blockIdx.x + 3] = ts2;
-        g_stamps[kStampWords * blockIdx.x + 4] = hw | ((unsigned long long)xcc << 32);
-    }
-#endif
 }
 
 // Site-major variant (one tile per workgroup, codes read straight into
-// registers): the reference for the LDS path's race screen and the
-// WLD_MFMA_LAYOUT=rows experiments.
-template <bool DENSE, bool PREFILTER>
+// registers, all three digit planes): the reference for the LDS path's race
+// screen (WLD_OPT_MFMA_LAYOUT).
+template <int MODE>
 __global__ __launch_bounds__(256, 2) void pair_mfma_rows_kernel(const uint8_t *__restrict__ codes,
                                                                  const int8_t *__restrict__ planes,
                                                                  const uint64_t *__restrict__ ok_bits,
                                                                  const uint32_t *__restrict__ tiles, uint32_t L,
                                                                  uint32_t NP, uint32_t n_chunk_rows, float thr,
-                                                                 int shift, OrderArgs o, DenseArgs dn) {
+                                                                 int shift, OrderArgs o, DenseArgs dn, ScreenArgs sc) {
     __shared__ unsigned long long sBits[kTile];
     __shared__ uint32_t sRowBase[kTile];
     const uint32_t tile = tiles[blockIdx.x];
@@ -664,16 +693,24 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_rows_kernel(const uint8_t *_
         const v4i d2 = *reinterpret_cast<const v4i *>(pd + 2 * NP + k0);
         mfma_block(acc.v, ca, cb, d0, d1, d2);
     }
-    tile_epilogue<DENSE, PREFILTER>(acc, ta, tb, tid, ok_bits[ta], ok_bits[tb], L, n_chunk_rows, thr, shift,
-                                    NP <= 65024u, 0x24u, o, dn, sBits, sRowBase);
+    const bool narrow = NP <= 65024u;
+    auto sum = [&](int x, int y, int i) -> double {
+        if (narrow) {
+            const int hi = acc.get(x, 1, y, i) + acc.get(x, 2, y, i) * 256;
+            return fma(256.0, (double)hi, (double)acc.get(x, 0, y, i));
+        }
+        return fma(65536.0, (double)acc.get(x, 2, y, i), fma(256.0, (double)acc.get(x, 1, y, i), (double)acc.get(x, 0, y, i)));
+    };
+    tile_epilogue<MODE, Acc32<3>>(sum, ta, tb, tid, ok_bits[ta], ok_bits[tb], L, n_chunk_rows, thr, shift, o, dn, sc,
+                                  sBits, sRowBase);
 }
 
 void launch_mfma_prep(const uint8_t *site_ok, const float *w_pad, size_t L, size_t LP, size_t NP, int shift,
                       int8_t *planes, hipStream_t s) {
-    unsigned *mask = reinterpret_cast<unsigned *>(planes + planemask_offset(LP, NP));
-    (void)hipMemsetAsync(mask, 0, sizeof(unsigned), s);
+    unsigned *stats = reinterpret_cast<unsigned *>(planes + planemask_offset(LP, NP));
+    (void)hipMemsetAsync(stats, 0, 32, s);
     hipLaunchKernelGGL(mfma_prep_kernel, dim3((unsigned)((NP + 255) / 256)), dim3(256), 0, s, w_pad, (uint32_t)NP,
-                       shift, planes, planes + digf_offset(NP), mask);
+                       shift, planes, planes + digf_offset(NP), stats);
     hipLaunchKernelGGL(okbits_kernel, dim3((unsigned)(LP / 64)), dim3(64), 0, s, site_ok, (uint32_t)L,
                        reinterpret_cast<uint64_t *>(planes + okbits_offset(NP)));
 }
@@ -684,66 +721,96 @@ void launch_frag(const uint8_t *codes, size_t LP, size_t NP, uint8_t *frag, hipS
                        (uint32_t)NP, frag);
 }
 
-template <int NPL>
-void launch_lds(const uint8_t *frag, const uint8_t *frag_b, const int8_t *wplanes, const uint64_t *ok_bits, const uint32_t *tiles,
-                uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
-                uint32_t plane_idx, bool prefilter, const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
-    const DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
-    const dim3 g(n_tiles), b(256);
-    if (dense)
-        hipLaunchKernelGGL((pair_mfma_kernel<true, false, NPL>), g, b, 0, s, frag, frag_b, wplanes, ok_bits, tiles, L,
-                           NP, n_chunk_rows, thr, shift, plane_idx, o, dn);
-    else if (prefilter)
-        hipLaunchKernelGGL((pair_mfma_kernel<false, true, NPL>), g, b, 0, s, frag, frag_b, wplanes, ok_bits, tiles, L,
-                           NP, n_chunk_rows, thr, shift, plane_idx, o, dn);
-    else
-        hipLaunchKernelGGL((pair_mfma_kernel<false, false, NPL>), g, b, 0, s, frag, frag_b, wplanes, ok_bits, tiles, L,
-                           NP, n_chunk_rows, thr, shift, plane_idx, o, dn);
-}
-
-unsigned mfma_plane_mask(const int8_t *wplanes, size_t LP, size_t NP, hipStream_t s) {
-    unsigned m = 7;
-    if (hipMemcpyAsync(&m, wplanes + planemask_offset(LP, NP), sizeof(m), hipMemcpyDeviceToHost, s) != hipSuccess ||
+int mfma_weight_stats(const int8_t *wplanes, size_t LP, size_t NP, hipStream_t s, MfmaWeightStats *out) {
+    struct {
+        unsigned mask, pad;
+        unsigned long long resid[3];
+    } h{};
+    if (hipMemcpyAsync(&h, wplanes + planemask_offset(LP, NP), sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
-        return 7;  // all planes: always correct
-    return m & 7;
+        return -1;
+    out->plane_mask = h.mask & 15;
+    out->nonneg = !(h.mask & 0x100);
+    for (int t = 0; t < 3; ++t) out->resid[t] = h.resid[t];
+    return 0;
 }
 
-void launch_pair_mfma(const uint8_t *codes, const uint8_t *frag, const uint8_t *frag_b, const int8_t *wplanes, const uint32_t *tiles,
-                      uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, int shift,
-                      unsigned plane_mask, bool prefilter, const OrderArgs &o, const DenseArgs *dense,
-                      hipStream_t s) {
+namespace {
+template <int MODE, int NPL, bool LOOP = false>
+void launch_lds(const MfmaLaunch &m, const uint64_t *ok_bits, const uint32_t *tiles, uint32_t n_tiles,
+                const unsigned *tile_count, uint32_t grid, uint32_t plane_idx, const OrderArgs &o, const DenseArgs &dn,
+                const ScreenArgs &sc, hipStream_t s) {
+    hipLaunchKernelGGL((pair_mfma_kernel<MODE, NPL, LOOP>), dim3(grid), dim3(64 * GroupShape<NPL>::kWaves), 0, s, m.frag, m.frag_b, m.wplanes,
+                       ok_bits, tiles, n_tiles, tile_count, m.L, m.NP, m.n_chunk_rows, m.thr, m.shift, plane_idx, o,
+                       dn, sc);
+}
+
+template <int MODE, bool LOOP = false>
+void launch_lds_planes(uint32_t n_planes, const MfmaLaunch &m, const uint64_t *ok_bits, const uint32_t *tiles,
+                       uint32_t n_tiles, const unsigned *tile_count, uint32_t grid, uint32_t plane_idx,
+                       const OrderArgs &o, const DenseArgs &dn, const ScreenArgs &sc, hipStream_t s) {
+    if (n_planes == 4)
+        launch_lds<MODE, 4, LOOP>(m, ok_bits, tiles, n_tiles, tile_count, grid, plane_idx, o, dn, sc, s);
+    else if (n_planes == 3)
+        launch_lds<MODE, 3, LOOP>(m, ok_bits, tiles, n_tiles, tile_count, grid, plane_idx, o, dn, sc, s);
+    else if (n_planes == 2 || LOOP)  // the looping candidate launch follows a screen: >= 2 planes
+        launch_lds<MODE, 2, LOOP>(m, ok_bits, tiles, n_tiles, tile_count, grid, plane_idx, o, dn, sc, s);
+    else
+        launch_lds<MODE, 1, false>(m, ok_bits, tiles, n_tiles, tile_count, grid, plane_idx, o, dn, sc, s);
+}
+}  // namespace
+
+bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *dense, hipStream_t s,
+                      hipEvent_t screen_done) {
     const DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
-    const uint64_t *ok_bits = reinterpret_cast<const uint64_t *>(wplanes + okbits_offset(NP));
-    const dim3 g(n_tiles), b(256);
-    if (frag) {
-        // the nonzero digit planes in ascending order, 2 bits each; no plane is
-        // all zero only if some weight is nonzero, which the caller guarantees
-        plane_mask &= 7;
-        if (!plane_mask) plane_mask = 7;
-        uint32_t idx = 0, n = 0;
-        for (uint32_t p = 0; p < 3; ++p)
-            if (plane_mask >> p & 1) idx |= p << (2 * n++);
-        if (n == 3)
-            launch_lds<3>(frag, frag_b, wplanes, ok_bits, tiles, n_tiles, L, NP, n_chunk_rows, thr, shift, idx, prefilter, o,
-                          dense, s);
-        else if (n == 2)
-            launch_lds<2>(frag, frag_b, wplanes, ok_bits, tiles, n_tiles, L, NP, n_chunk_rows, thr, shift, idx, prefilter, o,
-                          dense, s);
-        else
-            launch_lds<1>(frag, frag_b, wplanes, ok_bits, tiles, n_tiles, L, NP, n_chunk_rows, thr, shift, idx, prefilter, o,
-                          dense, s);
-    } else {
+    const uint64_t *ok_bits = reinterpret_cast<const uint64_t *>(m.wplanes + okbits_offset(m.NP));
+    const bool prefilter = !dense && m.prefilter && m.thr > 0.0f;
+    ScreenArgs sc{0.0, m.nonneg, m.cand_list, m.cand_count};
+    if (!m.frag) {  // site-major kernel (all three planes)
+        const dim3 g(m.n_tiles), b(256);
         if (dense)
-            hipLaunchKernelGGL((pair_mfma_rows_kernel<true, false>), g, b, 0, s, codes, wplanes, ok_bits, tiles, L,
-                               NP, n_chunk_rows, thr, shift, o, dn);
+            hipLaunchKernelGGL((pair_mfma_rows_kernel<kModeDense>), g, b, 0, s, m.codes, m.wplanes, ok_bits, m.tiles,
+                               m.L, m.NP, m.n_chunk_rows, m.thr, m.shift, o, dn, sc);
         else if (prefilter)
-            hipLaunchKernelGGL((pair_mfma_rows_kernel<false, true>), g, b, 0, s, codes, wplanes, ok_bits, tiles, L,
-                               NP, n_chunk_rows, thr, shift, o, dn);
+            hipLaunchKernelGGL((pair_mfma_rows_kernel<kModePrefilter>), g, b, 0, s, m.codes, m.wplanes, ok_bits,
+                               m.tiles, m.L, m.NP, m.n_chunk_rows, m.thr, m.shift, o, dn, sc);
         else
-            hipLaunchKernelGGL((pair_mfma_rows_kernel<false, false>), g, b, 0, s, codes, wplanes, ok_bits, tiles, L,
-                               NP, n_chunk_rows, thr, shift, o, dn);
+            hipLaunchKernelGGL((pair_mfma_rows_kernel<kModeAll>), g, b, 0, s, m.codes, m.wplanes, ok_bits, m.tiles,
+                               m.L, m.NP, m.n_chunk_rows, m.thr, m.shift, o, dn, sc);
+        return false;
     }
+    // the nonzero digit planes in ascending order, 2 bits each; no plane is
+    // all zero only if some weight is nonzero, which the caller guarantees
+    unsigned mask = m.plane_mask & 15;
+    if (!mask) mask = 15;
+    uint32_t idx = 0, n = 0, top = 0;
+    for (uint32_t p = 0; p < kMaxPlanes; ++p)
+        if (mask >> p & 1) idx |= p << (2 * n++), top = p;
+    // three active planes other than 0-2 (a 4-plane shift with one all-zero
+    // plane) run as four: NPL 3 always means planes 0, 1, 2
+    if (n == 3 && idx != kPlanes012) n = 4;
+    if (n == 4) idx = 0 | (1 << 2) | (2 << 4) | (3 << 6);
+    if (dense) {
+        launch_lds_planes<kModeDense>(n, m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, idx, o, dn, sc, s);
+        return false;
+    }
+    if (!prefilter) {
+        launch_lds_planes<kModeAll>(n, m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, idx, o, dn, sc, s);
+        return false;
+    }
+    if (!m.screen || n < 2) {
+        launch_lds_planes<kModePrefilter>(n, m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, idx, o, dn, sc, s);
+        return false;
+    }
+    // Screen: the top plane alone over every tile, the residual of the lower
+    // planes bounded by R (in top-digit units: exact, a power-of-two scaling
+    // of an integer below 2^53); candidate tiles then get every plane.
+    sc.R = ldexp((double)m.resid[top - 1], -8 * (int)top);
+    launch_lds<kModeScreen, 1>(m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, top, o, dn, sc, s);
+    if (screen_done) (void)hipEventRecord(screen_done, s);
+    const uint32_t grid = std::min<uint32_t>(m.n_tiles, kCandidateGrid);
+    launch_lds_planes<kModePrefilter, true>(n, m, ok_bits, m.cand_list, 0, m.cand_count, grid, idx, o, dn, sc, s);
+    return true;
 }
 
 }  // namespace wld

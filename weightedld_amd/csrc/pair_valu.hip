@@ -281,12 +281,12 @@ __global__ __launch_bounds__(256, MF ? WLD_VALU_MF_WG : 2) void pair_valu_kernel
 
 void launch_pair_valu(const uint8_t *codes, const float *w, const uint8_t *site_ok, const uint32_t *tiles,
                       uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, bool safe,
-                      const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
+                      bool plain, const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
     DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
     const uint32_t flush = (uint32_t)std::max(1.0, std::floor(std::sqrt((double)NP) / 64.0 + 0.5));
-    // finite weights: products and sums on the matrix cores (WLD_VALU_PLAIN=1:
-    // the VALU loop, for A/B); non-finite weights keep the select loop
-    static const bool plain = getenv("WLD_VALU_PLAIN") != nullptr;
+    // finite weights: products and sums on the matrix cores (plain, option
+    // WLD_OPT_VALU_PLAIN: the VALU loop, for A/B); non-finite weights keep the
+    // select loop
     const dim3 g(n_tiles), b(256);
     if (dense) {
         if (safe)
