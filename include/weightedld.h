@@ -115,6 +115,19 @@ typedef struct wld_ctx wld_ctx;
 /* One context per device; owns its HIP stream, device buffers and results.
  * Not thread-safe; separate contexts are independent.  device = HIP ordinal. */
 int wld_create(int device, wld_ctx **out);
+/* A context over n_devices devices (HIP ordinals; repeats allowed, e.g. to run
+ * several shards on one device in tests): one member context per entry.
+ * wld_load replicates the input to every member; wld_run_host and
+ * wld_all_weighted_ld_pairs (the reference's one call, lib.rs:578-684, which
+ * uses every core) shard the reference's chunk sequence over the members
+ * (wld_shard_chunks: contiguous ranges balanced by pair count), run them
+ * concurrently, and return the rows in the reference order (shards
+ * concatenated in descending shard order).  Options and the kernel choice
+ * apply to every member; wld_last_stats reports member 0's kernel with the
+ * group's pair/row totals.  Other device entry points fail with WLD_E_STATE
+ * on such a context.  With n_devices == 1 it behaves like wld_create. */
+int wld_create_multi(const int *devices, int n_devices, wld_ctx **out);
+int wld_n_devices(const wld_ctx *ctx); /* 1, or the member count of a multi-device context */
 void wld_destroy(wld_ctx *ctx);
 
 /* Kernel selection.  AUTO (default): the exact-integer MFMA kernel when the

@@ -73,3 +73,121 @@ def test_gloo_shard_gather_matches_unsharded(world, L, N, thr, by_chunk):
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     ok, n_got, n_ref = q.get(timeout=10)
     assert ok and n_got == n_ref
+
+
+class OracleShardContext:
+    """Stand-in for a device Context in the N>1 step path (ShardStep,
+    PipelinedShardStep): run_chunks_async computes the chunk range's rows with
+    the oracle and writes the row count (int64) to the given address, as
+    wld_run_chunks_async does on the device; rows_copy_device copies them to
+    the given (host) addresses, as wld_rows_copy_device does."""
+
+    def __init__(self, buf, w):
+        self.buf, self.w, self.rows, self.pending = buf, w, None, False
+
+    def stream_ptr(self):
+        return 0
+
+    def run_chunks_async(self, thr, lo, hi, d_count_ptr=None):
+        import ctypes
+
+        import _oracle as O
+        assert not self.pending, "run_chunks_async twice without run_wait"
+        self.rows = O.all_pairs(self.buf, self.w, thr, n_threads=2, chunk_lo=lo, chunk_hi=hi)
+        self.pending = True
+        if d_count_ptr:
+            ctypes.c_int64.from_address(d_count_ptr).value = len(self.rows["r2"])
+
+    def run_wait(self):
+        assert self.pending, "run_wait with nothing in flight"
+        self.pending = False
+        return len(self.rows["r2"])
+
+    def rows_copy_device(self, a, b, d, dp, r2):
+        import ctypes
+        for ptr, f, dt in ((a, "site_a", np.uint32), (b, "site_b", np.uint32), (d, "d", np.float32),
+                           (dp, "d_prime", np.float32), (r2, "r2", np.float32)):
+            col = np.ascontiguousarray(self.rows[f].astype(dt))
+            if ptr and col.size:
+                ctypes.memmove(ptr, col.ctypes.data, col.nbytes)
+
+
+def ld_region_data(L, N, seed):
+    """Random sites (no pair near r2 0.5 at this N) plus one block of 40
+    linked sites near the end of the site order: at r2_threshold 0.5 only the
+    shards holding those sites' chunks have rows."""
+    rng = np.random.default_rng(seed)
+    buf = rng.integers(0, 2, size=(L, N)).astype(np.uint8)  # 2 symbols: every site has maj+min
+    f = rng.random(N) < 0.4
+    for s in range(L - 60, L - 20):
+        buf[s] = np.where(f ^ (rng.random(N) < 0.03), 1, 0)
+    return buf, rng.random(N).astype(np.float32) + 0.2
+
+
+def _step_worker(rank, world, port, L, N, thrs, pipelined, q):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import torch.distributed as dist
+
+    import _oracle as O
+    from weightedld_amd import dist as wdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        buf, w = ld_region_data(L, N, 5)
+        lo, hi = wdist.shard_chunks(L, world, rank)
+        results = []
+        if pipelined:
+            pipe = wdist.PipelinedShardStep([OracleShardContext(buf, w), OracleShardContext(buf, w)], rank, world,
+                                            "cpu")
+            for t in thrs:
+                r = pipe.submit(t, lo, hi)
+                if r is not None:
+                    results.append(r)
+            results.append(pipe.drain())
+        else:
+            step = wdist.ShardStep(OracleShardContext(buf, w), rank, world, "cpu")
+            results = [step(t, lo, hi) for t in thrs]
+        mine = [int(n) for n, _ in results]
+        counts = [None] * world
+        dist.all_gather_object(counts, mine)
+        if rank == 0:
+            ok = []
+            for i, t in enumerate(thrs):
+                ref = O.all_pairs(buf, w, t, n_threads=2)
+                got = wdist.unpack_rows(results[i][1])
+                ok.append(all(np.array_equal(got[f], ref[f].astype(got[f].dtype)) for f in wdist.ROW_FIELDS))
+            q.put((ok, counts))
+        else:
+            assert all(r[1] is None for r in results)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("pipelined", [False, True], ids=["step", "pipelined"])
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_gloo_shard_steps_match_unsharded(world, pipelined):
+    """ShardStep / PipelinedShardStep (the bench's N>1 step path) at world
+    2-4 under gloo: per step, the count exchange, the row gather issued only
+    when some rank has rows, and (pipelined) step i-1's gather issued after
+    step i's count exchange — every step's gathered rows equal the unsharded
+    oracle's, in reference order, with threshold sequences where no rank,
+    one rank or every rank has rows, and nothing deadlocks."""
+    L, N = 1200, 200
+    thrs = [0.0, 2.0, 0.5, 2.0, 0.0, 0.5, 0.5]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_step_worker, args=(r, world, port, L, N, thrs, pipelined, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    ok, counts = q.get(timeout=10)
+    assert all(ok), ok
+    # the planted block gives rows at 0.5 to some ranks only; 2.0 to none
+    per_step = list(zip(*counts))
+    assert all(sum(c) == 0 for c, t in zip(per_step, thrs) if t == 2.0)
+    assert any(0 < sum(1 for x in c if x) < world for c, t in zip(per_step, thrs) if t == 0.5)

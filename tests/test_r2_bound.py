@@ -1,0 +1,113 @@
+"""The pair kernels' skip test (pair_common.hpp r2_bound_skip, compiled for
+the host from the same source) against the f32 epilogue (lib.rs:482-520) on
+adversarial inputs: a pair it skips must never pass r2 > thr when the
+epilogue runs on the correctly rounded exact sums — including the
+near-degenerate tables (a minor allele carrying ~1e-6 of the weight) where the
+round-1 margin (1e-5 + 1e-4 thr below thr) skipped pairs that pass — and with
+approximate sums (the one-plane screen: every 2x2 cell within R in total).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+U = 2.0 ** -24
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("bound") / "bound_check")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-ffp-contract=off",
+                    "-I", os.path.join(REPO, "include"), "-I", os.path.join(REPO, "weightedld_amd", "csrc"),
+                    "-x", "hip", os.path.join(REPO, "tests", "cpp", "bound_check.cpp"), "-o", exe], check=True)
+
+    def run(T, A, B, AB, R, thr, nonneg=True):
+        n = len(T)
+        rec = np.stack([np.asarray(x, np.float64) * np.ones(n) for x in (T, A, B, AB, R, thr, float(nonneg))], 1)
+        d = tmp_path_factory.mktemp("io")
+        rec.tofile(str(d / "in.bin"))
+        subprocess.run([exe, str(d / "in.bin"), str(d / "out.bin")], check=True)
+        return np.fromfile(str(d / "out.bin"), dtype=np.uint8).astype(bool)
+    return run
+
+
+def f32_r2(T, SA, SB, SAB):
+    """ld_epilogue's r2 on the f32-rounded sums (numpy float32, op for op)."""
+    f = np.float32
+    T, PA, PB, o3 = T.astype(f), SA.astype(f), SB.astype(f), SAB.astype(f)
+    with np.errstate(all="ignore"):
+        Pa, Pb = T - PA, T - PB
+        o1 = PB - o3
+        o2 = PA - o3
+        o0 = Pa - o1
+        PA, PB, Pa, Pb = PA / T, PB / T, Pa / T, Pb / T
+        o0, o1, o2, o3 = o0 / T, o1 / T, o2 / T, o3 / T
+        d = ((PA * PB - o3) + (Pa * Pb - o0) + (o2 - PA * Pb) + (o1 - Pa * PB)) / f(4)
+        return d * d / (PA * Pa * PB * Pb)
+
+
+def near_threshold_tables(rng, n, thr, scale=2.0 ** 34):
+    """Integer 2x2 tables with rare cells and exact r2 just below thr."""
+    e = 10.0 ** rng.uniform(-6, -1, (3, n))
+    n11, n10, n01 = np.floor(e[0] * scale), np.floor(e[1] * scale), np.floor(e[2] * scale)
+    n00 = scale - n11 - n10 - n01
+    T, A, B, AB = n11 + n10 + n01 + n00, n11 + n10, n11 + n01, n11
+    num, den = A * B - AB * T, A * (T - A) * B * (T - B)
+    r2 = num * num / den
+    sel = (r2 < thr) & (r2 > thr * (1 - 3e-3))
+    return T[sel], A[sel], B[sel], AB[sel]
+
+
+def test_bound_sound_on_near_degenerate_tables(harness):
+    rng = np.random.default_rng(7)
+    viol_old = viol_new = skipped = total = 0
+    for thr in (0.05, 0.1, 0.3):
+        for _ in range(20):
+            T, A, B, AB = near_threshold_tables(rng, 1_000_000, thr)
+            passes = f32_r2(T, A, B, AB) > np.float32(thr)
+            skip = harness(T, A, B, AB, 0.0, thr)
+            num, den = A * B - AB * T, A * (T - A) * B * (T - B)
+            old = (den > 0) & (num * num < (thr - (1e-5 + 1e-4 * thr)) * den)  # round 1's margin
+            viol_new += int((skip & passes).sum())
+            viol_old += int((old & passes).sum())
+            skipped += int(skip.sum())
+            total += len(T)
+    assert total > 10_000 and skipped > 0.1 * total
+    assert viol_new == 0
+    assert viol_old > 0  # the round-1 margin was unsound on these tables
+
+
+@pytest.mark.parametrize("nonneg", [True, False])
+def test_bound_sound_with_screen_residuals(harness, nonneg):
+    # approximate sums: cells perturbed by integers with sum |e_c| <= R
+    rng = np.random.default_rng(11 + nonneg)
+    viol = skipped = 0
+    for it in range(30):
+        n = 200_000
+        scale = 2.0 ** rng.integers(12, 36)
+        c = rng.random((4, n)) + (0.02 if it % 3 else 0.0)
+        if it % 3 == 2:  # rare alleles
+            eps = 10.0 ** rng.uniform(-5, -1, n)
+            c[0] *= eps
+            c[1] *= eps
+        c = np.floor(c * scale)
+        if not nonneg:  # cells may be negative (signed weights)
+            c[rng.integers(0, 4, n), np.arange(n)] *= -0.01
+            c = np.floor(c)
+        T, A, B, AB = c.sum(0), c[0] + c[1], c[0] + c[2], c[0]
+        thr = float(np.float32(rng.choice([0.01, 0.05, 0.2, 0.6])))
+        R = np.floor(rng.choice([0.0, 1e-4, 1e-3, 1e-2]) * scale)
+        e = rng.random((4, n)) * rng.choice([-1.0, 1.0], (4, n))
+        e = np.trunc(e / np.maximum(np.abs(e).sum(0), 1e-12) * R * rng.random(n))
+        h = c + e
+        skip = harness(h.sum(0), h[0] + h[1], h[0] + h[2], h[0], R, thr, nonneg)
+        with np.errstate(invalid="ignore"):
+            passes = f32_r2(T, A, B, AB) > np.float32(thr)
+        if nonneg:
+            assert (c >= 0).all()
+        viol += int((skip & passes).sum())
+        skipped += int(skip.sum())
+    assert viol == 0 and skipped > 0

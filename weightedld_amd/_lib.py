@@ -93,6 +93,8 @@ SIGNATURES = {
                                                     ctypes.POINTER(_vp)]),
     "wld_henikoff_weights": (_int, [_vp, _f32p]),
     "wld_create": (_int, [_int, ctypes.POINTER(_vp)]),
+    "wld_create_multi": (_int, [ctypes.POINTER(_int), _int, ctypes.POINTER(_vp)]),
+    "wld_n_devices": (_int, [_vp]),
     "wld_destroy": (None, [_vp]),
     "wld_set_kernel": (_int, [_vp, _int]),
     "wld_set_option": (_int, [_vp, _int, ctypes.c_int64]),

@@ -201,10 +201,17 @@ class PairStore:
 class Context:
     """One device context (wld_ctx): HIP stream, device buffers, results."""
 
-    def __init__(self, device=0, kernel=KERNEL_AUTO):
+    def __init__(self, device=0, kernel=KERNEL_AUTO, devices=None):
+        """devices (a list of HIP ordinals, repeats allowed): a multi-device
+        context (wld_create_multi) that shards load/run_host/all-pairs calls."""
         h = ctypes.c_void_p()
         self._lib = lib()  # kept: module globals may be gone when __del__ runs at exit
-        check(self._lib.wld_create(device, ctypes.byref(h)), "wld_create")
+        if devices is not None:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            check(self._lib.wld_create_multi(arr, len(devices), ctypes.byref(h)), "wld_create_multi")
+            device = devices[0]
+        else:
+            check(self._lib.wld_create(device, ctypes.byref(h)), "wld_create")
         self._h = h
         self.device = device
         if kernel != KERNEL_AUTO:
@@ -216,6 +223,9 @@ class Context:
             self._h = None
 
     __del__ = close
+
+    def n_devices(self):
+        return int(lib().wld_n_devices(self._h))
 
     def set_kernel(self, kernel):
         check(lib().wld_set_kernel(self._h, kernel), "wld_set_kernel")

@@ -10,9 +10,12 @@
 // point fails with WLD_E_NODEV.
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.hpp"
@@ -87,6 +90,9 @@ struct RunPending {
 
 struct wld_ctx {
     int device = 0;
+    // a device group (wld_create_multi): one member context per device; the
+    // group itself owns no stream or buffers
+    std::vector<wld_ctx *> members;
     hipStream_t stream = nullptr;
     hipEvent_t ev[7] = {};  // 2..3 pair phase (6: after the screen), 3..4/5 order phase
     RunPending pend;                      // the run between run_enqueue and run_complete
@@ -128,6 +134,8 @@ struct wld_ctx {
     wld_run_stats stats{};
 
     ~wld_ctx() {
+        for (wld_ctx *m : members) delete m;
+        if (!members.empty()) return;
         (void)hipSetDevice(device);
         DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &tiles, &cand,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &st_a, &st_b, &st_d,
@@ -142,8 +150,14 @@ struct wld_ctx {
 
 namespace {
 
+// Every single-device entry point starts here; a device group (wld_create_multi)
+// supports only wld_load, wld_run_host, wld_all_weighted_ld_pairs and the
+// option/kernel/stats calls, which dispatch to its members.
 int set_dev(wld_ctx *c) {
     if (!c) return fail(WLD_E_ARG, "null context");
+    if (!c->members.empty())
+        return fail(WLD_E_STATE, "this call needs a single-device context; a multi-device context supports "
+                                 "wld_load, wld_run_host and wld_all_weighted_ld_pairs");
     HIP_TRY(hipSetDevice(c->device));
     return WLD_OK;
 }
@@ -482,10 +496,32 @@ int wld_create(int device, wld_ctx **out) {
     return WLD_OK;
 }
 
+int wld_create_multi(const int *devices, int n_devices, wld_ctx **out) {
+    if (!out) return fail(WLD_E_ARG, "wld_create_multi: null out");
+    *out = nullptr;
+    if (!devices || n_devices < 1) return fail(WLD_E_ARG, "wld_create_multi: need at least one device");
+    auto *g = new wld_ctx;
+    g->device = devices[0];
+    for (int k = 0; k < n_devices; ++k) {
+        wld_ctx *m = nullptr;
+        const int st = wld_create(devices[k], &m);
+        if (st != WLD_OK) {
+            delete g;
+            return st;
+        }
+        g->members.push_back(m);
+    }
+    *out = g;
+    return WLD_OK;
+}
+
+int wld_n_devices(const wld_ctx *ctx) { return !ctx ? 0 : ctx->members.empty() ? 1 : (int)ctx->members.size(); }
+
 void wld_destroy(wld_ctx *ctx) { delete ctx; }
 
 int wld_set_kernel(wld_ctx *ctx, int kernel) {
     if (!ctx) return fail(WLD_E_ARG, "null context");
+    for (wld_ctx *m : ctx->members) WLD_TRY(wld_set_kernel(m, kernel));
     if (kernel < WLD_KERNEL_AUTO || kernel > WLD_KERNEL_MFMA) return fail(WLD_E_ARG, "bad kernel id %d", kernel);
     if (kernel == WLD_KERNEL_MFMA && !mfma_supported()) return fail(WLD_E_ARG, "MFMA kernel not built");
     ctx->kernel_pref = kernel;
@@ -494,6 +530,7 @@ int wld_set_kernel(wld_ctx *ctx, int kernel) {
 
 int wld_set_option(wld_ctx *c, int option, int64_t value) {
     if (!c) return fail(WLD_E_ARG, "null context");
+    for (wld_ctx *m : c->members) WLD_TRY(wld_set_option(m, option, value));
     if (c->pend.active) return fail(WLD_E_STATE, "wld_set_option during a run");
     switch (option) {
         case WLD_OPT_PREFILTER: c->opt_prefilter = value != 0; break;
@@ -541,6 +578,24 @@ int wld_get_option(wld_ctx *c, int option, int64_t *value) {
 
 int wld_load(wld_ctx *c, const uint8_t *sites, size_t n_sites, size_t n_seqs, const uint64_t *site_map,
              const float *weights) {
+    if (c && !c->members.empty()) {
+        // every device gets the whole input (replicated; it is small next to
+        // the pair space), loaded concurrently
+        const size_t G = c->members.size();
+        std::vector<int> st(G, WLD_OK);
+        std::vector<std::string> msg(G);
+        std::vector<std::thread> th;
+        for (size_t k = 0; k < G; ++k)
+            th.emplace_back([&, k] {
+                st[k] = wld_load(c->members[k], sites, n_sites, n_seqs, site_map, weights);
+                if (st[k] != WLD_OK) msg[k] = wld_last_error();
+            });
+        for (auto &t : th) t.join();
+        for (size_t k = 0; k < G; ++k)
+            if (st[k] != WLD_OK) return fail(st[k], "device %d: %s", c->members[k]->device, msg[k].c_str());
+        c->stats = c->members[0]->stats;
+        return WLD_OK;
+    }
     WLD_TRY(set_dev(c));
     if ((!sites && n_sites * n_seqs) || (!weights && n_seqs)) return fail(WLD_E_ARG, "wld_load: null input");
     if (n_sites >= (1u << 16) * (size_t)kTile) return fail(WLD_E_ARG, "n_sites %zu too large", n_sites);
@@ -983,16 +1038,18 @@ void wld_pairs_free(wld_pairs *p) {
     memset(p, 0, sizeof(*p));
 }
 
-int wld_run_host(wld_ctx *c, float r2_threshold, wld_progress_fn progress, void *user, wld_pairs *out) {
-    if (!out) return fail(WLD_E_ARG, "null out");
+namespace {
+// The chunks [lb, le) of the loaded set, rows to host: batches of whole
+// chunks, contiguous in the reference order, of at most opt_host_batch_pairs
+// (2^31) pairs each (a run's staging positions are 32-bit); their rows
+// concatenate in order.  progress (may be null) gets the running pair count
+// per batch.
+int run_host_range(wld_ctx *c, float r2_threshold, uint32_t lb, uint32_t le, wld_progress_fn progress, void *user,
+                   wld_pairs *out) {
     memset(out, 0, sizeof(*out));
     WLD_TRY(set_dev(c));
     if (!c->loaded) return fail(WLD_E_STATE, "wld_run_host before wld_load");
-    // Batches of whole chunks, contiguous in the reference order, of at most
-    // 2^31 pairs each (a run's staging positions are 32-bit); their rows
-    // concatenate in order.  progress gets the running pair count per batch.
     const uint64_t limit = std::max<uint64_t>(1, c->opt_host_batch_pairs);
-    const uint32_t m = chunks_of(c->L);
     uint64_t cap = 0, done = 0, pairs_done = 0;
     auto grow = [&](uint64_t need) -> int {
         if (need <= cap) return WLD_OK;
@@ -1008,10 +1065,10 @@ int wld_run_host(wld_ctx *c, float r2_threshold, wld_progress_fn progress, void 
         return WLD_OK;
     };
     int st = grow(1);
-    for (uint32_t b = 0; st == WLD_OK && b < m;) {
+    for (uint32_t b = lb; st == WLD_OK && b < le;) {
         uint32_t e = b;
         uint64_t pairs = 0;
-        while (e < m) {
+        while (e < le) {
             const uint64_t p1 = pairs_in_chunks(c->L, e, e + 1);
             if (e > b && pairs + p1 > limit) break;
             pairs += p1;
@@ -1039,6 +1096,101 @@ int wld_run_host(wld_ctx *c, float r2_threshold, wld_progress_fn progress, void 
     return WLD_OK;
 }
 
+// wld_run_host on a device group: member k runs shard k of the reference's
+// chunk sequence (wld_shard_chunks: contiguous, balanced by pair count) on
+// its own host thread (each run blocks on its device); the calling thread
+// reports progress as shards complete and concatenates the shards' rows in
+// DESCENDING shard order (shard 0 holds the last chunks).
+int run_host_group(wld_ctx *g, float thr, wld_progress_fn progress, void *user, wld_pairs *out) {
+    const int G = (int)g->members.size();
+    const size_t L = g->members[0]->L;
+    std::vector<wld_pairs> part(G);
+    std::vector<int> status(G, WLD_OK);
+    std::vector<std::string> msg(G);
+    std::vector<uint64_t> pairs(G, 0);
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<int> finished;
+    std::vector<std::thread> th;
+    for (int k = 0; k < G; ++k) {
+        uint32_t lb = 0, le = 0;
+        WLD_TRY(wld_shard_chunks(L, G, k, &lb, &le));
+        pairs[k] = pairs_in_chunks(L, lb, le);
+        th.emplace_back([&, k, lb, le] {
+            const int st = run_host_range(g->members[k], thr, lb, le, nullptr, nullptr, &part[k]);
+            std::lock_guard<std::mutex> lk(mu);
+            status[k] = st;
+            if (st != WLD_OK) msg[k] = wld_last_error();
+            finished.push_back(k);
+            cv.notify_one();
+        });
+    }
+    uint64_t pairs_done = 0;
+    for (int n = 0; n < G; ++n) {  // progress on the calling thread, as shards complete
+        int k;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return (int)finished.size() > n; });
+            k = finished[n];
+        }
+        pairs_done += pairs[k];
+        if (progress && status[k] == WLD_OK) progress(pairs_done, user);
+    }
+    for (auto &t : th) t.join();
+    int st = WLD_OK;
+    for (int k = 0; k < G; ++k)
+        if (status[k] != WLD_OK && st == WLD_OK) st = fail(status[k], "device %d (shard %d): %s", g->members[k]->device, k, msg[k].c_str());
+    uint64_t total = 0;
+    for (auto &p : part) total += p.n;
+    if (st == WLD_OK) {
+        const uint64_t n = std::max<uint64_t>(total, 1);
+        out->site_a = (uint32_t *)malloc(n * 4);
+        out->site_b = (uint32_t *)malloc(n * 4);
+        out->d = (float *)malloc(n * 4);
+        out->d_prime = (float *)malloc(n * 4);
+        out->r2 = (float *)malloc(n * 4);
+        if (!out->site_a || !out->site_b || !out->d || !out->d_prime || !out->r2)
+            st = fail(WLD_E_OOM, "host allocation of %llu rows failed", (unsigned long long)total);
+    }
+    if (st == WLD_OK) {
+        uint64_t at = 0;
+        for (int k = G - 1; k >= 0; --k) {
+            const wld_pairs &p = part[k];
+            memcpy(out->site_a + at, p.site_a, p.n * 4);
+            memcpy(out->site_b + at, p.site_b, p.n * 4);
+            memcpy(out->d + at, p.d, p.n * 4);
+            memcpy(out->d_prime + at, p.d_prime, p.n * 4);
+            memcpy(out->r2 + at, p.r2, p.n * 4);
+            at += p.n;
+        }
+        out->n = total;
+    } else {
+        wld_pairs_free(out);
+    }
+    for (auto &p : part) wld_pairs_free(&p);
+    g->stats = g->members[0]->stats;
+    g->stats.pairs = pairs_done;
+    g->stats.rows = st == WLD_OK ? total : 0;
+    double kms = 0.0;
+    for (wld_ctx *m : g->members) kms = std::max(kms, m->stats.pair_kernel_ms);
+    g->stats.pair_kernel_ms = kms;  // the slowest device's last batch
+    return st;
+}
+
+}  // namespace
+
+int wld_run_host(wld_ctx *c, float r2_threshold, wld_progress_fn progress, void *user, wld_pairs *out) {
+    if (!out) return fail(WLD_E_ARG, "null out");
+    memset(out, 0, sizeof(*out));
+    if (!c) return fail(WLD_E_ARG, "null context");
+    if (!c->members.empty()) {
+        for (wld_ctx *m : c->members)
+            if (!m->loaded) return fail(WLD_E_STATE, "wld_run_host before wld_load");
+        return run_host_group(c, r2_threshold, progress, user, out);
+    }
+    return run_host_range(c, r2_threshold, 0, chunks_of(c->L), progress, user, out);
+}
+
 int wld_all_weighted_ld_pairs(wld_ctx *c, const uint8_t *sites, size_t n_sites, size_t n_seqs,
                               const uint64_t *site_map, const float *weights, float r2_threshold,
                               wld_progress_fn progress, void *user, wld_pairs *out) {
@@ -1052,6 +1204,12 @@ int wld_all_weighted_ld_pairs(wld_ctx *c, const uint8_t *sites, size_t n_sites, 
 int wld_single_weighted_ld_pair(wld_ctx *c, const uint8_t *a, const uint8_t *b, const float *weights, size_t n_seqs,
                                 float out[3]) {
     if (!a || !b || !weights || !out) return fail(WLD_E_ARG, "null argument");
+    if (c && !c->members.empty()) {
+        // one pair: the first device; the group's loaded set is replaced (as
+        // on a single context), so every member needs a new wld_load
+        for (wld_ctx *m : c->members) m->loaded = false;
+        c = c->members[0];
+    }
     std::vector<uint8_t> buf(2 * n_seqs);
     memcpy(buf.data(), a, n_seqs);
     memcpy(buf.data() + n_seqs, b, n_seqs);

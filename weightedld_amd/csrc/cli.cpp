@@ -7,6 +7,9 @@
 //   --vcf-input PATH   VCF input following WeightedLD.py's handle_vcf (no site
 //                      filter, site index = POS), for BASELINE config 3
 //   --device N         HIP device ordinal (default 0)
+//   --devices G|LIST   shard the pair space over G devices (0..G-1) or a comma
+//                      list of ordinals (repeats allowed) in this one process
+//                      (wld_create_multi); overrides --device
 //   --kernel K         auto | valu | mfma (default auto)
 #include <chrono>
 #include <cinttypes>
@@ -109,6 +112,7 @@ struct Opt {
     bool unweighted = false;
     bool gpu_prepass = false;
     int device = 0;
+    std::vector<int> devices;  // --devices: a multi-device context
     int kernel = WLD_KERNEL_AUTO;
 };
 
@@ -138,6 +142,7 @@ void usage(FILE *f) {
             "Separated Value format\n"
             "        --vcf-input <vcf-input>              (addition) VCF input, WeightedLD.py handle_vcf semantics\n"
             "        --device <device>                    (addition) HIP device ordinal [default: 0]\n"
+            "        --devices <devices>                  (addition) shard over G devices (0..G-1) or a list \"0,1,..\"\n"
             "        --kernel <kernel>                    (addition) auto | valu | mfma [default: auto]\n");
 }
 
@@ -205,6 +210,24 @@ Opt parse(int argc, char **argv) {
             o.gpu_prepass = true;
         } else if (a == "--device") {
             o.device = atoi(need("--device").c_str());
+        } else if (a == "--devices") {
+            const std::string v = need("--devices");
+            o.devices.clear();
+            if (v.find(',') == std::string::npos) {
+                const int g = atoi(v.c_str());
+                if (g < 1) arg_error("Invalid value for '--devices':", v.c_str());
+                for (int k = 0; k < g; ++k) o.devices.push_back(k);
+            } else {
+                size_t at = 0;
+                while (at <= v.size()) {
+                    const size_t e = std::min(v.find(',', at), v.size());
+                    const std::string t = v.substr(at, e - at);
+                    if (t.empty() || t.find_first_not_of("0123456789") != std::string::npos)
+                        arg_error("Invalid value for '--devices':", v.c_str());
+                    o.devices.push_back(atoi(t.c_str()));
+                    at = e + 1;
+                }
+            }
         } else if (a == "--kernel") {
             std::string k = need("--kernel");
             o.kernel = k == "valu" ? WLD_KERNEL_VALU : k == "mfma" ? WLD_KERNEL_MFMA : WLD_KERNEL_AUTO;
@@ -216,6 +239,8 @@ Opt parse(int argc, char **argv) {
     if (o.fasta_input.empty() && o.vcf_input.empty())
         arg_error("The following required arguments were not provided:", "--fasta-input <fasta-input>");
     if (!have_pair) arg_error("The following required arguments were not provided:", "--pair-output <pair-output>");
+    if (o.gpu_prepass && o.devices.size() > 1)
+        arg_error("The argument '--gpu-prepass' cannot be used with", "--devices (the device pre-pass runs on one device)");
     return o;
 }
 
@@ -231,12 +256,15 @@ Opt parse(int argc, char **argv) {
 
 // Rust's `main() -> Result<(), io::Error>` prints "Error: ..." and exits 1;
 // a panic prints the panic message and exits 101.
-[[noreturn]] void die(int st, const char *what) {
+// msg: the failed call's wld_last_error() (thread-local: pass it when the call
+// ran on another thread).
+[[noreturn]] void die(int st, const char *what, const char *msg = nullptr) {
+    if (!msg) msg = wld_last_error();
     if (st == WLD_E_FORMAT || st == WLD_E_ARG) {
-        fprintf(stderr, "thread 'main' panicked at '%s: %s'\n", what, wld_last_error());
+        fprintf(stderr, "thread 'main' panicked at '%s: %s'\n", what, msg);
         quit(101);
     }
-    fprintf(stderr, "Error: %s: %s (%s)\n", what, wld_status_string(st), wld_last_error());
+    fprintf(stderr, "Error: %s: %s (%s)\n", what, wld_status_string(st), msg);
     quit(1);
 }
 
@@ -412,10 +440,15 @@ int main(int argc, char **argv) {
     // read, so that the LD timing below covers the computation only.
     wld_ctx *ctx = nullptr;
     int ctx_st = WLD_OK;
-    std::thread ctx_thread([&] { ctx_st = wld_create(opt.device, &ctx); });
+    std::string ctx_msg;
+    std::thread ctx_thread([&] {
+        ctx_st = opt.devices.empty() ? wld_create(opt.device, &ctx)
+                                     : wld_create_multi(opt.devices.data(), (int)opt.devices.size(), &ctx);
+        if (ctx_st != WLD_OK) ctx_msg = wld_last_error();
+    });
     auto get_ctx = [&]() -> wld_ctx * {
         if (ctx_thread.joinable()) ctx_thread.join();
-        if (ctx_st != WLD_OK) die(ctx_st, "wld_create");
+        if (ctx_st != WLD_OK) die(ctx_st, "wld_create", ctx_msg.c_str());
         if (opt.kernel != WLD_KERNEL_AUTO) {
             int s2 = wld_set_kernel(ctx, opt.kernel);
             if (s2 != WLD_OK) die(s2, "wld_set_kernel");

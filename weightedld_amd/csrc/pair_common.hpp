@@ -61,8 +61,9 @@ __device__ __forceinline__ void ld_epilogue(float total_weight, float PA, float 
 // 1e-12 relative allowance for the f64 evaluation itself.  Exact cells must be
 // >= 0 (normalised quantities in [0, 1]): guaranteed for nonnegative weights,
 // else checked as n^_c >= R.
-__device__ __forceinline__ bool r2_bound_skip(double T, double A, double B, double AB, double R, float thr,
-                                              bool nonneg) {
+// (__host__ as well: tests/cpp/bound_check.cpp runs the same code on the CPU.)
+__host__ __device__ __forceinline__ bool r2_bound_skip(double T, double A, double B, double AB, double R, float thr,
+                                                       bool nonneg) {
     constexpr double u = 0x1p-24;
     const double n10 = A - AB, n01 = B - AB, n00 = (T - A) - n01;
     if (!nonneg && fmin(fmin(AB, n10), fmin(n01, n00)) < R) return false;

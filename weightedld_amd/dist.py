@@ -10,6 +10,8 @@ backend; gloo in the CPU tests).  Because chunk rows DESCEND in the reference's
 triu_index order (lib.rs:623-632), rank 0 concatenates the shards in
 descending rank order.
 """
+import contextlib
+
 import numpy as np
 
 from .api import Context
@@ -96,20 +98,46 @@ class RowGather:
         return torch.cat([gl[g][:, :counts[g]] for g in reversed(range(self.world))], dim=1)
 
 
+class _HostStream:
+    """Stand-in for the context's stream when the step runs on the CPU (the
+    gloo rehearsal of the N>1 path in tests/test_dist.py): ordering is program
+    order, so waits are no-ops."""
+
+    def wait_event(self, event):
+        pass
+
+
+class _HostEvent:
+    def record(self, stream=None):
+        pass
+
+
+def _stream_scope(stream):
+    import torch
+
+    return contextlib.nullcontext() if isinstance(stream, _HostStream) else torch.cuda.stream(stream)
+
+
 class ShardStep:
     """One all_weighted_ld_pairs pass over this rank's chunk range with the
     row gather to rank 0, in one host wait when no rank has rows: the pair
     kernel and the row count are enqueued on the context's stream
     (wld_run_chunks_async), the count all_gather is ordered after them on that
     same stream, and one device-to-host read of the gathered counts completes
-    both.  Returns (rows on this rank, gathered [5, n] rows on rank 0 / None)."""
+    both.  Returns (rows on this rank, gathered [5, n] rows on rank 0 / None).
+
+    ctx is anything with the Context methods the step uses
+    (run_chunks_async, run_wait, rows_copy_device, stream_ptr); with a CPU
+    `device` the step runs in program order on host tensors (gloo)."""
 
     def __init__(self, ctx, rank, world, device, group=None):
         import torch
 
         self.ctx = ctx
         self.gather = RowGather(rank, world, device, group)
-        self.stream = torch.cuda.ExternalStream(ctx.stream_ptr(), device=device)
+        device = torch.device(device)
+        self.stream = (torch.cuda.ExternalStream(ctx.stream_ptr(), device=device) if device.type == "cuda"
+                       else _HostStream())
         self.rows_seen = False  # some rank had rows in the last finished step
 
     def enqueue(self, thr, chunk_begin, chunk_end, kernel_done=None):
@@ -120,7 +148,7 @@ class ShardStep:
         import torch.distributed as dist
 
         g = self.gather
-        with torch.cuda.stream(self.stream):
+        with _stream_scope(self.stream):
             self.ctx.run_chunks_async(thr, chunk_begin, chunk_end, g.cnt.data_ptr())
             if kernel_done is not None:
                 kernel_done.record(self.stream)
@@ -131,7 +159,7 @@ class ShardStep:
         import torch
 
         g = self.gather
-        with torch.cuda.stream(self.stream):
+        with _stream_scope(self.stream):
             counts = g.cnts.tolist()  # the step's one host wait when no rank has rows
         self.rows_seen = max(counts) > 0
         n = self.ctx.run_wait()  # returns at once: the stream is idle
@@ -163,7 +191,8 @@ class PipelinedShardStep:
 
         assert len(ctxs) == 2
         self.steps = [ShardStep(c, rank, world, device, group) for c in ctxs]
-        self.done = [torch.cuda.Event(), torch.cuda.Event()]
+        self.done = ([torch.cuda.Event(), torch.cuda.Event()] if torch.device(device).type == "cuda"
+                     else [_HostEvent(), _HostEvent()])
         self.serialize = serialize_kernels  # False: step i's kernel may start in step i-1's tail
         self.i = 0
         self.pending = None
