@@ -34,8 +34,31 @@ $(PKG)/bin/weighted_ld: $(CSRC)/cli.cpp $(CSRC)/tsv_format.hpp $(PKG)/libweighte
 oracle:
 	$(MAKE) -s -C oracle
 
+# Host code under AddressSanitizer + UndefinedBehaviorSanitizer (CPU only, this
+# container): host.cpp (FASTA/VCF readers, filter, Henikoff) and cli.cpp built
+# with g++ -fsanitize, linked with the unchanged gfx950 device objects; the host
+# tests and the CLI's error paths then run against that build.
+SAN := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g -O1
+SANDIR := build/asan
+DEV_OBJS := $(filter-out $(OBJDIR)/host.o,$(OBJS))
+
+$(SANDIR)/host.o: $(CSRC)/host.cpp $(HDRS)
+	@mkdir -p $(SANDIR)
+	g++ $(SAN) -std=c++17 -fPIC -Wall -Iinclude -I$(CSRC) -c $< -o $@
+
+$(SANDIR)/libweightedld.so: $(DEV_OBJS) $(SANDIR)/host.o
+	g++ -shared $(SAN) -o $@ $^ -L/opt/rocm/lib -lamdhip64 -lpthread -Wl,-rpath,/opt/rocm/lib
+
+$(SANDIR)/weighted_ld: $(CSRC)/cli.cpp $(CSRC)/tsv_format.hpp $(SANDIR)/libweightedld.so include/weightedld.h
+	g++ $(SAN) -std=c++17 -Wall -Iinclude -I$(CSRC) -o $@ $< -L$(SANDIR) -lweightedld -Wl,-rpath,'$$ORIGIN' -lpthread
+
+sanitize: $(SANDIR)/libweightedld.so $(SANDIR)/weighted_ld oracle
+	WLD_TEST_BUILD=$(SANDIR) ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 \
+	LD_PRELOAD="$$(g++ -print-file-name=libasan.so) $$(g++ -print-file-name=libubsan.so)" \
+	python3 -m pytest tests/test_host.py tests/test_tsv_format.py -q -m "not gpu" -p no:cacheprovider
+
 clean:
 	rm -rf build $(PKG)/libweightedld.so $(PKG)/bin
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all clean oracle
+.PHONY: all clean oracle sanitize

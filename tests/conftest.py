@@ -10,6 +10,17 @@ TESTS = os.path.dirname(os.path.abspath(__file__))
 if TESTS not in sys.path:
     sys.path.insert(0, TESTS)
 
+# The library and CLI under test.  `make sanitize` points WLD_TEST_BUILD at
+# build/asan (host code under ASan + UBSan); the product's own loader has no
+# such redirection.
+CLI = os.path.join(REPO, "weightedld_amd", "bin", "weighted_ld")
+_TEST_BUILD = os.environ.get("WLD_TEST_BUILD")
+if _TEST_BUILD:
+    import weightedld_amd
+    from weightedld_amd import _lib
+    _lib.LIB_PATH = weightedld_amd.LIB_PATH = os.path.join(os.path.abspath(_TEST_BUILD), "libweightedld.so")
+    CLI = os.path.join(os.path.abspath(_TEST_BUILD), "weighted_ld")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")

@@ -13,11 +13,10 @@ import numpy as np
 import pytest
 
 import _oracle as O
-from conftest import FIXTURES, REPO
+from conftest import CLI, FIXTURES, REPO
 from test_gpu_parity import compare_rows, synth
 
 pytestmark = pytest.mark.gpu
-CLI = os.path.join(REPO, "weightedld_amd", "bin", "weighted_ld")
 
 
 @pytest.fixture(scope="module")

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import _oracle as O
-from conftest import FIXTURES, REPO, SYNTH
+from conftest import CLI, FIXTURES, REPO, SYNTH
 
 pytestmark = pytest.mark.gpu
 
@@ -54,7 +54,7 @@ def synth(L, N, seed, p_missing=0.1, p_major=0.6, unknown=0.0):
     return codes.astype(np.uint8)
 
 
-def agree(g, r, t=None, tol=TOL, field=None, escape=None):
+def agree(g, r, t=None, tol=TOL, field=None, escape=None, den=None):
     """Per-value parity criterion.  g: GPU f32, r: oracle f32 (lib.rs
     semantics), t: f64 value of the same sums/epilogue (or None).
     Strict: within tol of the reference (relative for |r| > 1, where f32 itself
@@ -65,7 +65,11 @@ def agree(g, r, t=None, tol=TOL, field=None, escape=None):
     amplifies when den is small, on differently rounded sums (the reference's
     8-lane f32 sums, ~N/8 * 2^-24 relative; the GPU's exact sums rounded
     once), so on such pairs each is off the exact value by epilogue noise of
-    the same size.  escape=True extends that to every
+    the same size.  That noise is a few f32 ulps of the 2x2 cell terms over
+    den = |d / D'| (the exact values): with den given, D' may also be within
+    8 * 2^-24 / den of t (the reference itself reaches 4.7 such units on the
+    clustered set of test_gpu_screen, and f32 epilogues on the exactly
+    rounded, unquantised sums 3.1).  escape=True extends the escape to every
     field (only for inputs outside the reference's own 1e-5 accuracy, e.g.
     minor alleles carried by a few low-weight sequences).  Every escape is
     counted, with its |GPU - reference|, in the session's parity report
@@ -83,7 +87,10 @@ def agree(g, r, t=None, tol=TOL, field=None, escape=None):
             escape = field == "d_prime"
         if t is not None and escape:
             t = np.asarray(t, dtype=np.float64)
-            esc = ~strict & np.isfinite(t) & (np.abs(g - t) <= 2.0 * np.abs(r - t) + 1e-6 * np.maximum(1.0, np.abs(t)))
+            allow = 2.0 * np.abs(r - t)
+            if den is not None:
+                allow = np.maximum(allow, 8.0 * 2.0 ** -24 / np.asarray(den, dtype=np.float64))
+            esc = ~strict & np.isfinite(t) & (np.abs(g - t) <= allow + 1e-6 * np.maximum(1.0, np.abs(t)))
             ok |= esc
         fin = strict & ~special
         PARITY.record(field or "value", len(g), float(diff[fin].max()) if fin.any() else 0.0,
@@ -105,9 +112,13 @@ def compare_dense(gpu, ref, truth=None, tol=TOL, mask=None):
     m = rvalid[iu] == 1
     if mask is not None:
         m &= mask
+    den = None
+    if truth is not None:
+        with np.errstate(all="ignore"):
+            den = np.abs(truth[0][iu][m] / truth[1][iu][m])
     for k, (g, r) in enumerate(((d, rd), (dp, rdp), (r2, rr2))):
         t = truth[k][iu][m] if truth is not None else None
-        ok = agree(g[iu][m], r[iu][m], t, tol, ("d", "d_prime", "r2")[k])
+        ok = agree(g[iu][m], r[iu][m], t, tol, ("d", "d_prime", "r2")[k], den=den if k == 1 else None)
         assert ok.all(), ("dsr"[k], np.count_nonzero(~ok), g[iu][m][~ok][:5], r[iu][m][~ok][:5],
                           None if t is None else t[~ok][:5])
 
@@ -142,8 +153,12 @@ def compare_rows(store, ref, thr, tol=TOL, buf=None, w=None, site_map=None):
             fa = np.array([inv[a] if inv else a for a, _ in common])
             fb = np.array([inv[b] if inv else b for _, b in common])
             truth = [td[fa, fb], tdp[fa, fb], tr2[fa, fb]]
+        den = None
+        if truth[0] is not None:
+            with np.errstate(all="ignore"):
+                den = np.abs(truth[0] / truth[1])
         for k, f in enumerate(("d", "d_prime", "r2")):
-            ok = agree(getattr(store, f)[ia], ref[f][ib], truth[k], tol, f)
+            ok = agree(getattr(store, f)[ia], ref[f][ib], truth[k], tol, f, den=den if k == 1 else None)
             assert ok.all(), (f, np.count_nonzero(~ok), getattr(store, f)[ia][~ok][:5], ref[f][ib][~ok][:5],
                               None if truth[k] is None else truth[k][~ok][:5])
     return len(common), len(only_gpu), len(only_ref)
@@ -447,7 +462,6 @@ def test_gpu_vcf_config3_vs_python(W, python_ref):
         assert abs(d - D) <= TOL and abs(dp - Dp) <= TOL and abs(r2 - R2) <= TOL
 
 
-CLI = os.path.join(REPO, "weightedld_amd", "bin", "weighted_ld")
 
 # expected Rust CLI output derived from lib.rs semantics
 CLI_EXPECT = {

@@ -15,13 +15,12 @@ import numpy as np
 import pytest
 
 import _oracle as O
-from conftest import FIXTURES, REPO, SYNTH
+from conftest import CLI, FIXTURES, REPO, SYNTH
 
 import weightedld_amd as W
 from weightedld_amd import _lib
 
 HEADER = os.path.join(REPO, "include", "weightedld.h")
-CLI = os.path.join(REPO, "weightedld_amd", "bin", "weighted_ld")
 
 
 def _gpu_present():

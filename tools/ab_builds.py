@@ -19,7 +19,6 @@ def child(path, config, reps, thr, unweighted=False):
     import torch  # noqa: F401
     import weightedld_amd._lib as L
     L.LIB_PATH = os.path.abspath(path)
-    os.environ["WLD_LIB"] = L.LIB_PATH  # tolerate older builds missing newer symbols
     import bench
     import weightedld_amd as W
     if "," in config:  # custom shape "N,L,thr"

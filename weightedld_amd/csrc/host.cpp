@@ -320,7 +320,7 @@ int wld_read_fasta(const char *path, wld_siteset **out) {
 
 int wld_siteset_from_buffer(const uint8_t *site_major, size_t n_sites, size_t n_seqs,
                             const uint64_t *site_map, wld_siteset **out) {
-    if (!out || (!site_major && n_sites * n_seqs)) return fail(WLD_E_ARG, "wld_siteset_from_buffer: null pointer");
+    if (!out || (!site_major && n_sites && n_seqs)) return fail(WLD_E_ARG, "wld_siteset_from_buffer: null pointer");
     auto *ss = new wld_siteset;
     SiteSet &s = ss->s;
     s.n_sites = n_sites;
