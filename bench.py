@@ -137,6 +137,8 @@ def main():
                     help="one step at a time (N=1: no second context; N>1: one ShardStep at a time)")
     ap.add_argument("--no-screen", action="store_true",
                     help="every tile with every weight-digit plane (WLD_OPT_SCREEN 0; same rows)")
+    ap.add_argument("--wide-screen", action="store_true",
+                    help="the i8 screen on 64x128 tiles (WLD_OPT_WIDE_SCREEN 1; same rows)")
     ap.add_argument("--no-prefilter", action="store_true",
                     help="every pair through the f32 epilogue (WLD_OPT_PREFILTER 0, implies --no-screen; same rows)")
     args = ap.parse_args()
@@ -204,6 +206,8 @@ def main():
             c.set_option("screen", 0)
         if args.no_prefilter:
             c.set_option("prefilter", 0)
+        if args.wide_screen:
+            c.set_option("wide_screen", 1)
         c.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
         return c
 
@@ -340,7 +344,8 @@ def main():
         achieved = alg_ops / (dom_ms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak,
                 "work": "algorithmic: 8*N int8 ops per site pair (4 masked weighted sums)",
-                "kernel": "pair_mfma_kernel<screen,1 plane>" if screened else "pair_mfma_kernel<%d planes>" % planes,
+                "kernel": ("pair_screen_kernel (64x128 tiles, 1 plane)" if args.wide_screen else
+                           "pair_mfma_kernel<screen,1 plane>") if screened else "pair_mfma_kernel<%d planes>" % planes,
                 "kernel_ms": dom_ms}
         # what the matrix cores executed: P digit planes x 8 N per pair
         ex_planes = 1 if screened else planes

@@ -132,7 +132,9 @@ void wld_destroy(wld_ctx *ctx);
 
 /* Kernel selection.  AUTO (default): the exact-integer MFMA kernel when the
  * weights are finite, their dynamic range fits its fixed-point weight planes
- * (min nonzero |w| >= 2^-10 max |w|) and n_seqs <= 5,592,320 (int32 sums),
+ * (3 digit planes, 23-bit fixed point, when min |w| >= 2^-4 max |w|; 4 planes,
+ * 31-bit, when min |w| >= 2^-12 max |w| and n_seqs <= 65,024: every weight
+ * within 2^-19 relative) and n_seqs <= 5,592,320 (int32 sums),
  * else the exact-product f32 kernel (WLD_KERNEL_VALU: f32-input MFMA for
  * finite weights, a VALU loop otherwise).  An explicit WLD_KERNEL_MFMA with
  * non-finite or all-zero weights, or more sequences, fails with WLD_E_ARG at
@@ -165,7 +167,10 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *                      MFMA; 1: a VALU fmaf loop (same sums, same order).
  *   WLD_OPT_STAGING_ROWS   initial staging capacity in rows (default 2^25;
  *                      grown on overflow by a re-run).
- *   WLD_OPT_HOST_BATCH_PAIRS  pairs per batch of wld_run_host (default 2^31). */
+ *   WLD_OPT_HOST_BATCH_PAIRS  pairs per batch of wld_run_host (default 2^31).
+ *   WLD_OPT_WIDE_SCREEN 0 (default): the one-plane i8 screen on 64x64 tiles;
+ *                      1: on 64x128 tiles (two 64x64 tiles per workgroup,
+ *                      f32 bound only; measured no faster). */
 #define WLD_OPT_PREFILTER 1
 #define WLD_OPT_SCREEN 2
 #define WLD_OPT_TILE_ORDER 3
@@ -174,6 +179,7 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
 #define WLD_OPT_VALU_PLAIN 6
 #define WLD_OPT_STAGING_ROWS 7
 #define WLD_OPT_HOST_BATCH_PAIRS 8
+#define WLD_OPT_WIDE_SCREEN 9
 int wld_set_option(wld_ctx *ctx, int option, int64_t value);
 int wld_get_option(wld_ctx *ctx, int option, int64_t *value);
 

@@ -125,13 +125,15 @@ def check_exact_model(ctx, buf, w, dense=None):
     return int(m.sum())
 
 
-def _run(ctx, thr, prefilter, screen):
+def _run(ctx, thr, prefilter, screen, wide=0):
     ctx.set_option("prefilter", prefilter)
     ctx.set_option("screen", screen)
+    ctx.set_option("wide_screen", wide)
     ctx.run(thr)
     rows, st = ctx.rows(), ctx.stats()
     ctx.set_option("prefilter", 1)
     ctx.set_option("screen", 1)
+    ctx.set_option("wide_screen", 0)
     return rows, st
 
 
@@ -212,9 +214,14 @@ def test_prefilter_and_screen_never_change_rows(W, ctxs, case):
     for thr in thrs:
         ref, _ = _run(ctx, thr, 0, 0)       # every pair through the f32 epilogue
         pre, _ = _run(ctx, thr, 1, 0)       # prefilter only
-        scr, st = _run(ctx, thr, 1, 1)      # screen + prefilter (the default)
+        nar, stn = _run(ctx, thr, 1, 1)     # screen + prefilter (the default; 64x64 screen tiles)
+        scr, st = _run(ctx, thr, 1, 1, 1)   # the i8 screen on 64x128 tiles
         _same_rows(pre, ref)
         _same_rows(scr, ref)
+        _same_rows(nar, ref)
+        # the 64x128 screen decides in f32 only (a pair it cannot decide makes
+        # its tile a candidate); the 64x64 screen falls back to f64 per pair
+        assert stn["candidate_tiles"] <= st["candidate_tiles"], (thr, stn["candidate_tiles"], st["candidate_tiles"])
         _rows_equal_dense(scr, dense, thr, L)
         screened_any |= st["screened"] == 1
         assert st["candidate_tiles"] <= st["tiles"]

@@ -24,12 +24,12 @@ def harness(tmp_path_factory):
                     "-I", os.path.join(REPO, "include"), "-I", os.path.join(REPO, "weightedld_amd", "csrc"),
                     "-x", "hip", os.path.join(REPO, "tests", "cpp", "bound_check.cpp"), "-o", exe], check=True)
 
-    def run(T, A, B, AB, R, thr, nonneg=True):
+    def run(T, A, B, AB, R, thr, nonneg=True, f32=False):
         n = len(T)
         rec = np.stack([np.asarray(x, np.float64) * np.ones(n) for x in (T, A, B, AB, R, thr, float(nonneg))], 1)
         d = tmp_path_factory.mktemp("io")
         rec.tofile(str(d / "in.bin"))
-        subprocess.run([exe, str(d / "in.bin"), str(d / "out.bin")], check=True)
+        subprocess.run([exe, str(d / "in.bin"), str(d / "out.bin")] + (["f32"] if f32 else []), check=True)
         return np.fromfile(str(d / "out.bin"), dtype=np.uint8).astype(bool)
     return run
 
@@ -49,7 +49,7 @@ def f32_r2(T, SA, SB, SAB):
         return d * d / (PA * Pa * PB * Pb)
 
 
-def near_threshold_tables(rng, n, thr, scale=2.0 ** 34):
+def near_threshold_tables(rng, n, thr, scale=2.0 ** 34, window=3e-3):
     """Integer 2x2 tables with rare cells and exact r2 just below thr."""
     e = 10.0 ** rng.uniform(-6, -1, (3, n))
     n11, n10, n01 = np.floor(e[0] * scale), np.floor(e[1] * scale), np.floor(e[2] * scale)
@@ -57,7 +57,7 @@ def near_threshold_tables(rng, n, thr, scale=2.0 ** 34):
     T, A, B, AB = n11 + n10 + n01 + n00, n11 + n10, n11 + n01, n11
     num, den = A * B - AB * T, A * (T - A) * B * (T - B)
     r2 = num * num / den
-    sel = (r2 < thr) & (r2 > thr * (1 - 3e-3))
+    sel = (r2 < thr) & (r2 > thr * (1 - window))
     return T[sel], A[sel], B[sel], AB[sel]
 
 
@@ -110,4 +110,65 @@ def test_bound_sound_with_screen_residuals(harness, nonneg):
             assert (c >= 0).all()
         viol += int((skip & passes).sum())
         skipped += int(skip.sum())
+    assert viol == 0 and skipped > 0
+
+
+def screen_tables(rng, n, scale, rare):
+    """Nonnegative integer cells (top-plane sums, |T| <= 2^22) and screen
+    residuals: approximate cells within R in total."""
+    c = rng.random((4, n)) + 0.02
+    if rare:
+        eps = 10.0 ** rng.uniform(-4, -1, n)
+        c[0] *= eps
+        c[1] *= eps
+    c = np.floor(c / c.sum(0) * scale)
+    return c
+
+
+@pytest.mark.parametrize("rare", [False, True])
+def test_screen_f32_bound_sound_and_tight(harness, rare):
+    # r2_screen_skip_f32 (the one-plane screen's per-pair test): never skips a
+    # pair whose exact sums pass r2 > thr through the f32 epilogue, for any
+    # approximation within R; and it skips nearly every pair the f64 test
+    # skips (the screen kernel runs the f64 test on the pairs it leaves)
+    rng = np.random.default_rng(23 + rare)
+    viol = skipped = skipped64 = both = 0
+    for it in range(24):
+        n = 200_000
+        scale = float(2 ** rng.integers(10, 22))
+        c = screen_tables(rng, n, scale, rare)
+        T, A, B, AB = c.sum(0), c[0] + c[1], c[0] + c[2], c[0]
+        thr = float(np.float32(rng.choice([0.001, 0.01, 0.05, 0.2, 0.6])))
+        R = rng.choice([0.0, 1e-4, 1e-3, 1e-2]) * scale * rng.random()
+        e = rng.random((4, n)) * rng.choice([-1.0, 1.0], (4, n))
+        e = np.trunc(e / np.maximum(np.abs(e).sum(0), 1e-12) * R * rng.random(n))
+        h = c + e
+        # near-threshold pairs: scale the off-diagonal so exact r2 sits at thr
+        args = (h.sum(0), h[0] + h[1], h[0] + h[2], h[0], R, thr)
+        s32 = harness(*args, f32=True)
+        s64 = harness(*args)
+        with np.errstate(invalid="ignore"):
+            passes = f32_r2(T, A, B, AB) > np.float32(thr)
+        viol += int((s32 & passes).sum())
+        skipped += int(s32.sum())
+        skipped64 += int(s64.sum())
+        both += int((s32 & s64).sum())
+    assert viol == 0
+    assert skipped > 0
+    # ordinary tables: the f32 form alone decides nearly all of them; with
+    # marginals below 2^-12 of T it declines (the kernel's f64 test decides)
+    assert skipped >= (0.6 if rare else 0.97) * skipped64, (skipped, skipped64)
+
+
+@pytest.mark.parametrize("thr", [0.05, 0.1, 0.3])
+def test_screen_f32_bound_sound_near_threshold(harness, thr):
+    rng = np.random.default_rng(int(thr * 1000))
+    viol = skipped = 0
+    for _ in range(10):
+        T, A, B, AB = near_threshold_tables(rng, 1_000_000, thr, scale=2.0 ** 22, window=0.05)
+        passes = f32_r2(T, A, B, AB) > np.float32(thr)
+        for R in (0.0, 1.0, 17.5):
+            skip = harness(T, A, B, AB, R, thr, f32=True)
+            viol += int((skip & passes).sum())
+            skipped += int(skip.sum())
     assert viol == 0 and skipped > 0

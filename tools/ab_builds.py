@@ -33,6 +33,9 @@ def child(path, config, reps, thr, unweighted=False):
     if os.environ.get("WLD_AB_WEIGHTS") == "2pl":  # two active digit planes (1 and 2)
         w = np.where(np.random.default_rng(3).random(N) < 0.5, 1.0, 3 / 256).astype(np.float32)
     ctx = W.Context(0, W.KERNEL_MFMA)
+    for kv in filter(None, os.environ.get("WLD_AB_OPTS", "").split(";")):  # name=path@WLD_AB_OPTS=opt=v;opt=v
+        k, v = kv.split("=", 1)
+        ctx.set_option(k, int(v))
     ctx.load(buf, w)
     ctx.run(thr)
     import ctypes

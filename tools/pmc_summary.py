@@ -7,28 +7,27 @@ import glob
 import sys
 
 for f in sorted(glob.glob(sys.argv[1] + "/**/*_counter_collection.csv", recursive=True)):
-    agg = collections.defaultdict(list)
-    dur = {}
-    for r in csv.DictReader(open(f)):
-        if "pair_mfma" not in r["Kernel_Name"]:
-            continue
-        agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-        dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-    if not agg:
+  by_kernel = collections.defaultdict(lambda: (collections.defaultdict(list), {}))
+  for r in csv.DictReader(open(f)):
+    if "pair_mfma" not in r["Kernel_Name"] and "pair_screen" not in r["Kernel_Name"]:
         continue
-    m = {k: sum(v) / len(v) for k, v in agg.items()}
-    d = sum(dur.values()) / len(dur)
-    out = {"file": f.split("/")[-1], "ms": round(d * 1e3, 3)}
-    if "GRBM_GUI_ACTIVE" in m:
-        cyc = m["GRBM_GUI_ACTIVE"] / 8
-        out["ghz"] = round(cyc / d / 1e9, 3)
-        if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
-            out["mfma_busy"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / cyc, 3)
-    if "SQ_WAVE_CYCLES" in m:
-        for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+    agg, dur = by_kernel[r["Kernel_Name"].split("(")[0]]
+    agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+  for kname, (agg, dur) in sorted(by_kernel.items()):
+        m = {k: sum(v) / len(v) for k, v in agg.items()}
+        d = sum(dur.values()) / len(dur)
+        out = {"file": f.split("/")[-1], "kernel": kname.replace("void wld::", ""), "dispatches": len(dur), "ms": round(d * 1e3, 3)}
+        if "GRBM_GUI_ACTIVE" in m:
+            cyc = m["GRBM_GUI_ACTIVE"] / 8
+            out["ghz"] = round(cyc / d / 1e9, 3)
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+                out["mfma_busy"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / cyc, 3)
+        if "SQ_WAVE_CYCLES" in m:
+            for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if k in m:
+                    out[k] = round(m[k] / m["SQ_WAVE_CYCLES"], 3)
+        for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_MISC", "FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"):
             if k in m:
-                out[k] = round(m[k] / m["SQ_WAVE_CYCLES"], 3)
-    for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"):
-        if k in m:
-            out[k] = m[k]
-    print(out)
+                out[k] = m[k]
+        print(out)

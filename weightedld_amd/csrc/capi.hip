@@ -102,6 +102,7 @@ struct wld_ctx {
     int kernel_pref = WLD_KERNEL_AUTO;
     // wld_set_option (include/weightedld.h)
     bool opt_prefilter = true, opt_screen = true, opt_tile_rows = false, opt_all_planes = false;
+    bool opt_wide_screen = false;  // WLD_OPT_WIDE_SCREEN: the i8 screen on 64x128 tiles (A/B: not faster)
     bool opt_site_major = false, opt_valu_plain = false;
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
 
@@ -122,12 +123,12 @@ struct wld_ctx {
     MfmaWeightStats wst{7, 1, {0, 0, 0}};  // digit-plane statistics of the load (MFMA)
 
     // run state
-    DevBuf tiles, cand, seg_cnt, seg_off, chunk_total, chunk_base, counters;
+    DevBuf tiles, wtiles, cand, seg_cnt, seg_off, chunk_total, chunk_base, counters;
     DevBuf st_a, st_b, st_d, st_dp, st_r2;
     DevBuf out_a, out_b, out_d, out_dp, out_r2;
     uint64_t st_capacity = 0;
     uint32_t tiles_lb = ~0u, tiles_le = ~0u;  // linear chunk range the tile list covers
-    uint32_t n_tiles = 0;
+    uint32_t n_tiles = 0, n_wtiles = 0;  // wtiles: the screen's wide tiles (kWideSecond)
     bool have_rows = false;
     bool screened = false;  // the last pass ran the one-plane screen
     uint64_t rows = 0;
@@ -137,7 +138,7 @@ struct wld_ctx {
         for (wld_ctx *m : members) delete m;
         if (!members.empty()) return;
         (void)hipSetDevice(device);
-        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &tiles, &cand,
+        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &tiles, &wtiles, &cand,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
@@ -248,7 +249,9 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
         if (c->use_frag) {
             // two copies: the selector-coded one (A operands, and B in the
             // v_perm build) and the 0/1/2-coded one the B side reads raw
-            WLD_TRY(ensure(c->frag, 2 * c->LP * c->NP));
+            // + 4 KB: the wide screen's copy of a partial last group reads past
+            // the last block's stages (into LDS stages it never reads)
+            WLD_TRY(ensure(c->frag, 2 * c->LP * c->NP + 4096));
             launch_frag(ptr<uint8_t>(c->codes), c->LP, c->NP, ptr<uint8_t>(c->frag), c->stream);
             HIP_TRY(hipGetLastError());
         }
@@ -340,17 +343,21 @@ void rows_to_linear(uint32_t n, uint32_t rb, uint32_t re, uint32_t &lb, uint32_t
 // the ~64 tiles resident on its 32 CUs read 8 A and 8 B tile columns (2 MB at
 // C4) that fit its 4 MB L2.  Short queues are padded with kNoTile entries,
 // which the pair kernels skip.
-std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t) {
+// (ta_mask: 0x7FFF for wide screen tiles, whose bit 31 is kWideSecond)
+std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t, uint32_t ta_mask = 0xFFFFu) {
     constexpr uint32_t kX = 8, kS = 8;
     std::vector<std::vector<uint32_t>> blocks;
     uint64_t last = ~0ull;
     std::vector<uint32_t> sorted(t);
-    std::sort(sorted.begin(), sorted.end(), [](uint32_t x, uint32_t y) {
-        const uint32_t bx = ((x >> 16) / kS) << 16 | ((x & 0xFFFFu) / kS), by = ((y >> 16) / kS) << 16 | ((y & 0xFFFFu) / kS);
-        return bx != by ? bx < by : x < y;
+    auto block_of = [ta_mask](uint32_t v) {
+        return (((v >> 16) & ta_mask) / kS) << 16 | ((v & 0xFFFFu) / kS);
+    };
+    std::sort(sorted.begin(), sorted.end(), [&](uint32_t x, uint32_t y) {
+        const uint32_t bx = block_of(x), by = block_of(y);
+        return bx != by ? bx < by : (x & ~kWideSecond) < (y & ~kWideSecond);
     });
     for (uint32_t v : sorted) {
-        const uint64_t key = ((v >> 16) / kS) << 16 | ((v & 0xFFFFu) / kS);
+        const uint64_t key = block_of(v);
         if (key != last) blocks.emplace_back(), last = key;
         blocks.back().push_back(v);
     }
@@ -385,9 +392,24 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
                 t.push_back((ta << 16) | tb);
     }
     std::sort(t.begin(), t.end());
+    // the screen's wide tiles: (ta, tb) with (ta, tb + 1) when both are in the
+    // list (rows of the list are runs of consecutive tb)
+    std::vector<uint32_t> w;
+    if (T_used < 32768) {
+        for (size_t i = 0; i < t.size(); ++i) {
+            const bool pair = i + 1 < t.size() && t[i + 1] == t[i] + 1;
+            w.push_back(pair ? t[i] | kWideSecond : t[i]);
+            i += pair;
+        }
+    }
     // only with many rounds of resident tiles: whole super-blocks per XCD
     // leave up to one super-block of imbalance (C2's 528 tiles: +14%)
+    if (!c->opt_tile_rows && w.size() >= 4096) w = xcd_order(w, 0x7FFFu);
     if (!c->opt_tile_rows && t.size() >= 4096 && T_used < 65535) t = xcd_order(t);
+    c->n_wtiles = (uint32_t)w.size();
+    WLD_TRY(ensure(c->wtiles, std::max<size_t>(w.size(), 1) * sizeof(uint32_t)));
+    if (!w.empty())
+        HIP_TRY(hipMemcpyAsync(c->wtiles.p, w.data(), w.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     c->n_tiles = (uint32_t)t.size();
     WLD_TRY(ensure(c->tiles, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));
     WLD_TRY(ensure(c->cand, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));  // screen candidates
@@ -428,6 +450,8 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         m.wplanes = ptr<int8_t>(c->planes);
         m.tiles = ptr<uint32_t>(c->tiles);
         m.n_tiles = c->n_tiles;
+        m.wtiles = c->opt_wide_screen && c->n_wtiles ? ptr<uint32_t>(c->wtiles) : nullptr;
+        m.n_wtiles = c->n_wtiles;
         m.L = (uint32_t)c->L;
         m.NP = (uint32_t)c->NP;
         m.n_chunk_rows = n;
@@ -555,6 +579,7 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
             if (value < 1) return fail(WLD_E_ARG, "WLD_OPT_HOST_BATCH_PAIRS must be >= 1");
             c->opt_host_batch_pairs = (uint64_t)value;
             break;
+        case WLD_OPT_WIDE_SCREEN: c->opt_wide_screen = value != 0; break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }
     return WLD_OK;
@@ -571,6 +596,7 @@ int wld_get_option(wld_ctx *c, int option, int64_t *value) {
         case WLD_OPT_VALU_PLAIN: *value = c->opt_valu_plain; break;
         case WLD_OPT_STAGING_ROWS: *value = (int64_t)c->opt_staging_rows; break;
         case WLD_OPT_HOST_BATCH_PAIRS: *value = (int64_t)c->opt_host_batch_pairs; break;
+        case WLD_OPT_WIDE_SCREEN: *value = c->opt_wide_screen; break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }
     return WLD_OK;

@@ -14,6 +14,9 @@ constexpr int kSeqPad = 64;      // sequences padded to a multiple of this
 constexpr int kTilesPerChunk = kChunk / kTile;
 // an empty slot of a reordered tile list (never a real tile: T_used < 65535 there)
 constexpr uint32_t kNoTile = 0xFFFFFFFFu;
+// wide screen tiles (ta << 16 | tb, ta < 2^15): the 64x64 tile (ta, tb + 1)
+// is part of the entry too
+constexpr uint32_t kWideSecond = 0x80000000u;
 
 // Code byte per (site, sequence): bit0 = sequence is major or minor at the site
 // ("in" the pair mask, lib.rs:435), bit1 = sequence is major (lib.rs:430,432).
@@ -84,7 +87,8 @@ struct MfmaLaunch {
     const uint8_t *frag_b;  // fragment-major 0/1/2-coded copy (B operands)
     const int8_t *wplanes;
     const uint32_t *tiles;
-    uint32_t n_tiles, L, NP, n_chunk_rows;
+    const uint32_t *wtiles;  // the same tiles paired along b (kWideSecond), for the screen; or null
+    uint32_t n_tiles, n_wtiles, L, NP, n_chunk_rows;
     float thr;
     int shift;
     unsigned plane_mask;

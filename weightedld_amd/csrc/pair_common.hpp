@@ -78,6 +78,41 @@ __host__ __device__ __forceinline__ bool r2_bound_skip(double T, double A, doubl
     return lhs <= rhs;
 }
 
+// The screen's per-pair test in f32 (about a third of r2_bound_skip's f64
+// cost; the one-plane screen kernel is VALU-issue bound).
+// Sound under: nonnegative weights; T, A, B, AB integers of magnitude
+// <= 2^22 (exact in f32, and so are T - A, T - B); R >= the L1 cell residual
+// (rounded up to f32).  It implies r2_bound_skip's inequality:
+//   * every approximate sum and cell is <= Tb = T + 2R (exact cells >= 0 sum
+//     to at most T + R, each within R), so R cmax <= R Tb, Tub <= Tb;
+//   * |fl(fl(A B) - fl(AB T)) - |A B - AB T|| <= 4.02u Tb^2, so
+//     E = R Tb + R^2 + 2^-19 Tb^2 (2^-19 = 32u >= 24u + 2^-40 + 4.02u, the
+//     slack covering E's own rounding) gives nub <= fl(num + E)(1 + 2u);
+//   * m_i = fl(x_i - R) <= (x_i - R)(1 + u), so the f32 product of the four
+//     marginals is <= their exact product times (1 + u)^7;
+//   * mlo >= 2^-12 Tb bounds r2_bound_skip's 28u Tub / mlo term by 6.84e-3,
+//     and c = 1 - 2^-7 covers it with every f32 rounding above (16u).
+// No skip (the tile becomes a candidate) whenever it cannot decide.  Finite
+// inputs only (integer sums).  tests/test_r2_bound.py checks it on the host.
+// Returned as a violation margin: the pair is skipped iff it is <= 0 (both
+// terms are differences of f32 values, whose rounded sign is exact).
+// thr_c = thr * (1 - 2^-7) in f32.
+__host__ __device__ __forceinline__ float r2_screen_violation(float T, float A, float B, float AB, float R,
+                                                              float thr_c) {
+    const float Tb = (T + 2.0f * R) * (1.0f + 0x1p-20f);
+    const float m1 = A - R, m2 = (T - A) - R, m3 = B - R, m4 = (T - B) - R;
+    const float mlo = fminf(fminf(m1, m2), fminf(m3, m4));
+    const float num = fabsf(A * B - AB * T);
+    const float E = R * Tb + R * R + 0x1p-19f * (Tb * Tb);
+    const float nub = num + E;
+    return fmaxf(nub * nub - thr_c * ((m1 * m2) * (m3 * m4)), 0x1p-12f * Tb - mlo);
+}
+__host__ __device__ __forceinline__ bool r2_screen_skip_f32(float T, float A, float B, float AB, float R, float thr) {
+    return r2_screen_violation(T, A, B, AB, R, thr * (1.0f - 0x1p-7f)) <= 0.0f;
+}
+// largest |top-plane sum| for which the screen may use r2_screen_skip_f32
+constexpr uint32_t kScreenF32MaxNP = 32768;  // 128 NP <= 2^22
+
 __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
