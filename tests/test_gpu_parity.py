@@ -571,7 +571,7 @@ def test_mfma_lds_pipeline_race_screen(W):
     for _ in range(4):
         n = ctx.run(0.001)
         assert n == n_ref
-        assert ctx.stats()["screened"] == 1
+        assert ctx.stats()["screened"] in (1, 2)
         got = wdist.pack_rows_device(ctx, n, dev)
         assert torch.equal(got, ref)
 

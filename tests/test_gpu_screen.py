@@ -125,15 +125,17 @@ def check_exact_model(ctx, buf, w, dense=None):
     return int(m.sum())
 
 
-def _run(ctx, thr, prefilter, screen, wide=0):
+def _run(ctx, thr, prefilter, screen, wide=0, fp4=0):
     ctx.set_option("prefilter", prefilter)
     ctx.set_option("screen", screen)
     ctx.set_option("wide_screen", wide)
+    ctx.set_option("screen_fp4", fp4)
     ctx.run(thr)
     rows, st = ctx.rows(), ctx.stats()
     ctx.set_option("prefilter", 1)
     ctx.set_option("screen", 1)
     ctx.set_option("wide_screen", 0)
+    ctx.set_option("screen_fp4", 0)
     return rows, st
 
 
@@ -197,6 +199,7 @@ def test_prefilter_and_screen_never_change_rows(W, ctxs, case):
         neg = rng.random(600) < 0.1
         w[neg] = -(0.1 + 0.2 * rng.random(int(neg.sum()))).astype(np.float32)
         thrs = [0.01, 0.05, 0.2]
+    ctx.set_option("screen_fp4", 2)  # build the fp4 screen's operands at load
     ctx.load(buf, w)
     assert ctx.stats()["kernel"] == W.KERNEL_MFMA
     # thresholds on the pairs' own r2 values: rows sitting exactly on the cut
@@ -214,11 +217,19 @@ def test_prefilter_and_screen_never_change_rows(W, ctxs, case):
     for thr in thrs:
         ref, _ = _run(ctx, thr, 0, 0)       # every pair through the f32 epilogue
         pre, _ = _run(ctx, thr, 1, 0)       # prefilter only
-        nar, stn = _run(ctx, thr, 1, 1)     # screen + prefilter (the default; 64x64 screen tiles)
-        scr, st = _run(ctx, thr, 1, 1, 1)   # the i8 screen on 64x128 tiles
+        nar, stn = _run(ctx, thr, 1, 1, 0, 0)  # the i8 screen on 64x64 tiles
+        scr, st = _run(ctx, thr, 1, 1, 1, 0)   # the i8 screen on 64x128 tiles
+        f4, st4 = _run(ctx, thr, 1, 1, 0, 1)   # the fp4 screen
+        dft, _ = _run(ctx, thr, 1, 1, 0, 2)    # fp4 auto
         _same_rows(pre, ref)
         _same_rows(scr, ref)
         _same_rows(nar, ref)
+        _same_rows(f4, ref)
+        _same_rows(dft, ref)
+        if st4["screened"]:
+            # fp4 operands exist only for nonnegative weights
+            assert st4["screened"] == (1 if case == "mixed_sign" else 2), st4
+            assert st4["candidate_tiles"] <= st4["tiles"]
         # the 64x128 screen decides in f32 only (a pair it cannot decide makes
         # its tile a candidate); the 64x64 screen falls back to f64 per pair
         assert stn["candidate_tiles"] <= st["candidate_tiles"], (thr, stn["candidate_tiles"], st["candidate_tiles"])
@@ -253,6 +264,36 @@ def test_prefilter_and_screen_never_change_rows(W, ctxs, case):
                   escape=True)
 
 
+def test_fp4_screen_auto_policy(W, ctxs):
+    # BASELINE-style random data: at 0.05 the fp4 screen rejects (nearly) every
+    # tile; at 0.002 its coarser bound leaves most tiles, so auto falls back to
+    # the i8 screen for that and every lower threshold — rows identical throughout
+    ctx = _ctx(ctxs, "mfma")
+    buf = synth(2500, 1500, 21)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ctx.set_option("screen_fp4", 2)
+    ctx.load(buf, w)
+    st = ctx.stats()
+    ctx.run(0.05)
+    st = ctx.stats()
+    assert st["screened"] == 2 and st["candidate_tiles"] <= st["tiles"] // 100, st
+    ref = O.all_pairs(buf, w, np.float32(0.05))
+    assert len(ctx.rows()) == len(ref["r2"])
+    seen = []
+    for thr in (0.002, 0.002, 0.001, 0.05):
+        ctx.run(thr)
+        st = ctx.stats()
+        seen.append((thr, st["screened"], st["candidate_tiles"], st["tiles"]))
+        rows = ctx.rows()
+        i8, _ = _run(ctx, thr, 1, 1, 0, 0)
+        ctx.set_option("screen_fp4", 2)
+        _same_rows(rows, i8)
+    # first run at 0.002: fp4 with many candidates; then i8 at <= 0.002; fp4 again at 0.05
+    assert seen[0][1] == 2 and seen[0][2] * 10 > seen[0][3], seen
+    assert seen[1][1] == 1 and seen[2][1] == 1 and seen[3][1] == 2, seen
+    ctx.set_option("screen_fp4", 0)
+
+
 def test_screen_rejects_random_tiles(W, ctxs):
     # On BASELINE-style random data at 0.05 no pair comes near the cut: the
     # screen must reject (nearly) every tile, so the all-planes launch is tiny.
@@ -263,7 +304,7 @@ def test_screen_rejects_random_tiles(W, ctxs):
     assert ctx.stats()["mfma_planes"] == 3
     n = ctx.run(0.05)
     st = ctx.stats()
-    assert st["screened"] == 1 and st["pair_kernel_launches"] == 2
+    assert st["screened"] in (1, 2) and st["pair_kernel_launches"] == 2
     assert st["candidate_tiles"] <= st["tiles"] // 100, st
     ref = O.all_pairs(buf, w, np.float32(0.05))
     assert n == len(ref["r2"])

@@ -4,7 +4,7 @@ tag=${1:-r02p2}
 out=gpurun_out/$tag
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT"
-for v in "wide:" "narrow:--no-wide-screen"; do
+for v in ${VARIANTS:-"i8:" "fp4:--fp4-screen"}; do
   n=${v%%:*}; a=${v#*:}
   timeout -k 10 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
     --output-format csv -d $out/pmc_$n/sq -o sq -- python3 bench.py --no-pipeline --steps 10 --warmup 3 --no-cpu-baseline $a > $out/sq_$n.log 2>&1 || exit 1

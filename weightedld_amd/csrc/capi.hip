@@ -103,13 +103,18 @@ struct wld_ctx {
     // wld_set_option (include/weightedld.h)
     bool opt_prefilter = true, opt_screen = true, opt_tile_rows = false, opt_all_planes = false;
     bool opt_wide_screen = false;  // WLD_OPT_WIDE_SCREEN: the i8 screen on 64x128 tiles (A/B: not faster)
+    int opt_screen_fp4 = 0;        // WLD_OPT_SCREEN_FP4: 0 never (default: measured no faster), 1 always, 2 auto
+    bool have_fp4 = false;         // frag4 holds this load's fp4 screen operands
+    float R4 = 0.0f;               // their weights' residual bound
+    float fp4_bad_thr = -1.0f;     // auto: the largest threshold at which the fp4 screen left > 10% candidates
+    bool fp4_used = false;         // the last pass screened on fp4
     bool opt_site_major = false, opt_valu_plain = false;
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
 
     // loaded SiteSet
     bool loaded = false;
     size_t L = 0, N = 0, LP = 0, NP = 0;
-    DevBuf raw, wraw, codes, w_pad, wstats, site_ok, site_map, planes, frag;
+    DevBuf raw, wraw, codes, w_pad, wstats, site_ok, site_map, planes, frag, frag4, w4;
     DevBuf keep, htab, htab_kept, site_index;  // device pre-pass (prepass.hip)
     std::vector<uint64_t> kept_map;  // parent indices of the kept sites (wld_site_map_copy)
     bool prepass_loaded = false;
@@ -138,7 +143,7 @@ struct wld_ctx {
         for (wld_ctx *m : members) delete m;
         if (!members.empty()) return;
         (void)hipSetDevice(device);
-        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &tiles, &wtiles, &cand,
+        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &frag4, &w4, &tiles, &wtiles, &cand,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
@@ -254,6 +259,25 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
             WLD_TRY(ensure(c->frag, 2 * c->LP * c->NP + 4096));
             launch_frag(ptr<uint8_t>(c->codes), c->LP, c->NP, ptr<uint8_t>(c->frag), c->stream);
             HIP_TRY(hipGetLastError());
+        }
+        // the fp4 screen's operands (screen_fp4.hip): nonnegative weights only
+        c->have_fp4 = false;
+        c->fp4_bad_thr = -1.0f;
+        if (c->use_frag && c->opt_screen_fp4 && c->NP <= kFp4MaxNP && c->L > 0) {
+            std::vector<float> hw(c->NP);
+            HIP_TRY(hipMemcpyAsync(hw.data(), c->w_pad.p, c->NP * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            std::vector<uint8_t> packed;
+            if (fp4_weights(hw.data(), N, c->NP, packed, &c->R4) == 0) {
+                WLD_TRY(ensure(c->w4, packed.size()));
+                HIP_TRY(hipMemcpyAsync(c->w4.p, packed.data(), packed.size(), hipMemcpyHostToDevice, c->stream));
+                WLD_TRY(ensure(c->frag4, screen_fp4_frag_bytes(c->LP, c->NP)));
+                launch_frag4(ptr<uint8_t>(c->codes), ptr<uint8_t>(c->w4), c->LP, c->NP, ptr<uint8_t>(c->frag4),
+                             c->stream);
+                HIP_TRY(hipGetLastError());
+                HIP_TRY(hipStreamSynchronize(c->stream));  // packed is freed on return
+                c->have_fp4 = true;
+            }
         }
     }
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
@@ -454,6 +478,13 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         m.n_wtiles = c->n_wtiles;
         m.L = (uint32_t)c->L;
         m.NP = (uint32_t)c->NP;
+        m.LP = (uint32_t)c->LP;
+        // the fp4 screen: when built, unless (auto) it proved ineffective at a
+        // threshold >= this one (then the i8 screen)
+        c->fp4_used = c->have_fp4 && c->n_wtiles && !dense &&
+                      (c->opt_screen_fp4 == 1 || (c->opt_screen_fp4 == 2 && thr > c->fp4_bad_thr));
+        m.frag4 = c->fp4_used ? ptr<uint8_t>(c->frag4) : nullptr;
+        m.R4 = c->R4;
         m.n_chunk_rows = n;
         m.thr = thr;
         m.shift = c->shift;
@@ -580,6 +611,10 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
             c->opt_host_batch_pairs = (uint64_t)value;
             break;
         case WLD_OPT_WIDE_SCREEN: c->opt_wide_screen = value != 0; break;
+        case WLD_OPT_SCREEN_FP4:
+            if (value < 0 || value > 2) return fail(WLD_E_ARG, "WLD_OPT_SCREEN_FP4 must be 0, 1 or 2");
+            c->opt_screen_fp4 = (int)value;  // operands are built at the next load
+            break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }
     return WLD_OK;
@@ -597,6 +632,7 @@ int wld_get_option(wld_ctx *c, int option, int64_t *value) {
         case WLD_OPT_STAGING_ROWS: *value = (int64_t)c->opt_staging_rows; break;
         case WLD_OPT_HOST_BATCH_PAIRS: *value = (int64_t)c->opt_host_batch_pairs; break;
         case WLD_OPT_WIDE_SCREEN: *value = c->opt_wide_screen; break;
+        case WLD_OPT_SCREEN_FP4: *value = c->opt_screen_fp4; break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }
     return WLD_OK;
@@ -926,7 +962,10 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     c->stats.order_ms = event_ms(c->ev[3], c->ev[order_end]);
     c->stats.pair_kernel_launches = c->n_tiles ? (c->screened ? 2 : 1) : 0;
     c->stats.tiles = c->n_tiles;
-    c->stats.screened = c->screened ? 1 : 0;
+    c->stats.screened = c->screened ? (c->fp4_used ? 2 : 1) : 0;
+    // auto: a threshold at which the fp4 bound leaves > 10% of the tiles to the
+    // exact kernel is screened on i8 from now on (and every lower one)
+    if (c->screened && c->fp4_used && h[2] * 10 > c->n_tiles) c->fp4_bad_thr = std::max(c->fp4_bad_thr, r.thr);
     c->stats.screen_ms = c->screened ? event_ms(c->ev[2], c->ev[6]) : 0.0;
     c->stats.candidate_tiles = c->screened ? h[2] : c->n_tiles;
     if (n_rows) *n_rows = rows;

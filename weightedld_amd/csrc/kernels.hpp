@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 namespace wld {
 
@@ -88,7 +89,9 @@ struct MfmaLaunch {
     const int8_t *wplanes;
     const uint32_t *tiles;
     const uint32_t *wtiles;  // the same tiles paired along b (kWideSecond), for the screen; or null
-    uint32_t n_tiles, n_wtiles, L, NP, n_chunk_rows;
+    const uint8_t *frag4;    // fp4 screen operands (screen_fp4.hip): screen on fp4 MFMA; or null
+    float R4;                // the fp4 weights' residual bound
+    uint32_t n_tiles, n_wtiles, L, LP, NP, n_chunk_rows;
     float thr;
     int shift;
     unsigned plane_mask;
@@ -99,6 +102,18 @@ struct MfmaLaunch {
     uint32_t *cand_list;   // n_tiles entries
     unsigned *cand_count;  // 0 before the launch (chunk_scan_kernel resets it)
 };
+// screen_fp4.hip: the screen on fp4 (e2m1) matrix cores, nonnegative
+// weights, NP <= kFp4MaxNP (doubled sums <= 18 NP stay exact below 2^22)
+constexpr size_t kFp4MaxNP = 196608;
+size_t screen_fp4_frag_bytes(size_t LP, size_t NP);
+// fp4 codes of w * s (packed two per byte, NP / 2 bytes) and the residual
+// bound R (f32, rounded up); -1 if some weight is negative, non-finite or all zero
+int fp4_weights(const float *w, size_t N, size_t NP, std::vector<uint8_t> &packed, float *R);
+void launch_frag4(const uint8_t *codes, const uint8_t *w4, size_t LP, size_t NP, uint8_t *frag4, hipStream_t s);
+void launch_screen_fp4(const uint8_t *frag4, const uint64_t *ok_bits, const uint32_t *wtiles, uint32_t n_wtiles,
+                       size_t LP, size_t NP, float thr, float R, const OrderArgs &o, uint32_t *cand_list,
+                       unsigned *cand_count, hipStream_t s);
+
 // Enqueues the MFMA pair kernel(s) of one pass; returns true when the screen
 // ran (then screen_done, if given, is recorded between the two launches).
 bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *dense, hipStream_t s,

@@ -113,6 +113,45 @@ __host__ __device__ __forceinline__ bool r2_screen_skip_f32(float T, float A, fl
 // largest |top-plane sum| for which the screen may use r2_screen_skip_f32
 constexpr uint32_t kScreenF32MaxNP = 32768;  // 128 NP <= 2^22
 
+// One full-wave LDS-DMA (global_load_lds_dwordx4): each lane copies 16 bytes
+// from gsrc to LDS byte address lds_dst + 16*lane (lds_dst wave-uniform).  Issued
+// as inline asm so that the compiler's wait-count bookkeeping does not see it
+// (it would otherwise wait for every in-flight copy before any LDS read of the
+// other buffer): completion is ordered only by the kernel's own protocol —
+// s_waitcnt vmcnt(0) by every issuing wave, then a barrier, then the reads.
+// M0 is saved and restored inside the statement (it is compiler-reserved).
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+}
+
+// The same copy addressed as SGPR base + per-lane 32-bit VGPR offset (no
+// 64-bit per-lane address arithmetic).
+__device__ __forceinline__ void glds16_s(const void *sbase, uint32_t voff, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(sbase), "s"(lds_dst)
+        : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
 __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
     const int lane = threadIdx.x & 63;
 #pragma unroll

@@ -229,6 +229,10 @@ struct Acc16 {
         const int X = v[i >> 2][x][p][0][i & 3], Y = v[i >> 2][x][p][1][i & 3];
         return (y ? X - Y : X + Y) >> 1;
     }
+    // (X, Y) of plane 0, channel_a x: X + Y = 2 S(x, in), X - Y = 2 S(x, major)
+    __device__ __forceinline__ int2 raw(int x, int i) const {
+        return make_int2(v[i >> 2][x][0][0][i & 3], v[i >> 2][x][0][1][i & 3]);
+    }
     static __device__ __forceinline__ uint32_t a_local(int i, uint32_t wave, uint32_t lane) {
         return 16 * (wave & 3) + 4 * (lane >> 4) + (i & 3);
     }
@@ -310,44 +314,6 @@ __device__ __forceinline__ void mfma_block(v16i (&acc)[2][3][2], v4i ca, v4i cb,
     }
 }
 
-// One full-wave LDS-DMA (global_load_lds_dwordx4): each lane copies 16 bytes
-// from gsrc to LDS byte address lds_dst + 16*lane (lds_dst wave-uniform).  Issued
-// as inline asm so that the compiler's wait-count bookkeeping does not see it
-// (it would otherwise wait for every in-flight copy before any LDS read of the
-// other buffer): completion is ordered only by the kernel's own protocol —
-// s_waitcnt vmcnt(0) by every issuing wave, then a barrier, then the reads.
-// M0 is saved and restored inside the statement (it is compiler-reserved).
-__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst) {
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds_dst)
-        : "memory");
-}
-
-// The same copy addressed as SGPR base + per-lane 32-bit VGPR offset (no
-// 64-bit per-lane address arithmetic).
-__device__ __forceinline__ void glds16_s(const void *sbase, uint32_t voff, uint32_t lds_dst) {
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %3\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, %2\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(voff), "s"(sbase), "s"(lds_dst)
-        : "memory");
-}
-
-__device__ __forceinline__ uint32_t lds_addr(const void *p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
-}
 
 
 template <int NPL>
@@ -425,7 +391,7 @@ __device__ __forceinline__ bool pair_eval(double T, double SA, double SB, double
 // 1 = major) and channel_b y as an exact integer in f64: in fixed-point units
 // (S = sum_p 2^(8p) acc_p), or for kModeScreen in units of the screened plane.
 template <int MODE, class Acc, class SumFn>
-__device__ __forceinline__ void tile_epilogue(const SumFn &sum, uint32_t ta, uint32_t tb, uint32_t tid,
+__device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, uint32_t ta, uint32_t tb, uint32_t tid,
                                               uint64_t okA, uint64_t okB, uint32_t L, uint32_t n_chunk_rows,
                                               float thr, int shift, const OrderArgs &o, const DenseArgs &dn,
                                               const ScreenArgs &sc, unsigned long long *sBits, uint32_t *sRowBase) {
@@ -436,13 +402,31 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, uint32_t ta, uin
         // sums in units of the screened digit plane, within R of the exact
         // sums scaled to that unit (cells: sum_c |e_c| <= R)
         bool cand = false;
-#ifdef WLD_DIAG_SCREEN_NOEPI
+        if (sc.f32 == 2) {
+            // doubled sums straight from the X/Y accumulators (raw(x, i) =
+            // {2T, 2SB} / {2SA, 2SAB}: exact integers <= 256 NP <= 2^22), the
+            // f32 bound as a violation margin, branch-free; every pair valid
+            // unless the tile touches the diagonal or a filtered/padding site
+            const float thr_c = thr * (1.0f - 0x1p-7f), R2 = 2.0f * sc.Rf;
+            float worst = -1.0f;
+            const bool full = okA == ~0ull && okB == ~0ull && ta != tb;
 #pragma unroll
-        for (int i = 0; i < Acc::kPairs; ++i) cand |= (sum(0, 0, i) + sum(1, 1, i) + sum(0, 1, i) + sum(1, 0, i)) == 0x7fffffff;
-        if (sc.f32 > 1000) {
-#else
-        if (sc.f32) {
-#endif
+            for (int i = 0; i < Acc::kPairs; ++i) {
+                const int2 p0 = acc.raw(0, i), p1 = acc.raw(1, i);  // (X, Y) of channel_a in, major
+                const float v = r2_screen_violation((float)(p0.x + p0.y), (float)(p1.x + p1.y), (float)(p0.x - p0.y),
+                                                    (float)(p1.x - p1.y), R2, thr_c);
+                if (full) {
+                    worst = fmaxf(worst, v);
+                } else {
+                    const uint32_t a_local = Acc::a_local(i, wave, lane);
+                    const uint32_t b_local = Acc::b_local(i, wave, lane);
+                    const bool valid =
+                        ((okB >> b_local) & 1) && a0 + a_local < b0 + b_local && ((okA >> a_local) & 1);
+                    if (valid) worst = fmaxf(worst, v);
+                }
+            }
+            cand = !(worst <= 0.0f);
+        } else if (sc.f32) {
 #pragma unroll
             for (int i = 0; i < Acc::kPairs; ++i) {
                 const uint32_t a_local = Acc::a_local(i, wave, lane);
@@ -453,11 +437,7 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, uint32_t ta, uin
                                                  (float)sum(1, 1, i), sc.Rf, thr))
                     cand |= !r2_bound_skip(sum(0, 0, i), sum(1, 0, i), sum(0, 1, i), sum(1, 1, i), sc.R, thr, true);
             }
-#ifdef WLD_DIAG_SCREEN_NOEPI
-        } else if (sc.f32 > 1000) {
-#else
         } else {
-#endif
 #pragma unroll
             for (int i = 0; i < Acc::kPairs; ++i) {
                 const uint32_t a_local = Acc::a_local(i, wave, lane);
@@ -593,16 +573,16 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
         auto issue = [&](uint32_t grp, uint32_t buf) {
             const uint32_t gb = smem_lds + buf * KGB;
             const uint32_t kb0 = grp * KG;
-            const uint8_t *base = src + (size_t)kb0 * 1024;
+            const uint8_t *base = src + (size_t)kb0 * 1024;  // wave-uniform (SGPR base, lane offset in a VGPR)
             const uint32_t lane16 = lane * 16;
 #pragma unroll
             for (int st = 0; st < KG; ++st)
                 if ((WAVES == 4 || (uint32_t)(st & 1) == (wave >> 2)) && kb0 + st < NKB)
-                    glds16(base + (uint32_t)(st * 1024) + lane16, gb + st * kStageCodes + wb * 1024);
+                    glds16_s(base + st * 1024, lane16, gb + st * kStageCodes + wb * 1024);
             // digit records of the group's stages (128 B each, contiguous from
             // digf_stage(kb0)): one 1 KB full-wave copy (allocation padded past
             // the last group)
-            if (wave == 0) glds16(digf + digf_stage(kb0) + lane16, gb + KG * kStageCodes);
+            if (wave == 0) glds16_s(digf + digf_stage(kb0), lane16, gb + KG * kStageCodes);
         };
 
         issue(0, 0);
@@ -688,7 +668,7 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
                 return v;
             }
         };
-        tile_epilogue<MODE, Acc16<NPL, NB>>(sum, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, shift, o, dn, sc, sBits,
+        tile_epilogue<MODE, Acc16<NPL, NB>>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, shift, o, dn, sc, sBits,
                                             sRowBase);
     };
     if constexpr (!LOOP) {
@@ -964,7 +944,7 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_rows_kernel(const uint8_t *_
         }
         return fma(65536.0, (double)acc.get(x, 2, y, i), fma(256.0, (double)acc.get(x, 1, y, i), (double)acc.get(x, 0, y, i)));
     };
-    tile_epilogue<MODE, Acc32<3>>(sum, ta, tb, tid, ok_bits[ta], ok_bits[tb], L, n_chunk_rows, thr, shift, o, dn, sc,
+    tile_epilogue<MODE, Acc32<3>>(sum, acc, ta, tb, tid, ok_bits[ta], ok_bits[tb], L, n_chunk_rows, thr, shift, o, dn, sc,
                                   sBits, sRowBase);
 }
 
@@ -1071,8 +1051,12 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     sc.R = ldexp((double)m.resid[top - 1], -8 * (int)top);
     sc.Rf = (float)sc.R;
     if ((double)sc.Rf < sc.R) sc.Rf = nextafterf(sc.Rf, INFINITY);
-    sc.f32 = m.nonneg && m.NP <= kScreenF32MaxNP;
-    if (m.wtiles && m.n_wtiles && m.nonneg && m.NP <= kScrF32MaxNP)
+    // 2: doubled sums (NP <= 16384), 1: halved sums with f64 fallback, 0: f64
+    sc.f32 = m.nonneg ? (m.NP <= kScrF32MaxNP ? 2 : m.NP <= kScreenF32MaxNP ? 1 : 0) : 0;
+    if (m.frag4 && m.wtiles && m.n_wtiles)
+        launch_screen_fp4(m.frag4, ok_bits, m.wtiles, m.n_wtiles, m.LP, m.NP, m.thr, m.R4, o, m.cand_list,
+                          m.cand_count, s);
+    else if (m.wtiles && m.n_wtiles && m.nonneg && m.NP <= kScrF32MaxNP)
         hipLaunchKernelGGL(pair_screen_kernel, dim3(m.n_wtiles), dim3(256), 0, s, m.frag, m.frag_b, m.wplanes, ok_bits,
                            m.wtiles, m.NP, m.thr, top, o, sc);
     else
