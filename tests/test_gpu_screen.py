@@ -308,13 +308,21 @@ def test_screen_rejects_random_tiles(W, ctxs):
     assert st["candidate_tiles"] <= st["tiles"] // 100, st
     ref = O.all_pairs(buf, w, np.float32(0.05))
     assert n == len(ref["r2"])
-    # the screen is skipped where it cannot reject (r2_threshold <= 0) and with
-    # one digit plane (equal weights: the one-plane kernel is already exact)
+    # the screen is skipped where it cannot reject (r2_threshold <= 0); with one
+    # digit plane (equal weights) its sums are exact (R = 0) and the candidate
+    # launch adds an all-zero plane: same rows as the unscreened kernel
     ctx.run(0.0)
     assert ctx.stats()["screened"] == 0
-    ctx.load(buf, np.ones(2000, dtype=np.float32))
-    ctx.run(0.05)
-    assert ctx.stats()["screened"] == 0 and ctx.stats()["mfma_planes"] == 1
+    ones = np.ones(2000, dtype=np.float32)
+    ctx.load(buf, ones)
+    for thr in (0.05, 0.004, 0.002):
+        n = ctx.run(thr)
+        st = ctx.stats()
+        assert st["screened"] == 1 and st["mfma_planes"] == 1, st
+        rows = ctx.rows()
+        un, _ = _run(ctx, thr, 1, 0)
+        _same_rows(rows, un)
+        compare_rows(rows, O.all_pairs(buf, ones, np.float32(thr)), np.float32(thr), buf=buf, w=ones)
 
 
 # --------------------------------------------------------------- BASELINE config 2

@@ -97,7 +97,7 @@ struct MfmaLaunch {
     unsigned plane_mask;
     int nonneg;
     bool prefilter;  // thr > 0: skip pairs r2_bound_skip rejects
-    bool screen;     // thr > 0 and >= 2 planes: one-plane screen, then candidates
+    bool screen;     // with the prefilter: one-plane screen, then candidates
     uint64_t resid[3];
     uint32_t *cand_list;   // n_tiles entries
     unsigned *cand_count;  // 0 before the launch (chunk_scan_kernel resets it)

@@ -1041,14 +1041,19 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
         launch_lds_planes<kModeAll>(n, m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, idx, o, dn, sc, s);
         return false;
     }
-    if (!m.screen || n < 2) {
+    if (!m.screen) {
         launch_lds_planes<kModePrefilter>(n, m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, idx, o, dn, sc, s);
         return false;
     }
     // Screen: the top plane alone over every tile, the residual of the lower
     // planes bounded by R (in top-digit units: exact, a power-of-two scaling
-    // of an integer below 2^53); candidate tiles then get every plane.
-    sc.R = ldexp((double)m.resid[top - 1], -8 * (int)top);
+    // of an integer below 2^53); candidate tiles then get every plane.  With
+    // one nonzero plane (equal weights, e.g. --unweighted) the screen's sums
+    // are exact (R = 0): it only moves the per-pair work to the cheap f32
+    // bound, and the candidate launch (two-plane instantiation) adds an
+    // all-zero plane.
+    sc.R = top > 0 ? ldexp((double)m.resid[top - 1], -8 * (int)top) : 0.0;
+    if (n == 1) idx = top | ((top == 0 ? 1u : 0u) << 2);
     sc.Rf = (float)sc.R;
     if ((double)sc.Rf < sc.R) sc.Rf = nextafterf(sc.Rf, INFINITY);
     // 2: doubled sums (NP <= 16384), 1: halved sums with f64 fallback, 0: f64
