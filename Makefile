@@ -3,11 +3,16 @@
 # Everything is compiled for gfx950 only.  -ffp-contract=off: the LdStats
 # epilogue must not be FMA-contracted (Rust never contracts); the pair kernels
 # use explicit fmaf where a fused multiply-add is exact by construction.
+# -fno-slp-vectorize: no packed-f32 VALU ops (v_pk_add/mul/fma_f32).  With them
+# the one-plane pair kernel's f32 epilogue gave timing-dependent wrong values
+# (one accumulator row, lanes 48-63) on MI355X; without them 16 repeated runs
+# were bit-identical and oracle-exact ("packed-f32 epilogue");
+# tests/test_codegen.py keeps them out of the built library.
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 PKG := weightedld_amd
 CSRC := $(PKG)/csrc
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Iinclude -I$(CSRC)
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Iinclude -I$(CSRC)
 HIP_SRCS := $(CSRC)/encode.hip $(CSRC)/prepass.hip $(CSRC)/pair_valu.hip $(CSRC)/pair_mfma.hip $(CSRC)/screen_fp4.hip \
             $(CSRC)/order.hip $(CSRC)/capi.hip
 CXX_SRCS := $(CSRC)/host.cpp

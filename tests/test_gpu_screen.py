@@ -39,7 +39,9 @@ def _same_rows(a, b):
     for f in ("site_a", "site_b", "d", "d_prime", "r2"):
         x, y = getattr(a, f), getattr(b, f)
         assert len(x) == len(y), (f, len(x), len(y))
-        assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), f
+        bad = np.nonzero(x.view(np.uint32) != y.view(np.uint32))[0]
+        assert len(bad) == 0, (f, len(bad), [(int(a.site_a[i]), int(a.site_b[i]), float(x[i]), float(y[i]),
+                                              float(a.r2[i]), float(b.r2[i])) for i in bad[:6]])
 
 
 def _rows_equal_dense(rows, dense, thr, L):
