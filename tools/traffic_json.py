@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Writes profiles/traffic.json's entry for the pair kernel from rocprofv3
 --pmc passes (FETCH_SIZE, WRITE_SIZE, TCC_HIT/MISS in separate runs):
-  tools/traffic_json.py PMC_DIR KEY SOURCE_NOTE [LDS_DMA_BYTES]"""
+  tools/traffic_json.py PMC_DIR KEY SOURCE_NOTE [LDS_DMA_BYTES] [KERNEL_SUBSTRING]
+KERNEL_SUBSTRING (e.g. "pair_mfma_kernel<3, 1, false>", the screen) restricts the
+average to one kernel instantiation; default: every pair kernel dispatch."""
 import collections
 import csv
 import glob
@@ -10,10 +12,12 @@ import os
 import sys
 
 pmc, key, source = sys.argv[1], sys.argv[2], sys.argv[3]
+ksub = sys.argv[5] if len(sys.argv) > 5 else ""
 vals = collections.defaultdict(list)
 for f in glob.glob(pmc + "/**/*_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "pair_mfma" in r["Kernel_Name"] or "pair_valu" in r["Kernel_Name"]:
+        name = r["Kernel_Name"]
+        if (ksub in name) if ksub else ("pair_mfma" in name or "pair_valu" in name):
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
 m = {k: sum(v) / len(v) for k, v in vals.items()}
 fetch, write = m.get("FETCH_SIZE", 0.0), m.get("WRITE_SIZE", 0.0)
@@ -31,9 +35,11 @@ entry = {
             "fragment copies fit the 256 MB MALL",
     "source": source,
 }
+if ksub:
+    entry["kernel"] = ksub
 if "TCC_HIT_sum" in m:
     entry["l2_hit_rate"] = m["TCC_HIT_sum"] / (m["TCC_HIT_sum"] + m["TCC_MISS_sum"])
-lds = int(sys.argv[4]) if len(sys.argv) > 4 else old.get("lds_dma_bytes_per_launch")
+lds = int(sys.argv[4]) if len(sys.argv) > 4 and sys.argv[4] else old.get("lds_dma_bytes_per_launch")
 if lds:
     entry["lds_dma_bytes_per_launch"] = lds
 data[key] = entry
