@@ -3,6 +3,9 @@
 // argv[1], writes one byte per record (1 = skip) to argv[2].  With argv[3] =
 // "f32": the screen's f32 form r2_screen_skip_f32 (inputs rounded to f32, R
 // rounded up; nonneg ignored — the f32 form is for nonnegative weights only).
+// With argv[3] = "f32g": the screen kernel's split form (screen_consts from a
+// launch-wide bound Tg >= T, passed in the nonneg field, then r2_screen_terms;
+// skip iff both terms are <= 0).
 #include <cmath>
 #include <cstdio>
 #include <string>
@@ -13,6 +16,7 @@
 int main(int argc, char **argv) {
     if (argc != 3 && argc != 4) return 2;
     const bool f32 = argc == 4 && std::string(argv[3]) == "f32";
+    const bool f32g = argc == 4 && std::string(argv[3]) == "f32g";
     FILE *f = fopen(argv[1], "rb");
     if (!f) return 3;
     std::vector<double> rec;
@@ -23,7 +27,16 @@ int main(int argc, char **argv) {
     std::vector<unsigned char> out(n);
     for (size_t i = 0; i < n; ++i) {
         const double *r = &rec[7 * i];
-        if (f32) {
+        if (f32g) {
+            float R = (float)r[4], Tg = (float)r[6];
+            if ((double)R < r[4]) R = std::nextafter(R, INFINITY);
+            if ((double)Tg < r[6]) Tg = std::nextafter(Tg, INFINITY);
+            float E, mloc, t2;
+            wld::screen_consts(Tg, R, E, mloc);
+            const float thr_c = (float)r[5] * (1.0f - 0x1p-7f);
+            const float t1 = wld::r2_screen_terms((float)r[0], (float)r[1], (float)r[2], (float)r[3], R, thr_c, E, mloc, t2);
+            out[i] = t1 <= 0.0f && t2 <= 0.0f ? 1 : 0;
+        } else if (f32) {
             float R = (float)r[4];
             if ((double)R < r[4]) R = std::nextafter(R, INFINITY);
             out[i] = wld::r2_screen_skip_f32((float)r[0], (float)r[1], (float)r[2], (float)r[3], R, (float)r[5]) ? 1 : 0;

@@ -232,9 +232,12 @@ def test_prefilter_and_screen_never_change_rows(W, ctxs, case):
             # fp4 operands exist only for nonnegative weights
             assert st4["screened"] == (1 if case == "mixed_sign" else 2), st4
             assert st4["candidate_tiles"] <= st4["tiles"]
-        # the 64x128 screen decides in f32 only (a pair it cannot decide makes
-        # its tile a candidate); the 64x64 screen falls back to f64 per pair
-        assert stn["candidate_tiles"] <= st["candidate_tiles"], (thr, stn["candidate_tiles"], st["candidate_tiles"])
+        # the 64x128 screen bounds each pair with its own T; the 64x64 screen
+        # with launch-wide constants (E and the marginal floor from T <= 2 sum
+        # of the top digits, screen_consts), a little looser on sites with many
+        # "out" sequences
+        assert stn["candidate_tiles"] <= st["candidate_tiles"] + max(2, st["candidate_tiles"] // 8), (
+            thr, stn["candidate_tiles"], st["candidate_tiles"])
         _rows_equal_dense(scr, dense, thr, L)
         screened_any |= st["screened"] == 1
         assert st["candidate_tiles"] <= st["tiles"]

@@ -24,12 +24,14 @@ def harness(tmp_path_factory):
                     "-I", os.path.join(REPO, "include"), "-I", os.path.join(REPO, "weightedld_amd", "csrc"),
                     "-x", "hip", os.path.join(REPO, "tests", "cpp", "bound_check.cpp"), "-o", exe], check=True)
 
-    def run(T, A, B, AB, R, thr, nonneg=True, f32=False):
+    def run(T, A, B, AB, R, thr, nonneg=True, f32=False, Tg=None):
         n = len(T)
-        rec = np.stack([np.asarray(x, np.float64) * np.ones(n) for x in (T, A, B, AB, R, thr, float(nonneg))], 1)
+        last = float(nonneg) if Tg is None else Tg
+        rec = np.stack([np.asarray(x, np.float64) * np.ones(n) for x in (T, A, B, AB, R, thr, last)], 1)
         d = tmp_path_factory.mktemp("io")
         rec.tofile(str(d / "in.bin"))
-        subprocess.run([exe, str(d / "in.bin"), str(d / "out.bin")] + (["f32"] if f32 else []), check=True)
+        mode = ["f32g"] if Tg is not None else ["f32"] if f32 else []
+        subprocess.run([exe, str(d / "in.bin"), str(d / "out.bin")] + mode, check=True)
         return np.fromfile(str(d / "out.bin"), dtype=np.uint8).astype(bool)
     return run
 
@@ -172,3 +174,50 @@ def test_screen_f32_bound_sound_near_threshold(harness, thr):
             viol += int((skip & passes).sum())
             skipped += int(skip.sum())
     assert viol == 0 and skipped > 0
+
+
+@pytest.mark.parametrize("rare", [False, True])
+def test_screen_launch_constants_sound(harness, rare):
+    # the screen kernel's split form: E and 2^-12 Tb from a launch-wide Tg >= T
+    # (Tg = 2 sum |top digits|), terms per pair.  With Tg = T it decides exactly
+    # as r2_screen_skip_f32; with any larger Tg it never skips a pair whose
+    # exact sums pass the f32 epilogue, and still skips most random tables.
+    rng = np.random.default_rng(41 + rare)
+    viol = skipped = same = total = 0
+    for it in range(12):
+        n = 200_000
+        scale = float(2 ** rng.integers(10, 22))
+        c = screen_tables(rng, n, scale, rare)
+        T, A, B, AB = c.sum(0), c[0] + c[1], c[0] + c[2], c[0]
+        thr = float(np.float32(rng.choice([0.001, 0.01, 0.05, 0.2, 0.6])))
+        R = rng.choice([0.0, 1e-4, 1e-3, 1e-2]) * scale * rng.random()
+        e = rng.random((4, n)) * rng.choice([-1.0, 1.0], (4, n))
+        e = np.trunc(e / np.maximum(np.abs(e).sum(0), 1e-12) * R * rng.random(n))
+        h = c + e
+        args = (h.sum(0), h[0] + h[1], h[0] + h[2], h[0], R, thr)
+        with np.errstate(invalid="ignore"):
+            passes = f32_r2(T, A, B, AB) > np.float32(thr)
+        eq = harness(*args, Tg=h.sum(0))
+        same += int((eq == harness(*args, f32=True)).sum())
+        total += n
+        for f in (1.0, 1.3, 4.0):
+            Tg = float(h.sum(0).max()) * f
+            s = harness(*args, Tg=Tg)
+            viol += int((s & passes).sum())
+            skipped += int(s.sum())
+    assert viol == 0
+    assert same == total
+    assert skipped > 0
+
+
+@pytest.mark.parametrize("thr", [0.05, 0.3])
+def test_screen_launch_constants_near_threshold(harness, thr):
+    rng = np.random.default_rng(int(thr * 1000) + 7)
+    viol = 0
+    for _ in range(6):
+        T, A, B, AB = near_threshold_tables(rng, 1_000_000, thr, scale=2.0 ** 22, window=0.05)
+        passes = f32_r2(T, A, B, AB) > np.float32(thr)
+        for R in (0.0, 1.0, 17.5):
+            for Tg in (float(T.max()), float(T.max()) * 2.0):
+                viol += int((harness(T, A, B, AB, R, thr, Tg=Tg) & passes).sum())
+    assert viol == 0

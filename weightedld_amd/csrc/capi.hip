@@ -125,7 +125,7 @@ struct wld_ctx {
     int shift = 0;
     int fixed_planes = 3;      // digit planes of the fixed-point weights (3: 23 bits, 4: 31 bits)
     unsigned plane_mask = 7;   // weight-digit planes with a nonzero digit (MFMA)
-    MfmaWeightStats wst{7, 1, {0, 0, 0}};  // digit-plane statistics of the load (MFMA)
+    MfmaWeightStats wst{7, 1, {0, 0, 0}, {0, 0, 0, 0}};  // digit-plane statistics of the load (MFMA)
 
     // run state
     DevBuf tiles, wtiles, cand, seg_cnt, seg_off, chunk_total, chunk_base, counters;
@@ -293,7 +293,7 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
         if (L) HIP_TRY(hipMemcpyAsync(c->site_map.p, m.data(), L * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
-    c->wst = MfmaWeightStats{7, 1, {0, 0, 0}};
+    c->wst = MfmaWeightStats{7, 1, {0, 0, 0}, {0, 0, 0, 0}};
     if (c->kernel == WLD_KERNEL_MFMA && mfma_weight_stats(ptr<int8_t>(c->planes), c->LP, c->NP, c->stream, &c->wst))
         return fail(WLD_E_HIP, "reading the weight-plane statistics failed");
     const unsigned all_planes = (1u << c->fixed_planes) - 1;
@@ -494,6 +494,7 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         m.prefilter = c->opt_prefilter && thr > 0.0f;
         m.screen = m.prefilter && c->opt_screen;
         for (int t = 0; t < 3; ++t) m.resid[t] = c->wst.resid[t];
+        for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
         m.cand_list = ptr<uint32_t>(c->cand);
         m.cand_count = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 2);
         sc = launch_pair_mfma(m, o, dense, c->stream, c->ev[6]);

@@ -74,6 +74,7 @@ struct MfmaWeightStats {
     unsigned plane_mask;  // bit p = digit plane p (of 4) has a nonzero digit
     int nonneg;           // every weight >= 0
     uint64_t resid[3];    // resid[t-1] = sum_k |q_k - 2^(8t) d_t,k|: what top plane t alone leaves out
+    uint64_t dsum[4];     // dsum[p] = sum_k |d_p,k|: bounds every one-plane sum of plane p
 };
 // synchronises s; returns 0, or -1 on a HIP error
 int mfma_weight_stats(const int8_t *wplanes, size_t LP, size_t NP, hipStream_t s, MfmaWeightStats *out);
@@ -99,6 +100,7 @@ struct MfmaLaunch {
     bool prefilter;  // thr > 0: skip pairs r2_bound_skip rejects
     bool screen;     // with the prefilter: one-plane screen, then candidates
     uint64_t resid[3];
+    uint64_t dsum[4];
     uint32_t *cand_list;   // n_tiles entries
     unsigned *cand_count;  // 0 before the launch (chunk_scan_kernel resets it)
 };

@@ -97,15 +97,30 @@ __host__ __device__ __forceinline__ bool r2_bound_skip(double T, double A, doubl
 // Returned as a violation margin: the pair is skipped iff it is <= 0 (both
 // terms are differences of f32 values, whose rounded sign is exact).
 // thr_c = thr * (1 - 2^-7) in f32.
-__host__ __device__ __forceinline__ float r2_screen_violation(float T, float A, float B, float AB, float R,
-                                                              float thr_c) {
-    const float Tb = (T + 2.0f * R) * (1.0f + 0x1p-20f);
+// The derivation holds for Tb any f32 upper bound of T + 2R (it only bounds
+// sums, cells and T + R from above), so a launch may fix Tb from a bound Tg on
+// every T it screens (the screen: Tg = 2 sum_k |top digit_k|, doubled sums)
+// and precompute E(Tb) and 2^-12 Tb once (screen_consts); per pair that leaves
+// r2_screen_terms, whose two terms must both be <= 0 for a skip.
+__host__ __device__ __forceinline__ void screen_consts(float Tg, float R, float &E, float &mloc) {
+    const float Tb = (Tg + 2.0f * R) * (1.0f + 0x1p-20f);
+    E = R * Tb + R * R + 0x1p-19f * (Tb * Tb);
+    mloc = 0x1p-12f * Tb;
+}
+__host__ __device__ __forceinline__ float r2_screen_terms(float T, float A, float B, float AB, float R, float thr_c,
+                                                          float E, float mloc, float &t2) {
     const float m1 = A - R, m2 = (T - A) - R, m3 = B - R, m4 = (T - B) - R;
     const float mlo = fminf(fminf(m1, m2), fminf(m3, m4));
-    const float num = fabsf(A * B - AB * T);
-    const float E = R * Tb + R * R + 0x1p-19f * (Tb * Tb);
-    const float nub = num + E;
-    return fmaxf(nub * nub - thr_c * ((m1 * m2) * (m3 * m4)), 0x1p-12f * Tb - mlo);
+    const float nub = fabsf(A * B - AB * T) + E;
+    t2 = mloc - mlo;
+    return nub * nub - thr_c * ((m1 * m2) * (m3 * m4));
+}
+__host__ __device__ __forceinline__ float r2_screen_violation(float T, float A, float B, float AB, float R,
+                                                              float thr_c) {
+    float E, mloc, t2;
+    screen_consts(T, R, E, mloc);
+    const float t1 = r2_screen_terms(T, A, B, AB, R, thr_c, E, mloc, t2);
+    return fmaxf(t1, t2);
 }
 __host__ __device__ __forceinline__ bool r2_screen_skip_f32(float T, float A, float B, float AB, float R, float thr) {
     return r2_screen_violation(T, A, B, AB, R, thr * (1.0f - 0x1p-7f)) <= 0.0f;

@@ -95,19 +95,20 @@ __host__ __device__ inline size_t digf_stage(uint32_t kb) { return (size_t)(kb /
 //                                         per 32-sequence stage, 1 KB per group
 //                                         (LDS path; k = 32kb + 16h + j)
 //   ok_bits[g] bit i = site 64g+i passes  (site_ok, lib.rs:400-408)
-//   stats (after the bits, 32 bytes):
+//   stats (after the bits, 64 bytes):
 //     u32  bit p (p < 4) = some digit of plane p is nonzero; bit 8 = some weight < 0
 //     u64  resid[t-1] = sum_k |q_k - 2^(8t) d_t,k| for t = 1, 2, 3: what the top
 //          plane t alone leaves out (the screen's residual bound)
+//     u64  dsum[p] = sum_k |d_p,k| for p = 0..3 (bounds the screen's sums)
 __host__ __device__ inline size_t planemask_offset(size_t LP, size_t NP) { return okbits_offset(NP) + LP / 64 * 8; }
 // + 1 KB: a half-group (kg < kGroup) digit DMA copies 1 KB from a 512-B offset
-size_t mfma_planes_bytes(size_t LP, size_t NP) { return planemask_offset(LP, NP) + 32 + kDigGroup; }
+size_t mfma_planes_bytes(size_t LP, size_t NP) { return planemask_offset(LP, NP) + 64 + kDigGroup; }
 
 __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict__ w_pad, uint32_t NP, int shift,
                                                          int8_t *__restrict__ planes, int8_t *__restrict__ digf,
                                                          unsigned *__restrict__ stats) {
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-    unsigned used = 0, res[3] = {0, 0, 0};
+    unsigned used = 0, res[3] = {0, 0, 0}, ds[kMaxPlanes] = {0, 0, 0, 0};
     if (k < NP) {
         const float w = w_pad[k];
         long long q = llrint(ldexp((double)w, shift));
@@ -120,6 +121,7 @@ __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict_
             q = (q - r) / 256;
             low += (int)r << (8 * p);
             planes[p * NP + k] = (int8_t)r;
+            ds[p] = (unsigned)(r < 0 ? -r : r);
             digf[digf_stage(kb) + (2 * p + h) * 16 + j] = (int8_t)r;
             used |= (r != 0) << p;
         }
@@ -131,6 +133,8 @@ __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict_
         used |= __shfl_xor(used, off, 64);
 #pragma unroll
         for (int t = 0; t < 3; ++t) res[t] += __shfl_xor(res[t], off, 64);
+#pragma unroll
+        for (int p = 0; p < kMaxPlanes; ++p) ds[p] += __shfl_xor(ds[p], off, 64);
     }
     if ((threadIdx.x & 63) == 0) {
         if (used) atomicOr(stats, used);
@@ -138,6 +142,9 @@ __global__ __launch_bounds__(256) void mfma_prep_kernel(const float *__restrict_
 #pragma unroll
         for (int t = 0; t < 3; ++t)
             if (res[t]) atomicAdd(acc + t, (unsigned long long)res[t]);
+#pragma unroll
+        for (int p = 0; p < kMaxPlanes; ++p)
+            if (ds[p]) atomicAdd(acc + 3 + p, (unsigned long long)ds[p]);
     }
 }
 
@@ -358,6 +365,7 @@ enum : int { kModeDense = 0, kModeAll = 1, kModePrefilter = 2, kModeScreen = 3 }
 struct ScreenArgs {
     double R;               // kModeScreen: residual bound in top-digit units
     float Rf;               // R rounded up to f32
+    float E, mloc;          // f32 == 2: screen_consts of the launch (doubled sums)
     int f32;                // kModeScreen: per-pair test in f32 (nonneg, NP <= kScreenF32MaxNP)
     int nonneg;             // all weights >= 0 (exact 2x2 cells are >= 0)
     uint32_t *cand_list;    // kModeScreen: candidate tiles (packed ta << 16 | tb)
@@ -407,25 +415,36 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
             // {2T, 2SB} / {2SA, 2SAB}: exact integers <= 256 NP <= 2^22), the
             // f32 bound as a violation margin, branch-free; every pair valid
             // unless the tile touches the diagonal or a filtered/padding site
+            // E and 2^-12 Tb fixed per launch from Tg = 2 sum |top digits| >= every
+            // doubled T (screen_consts); each term's f32 bits as an int: the
+            // maximum is > 0 iff some term is > 0 (finite terms: integer sums <= 2^22)
             const float thr_c = thr * (1.0f - 0x1p-7f), R2 = 2.0f * sc.Rf;
-            float worst = -1.0f;
+            int worst = -1;
             const bool full = okA == ~0ull && okB == ~0ull && ta != tb;
+            if (full) {
 #pragma unroll
-            for (int i = 0; i < Acc::kPairs; ++i) {
-                const int2 p0 = acc.raw(0, i), p1 = acc.raw(1, i);  // (X, Y) of channel_a in, major
-                const float v = r2_screen_violation((float)(p0.x + p0.y), (float)(p1.x + p1.y), (float)(p0.x - p0.y),
-                                                    (float)(p1.x - p1.y), R2, thr_c);
-                if (full) {
-                    worst = fmaxf(worst, v);
-                } else {
+                for (int i = 0; i < Acc::kPairs; ++i) {
+                    const int2 p0 = acc.raw(0, i), p1 = acc.raw(1, i);  // (X, Y) of channel_a in, major
+                    float t2;
+                    const float t1 = r2_screen_terms((float)(p0.x + p0.y), (float)(p1.x + p1.y), (float)(p0.x - p0.y),
+                                                     (float)(p1.x - p1.y), R2, thr_c, sc.E, sc.mloc, t2);
+                    worst = max(worst, max(__float_as_int(t1), __float_as_int(t2)));
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < Acc::kPairs; ++i) {
+                    const int2 p0 = acc.raw(0, i), p1 = acc.raw(1, i);
+                    float t2;
+                    const float t1 = r2_screen_terms((float)(p0.x + p0.y), (float)(p1.x + p1.y), (float)(p0.x - p0.y),
+                                                     (float)(p1.x - p1.y), R2, thr_c, sc.E, sc.mloc, t2);
                     const uint32_t a_local = Acc::a_local(i, wave, lane);
                     const uint32_t b_local = Acc::b_local(i, wave, lane);
                     const bool valid =
                         ((okB >> b_local) & 1) && a0 + a_local < b0 + b_local && ((okA >> a_local) & 1);
-                    if (valid) worst = fmaxf(worst, v);
+                    if (valid) worst = max(worst, max(__float_as_int(t1), __float_as_int(t2)));
                 }
             }
-            cand = !(worst <= 0.0f);
+            cand = worst > 0;
         } else if (sc.f32) {
 #pragma unroll
             for (int i = 0; i < Acc::kPairs; ++i) {
@@ -951,7 +970,7 @@ __global__ __launch_bounds__(256, 2) void pair_mfma_rows_kernel(const uint8_t *_
 void launch_mfma_prep(const uint8_t *site_ok, const float *w_pad, size_t L, size_t LP, size_t NP, int shift,
                       int8_t *planes, hipStream_t s) {
     unsigned *stats = reinterpret_cast<unsigned *>(planes + planemask_offset(LP, NP));
-    (void)hipMemsetAsync(stats, 0, 32, s);
+    (void)hipMemsetAsync(stats, 0, 64, s);
     hipLaunchKernelGGL(mfma_prep_kernel, dim3((unsigned)((NP + 255) / 256)), dim3(256), 0, s, w_pad, (uint32_t)NP,
                        shift, planes, planes + digf_offset(NP), stats);
     hipLaunchKernelGGL(okbits_kernel, dim3((unsigned)(LP / 64)), dim3(64), 0, s, site_ok, (uint32_t)L,
@@ -968,6 +987,7 @@ int mfma_weight_stats(const int8_t *wplanes, size_t LP, size_t NP, hipStream_t s
     struct {
         unsigned mask, pad;
         unsigned long long resid[3];
+        unsigned long long dsum[kMaxPlanes];
     } h{};
     if (hipMemcpyAsync(&h, wplanes + planemask_offset(LP, NP), sizeof(h), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
@@ -975,6 +995,7 @@ int mfma_weight_stats(const int8_t *wplanes, size_t LP, size_t NP, hipStream_t s
     out->plane_mask = h.mask & 15;
     out->nonneg = !(h.mask & 0x100);
     for (int t = 0; t < 3; ++t) out->resid[t] = h.resid[t];
+    for (int p = 0; p < kMaxPlanes; ++p) out->dsum[p] = h.dsum[p];
     return 0;
 }
 
@@ -1008,7 +1029,7 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     const DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
     const uint64_t *ok_bits = reinterpret_cast<const uint64_t *>(m.wplanes + okbits_offset(m.NP));
     const bool prefilter = !dense && m.prefilter && m.thr > 0.0f;
-    ScreenArgs sc{0.0, 0.0f, 0, m.nonneg, m.cand_list, m.cand_count};
+    ScreenArgs sc{0.0, 0.0f, 0.0f, 0.0f, 0, m.nonneg, m.cand_list, m.cand_count};
     if (!m.frag) {  // site-major kernel (all three planes)
         const dim3 g(m.n_tiles), b(256);
         if (dense)
@@ -1058,6 +1079,8 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     if ((double)sc.Rf < sc.R) sc.Rf = nextafterf(sc.Rf, INFINITY);
     // 2: doubled sums (NP <= 16384), 1: halved sums with f64 fallback, 0: f64
     sc.f32 = m.nonneg ? (m.NP <= kScrF32MaxNP ? 2 : m.NP <= kScreenF32MaxNP ? 1 : 0) : 0;
+    // every doubled one-plane T <= 2 sum_k |d_top,k| <= 256 NP <= 2^22 (exact in f32)
+    if (sc.f32 == 2) screen_consts((float)(2 * m.dsum[top]), 2.0f * sc.Rf, sc.E, sc.mloc);
     if (m.frag4 && m.wtiles && m.n_wtiles)
         launch_screen_fp4(m.frag4, ok_bits, m.wtiles, m.n_wtiles, m.LP, m.NP, m.thr, m.R4, o, m.cand_list,
                           m.cand_count, s);
