@@ -44,11 +44,13 @@ def child(path, config, reps, thr, unweighted=False):
     if hasattr(lib, "wld_debug_stamps"):
         st = (ctypes.c_ulonglong * 8)()
         lib.wld_debug_stamps(st, 1)
-    t, rows = [], 0
+    t, rows, ts = [], 0, []
     for _ in range(reps):
         rows = ctx.run(thr)
-        t.append(ctx.stats()["pair_kernel_ms"])
-    out = {"ms": t, "rows": rows}
+        sx = ctx.stats()
+        t.append(sx["pair_kernel_ms"])
+        ts.append(sx.get("screen_ms", 0.0))
+    out = {"ms": t, "rows": rows, "screen_ms": sorted(ts)[len(ts) // 2]}
     ops = 8.0 * ctx.stats()["mfma_planes"] * ((N + 63) // 64 * 64) * (Ls * (Ls - 1) / 2)
     out["tops"] = ops / (sorted(t)[len(t) // 2] * 1e-3) / 1e12
     if st is not None:
@@ -94,11 +96,13 @@ def main():
                 continue
             r = json.loads(out.stdout.strip().splitlines()[-1])
             res.setdefault(name, {"ms": [], "rows": r["rows"]})["ms"] += r["ms"]
+            res[name].setdefault("screen_ms", []).append(r.get("screen_ms", 0.0))
             print(json.dumps({"build": name, "median_ms": statistics.median(r["ms"]), "rows": r["rows"], "tops": r["tops"],
-                              "stamps": r.get("stamps_per_wave")}), flush=True)
+                              "screen_ms": r.get("screen_ms"), "stamps": r.get("stamps_per_wave")}), flush=True)
     for name, r in res.items():
         print(json.dumps({"build": name, "median_ms": statistics.median(r["ms"]), "min_ms": min(r["ms"]),
-                          "rows": r["rows"], "n": len(r["ms"])}))
+                          "screen_ms": statistics.median(r.get("screen_ms", [0.0])), "rows": r["rows"],
+                          "n": len(r["ms"])}))
 
 
 if __name__ == "__main__":
