@@ -152,12 +152,15 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *   WLD_OPT_PREFILTER  1 (default): with r2_threshold > 0 the MFMA kernel
  *                      skips the f32 epilogue of pairs that a rigorous bound
  *                      proves cannot pass; 0: every pair.
- *   WLD_OPT_SCREEN     1 (default): with the prefilter on, a screen launch on
- *                      the top nonzero weight-digit plane bounds every pair's
- *                      r2 (the lower planes' share bounded exactly; none with
- *                      a single nonzero plane, e.g. equal weights) and only
- *                      candidate 64x64 tiles are recomputed with every plane;
- *                      0: every tile, every plane.
+ *   WLD_OPT_SCREEN     1 (default, auto): with the prefilter on, a screen
+ *                      launch on the top nonzero weight-digit plane bounds
+ *                      every pair's r2 (the lower planes' share bounded
+ *                      exactly; none with a single nonzero plane, e.g. equal
+ *                      weights) and only candidate 64x64 tiles are recomputed
+ *                      with every plane — unless at this or a higher threshold
+ *                      the screen left more than half the tiles as candidates
+ *                      (then every tile goes to the full kernel directly);
+ *                      2: always screen; 0: every tile, every plane.
  *   WLD_OPT_TILE_ORDER 0 (default): L2/XCD-aware tile launch order; 1: plain
  *                      (a-tile, b-tile) order.
  *   WLD_OPT_ALL_PLANES 0 (default): all-zero digit planes are skipped; 1: the

@@ -129,7 +129,7 @@ def check_exact_model(ctx, buf, w, dense=None):
 
 def _run(ctx, thr, prefilter, screen, wide=0, fp4=0):
     ctx.set_option("prefilter", prefilter)
-    ctx.set_option("screen", screen)
+    ctx.set_option("screen", 2 if screen else 0)  # 2: screen even where auto would not
     ctx.set_option("wide_screen", wide)
     ctx.set_option("screen_fp4", fp4)
     ctx.run(thr)
@@ -297,6 +297,33 @@ def test_fp4_screen_auto_policy(W, ctxs):
     assert seen[0][1] == 2 and seen[0][2] * 10 > seen[0][3], seen
     assert seen[1][1] == 1 and seen[2][1] == 1 and seen[3][1] == 2, seen
     ctx.set_option("screen_fp4", 0)
+
+
+def test_screen_auto_policy(W, ctxs):
+    # A threshold at which the screen leaves more than half the tiles as
+    # candidates (random data, r2 ~ 1/N, thr a few times that) is not screened
+    # again, nor is any lower one; higher thresholds still are.  Rows as the
+    # oracle's throughout; option 2 screens regardless.
+    ctx = _ctx(ctxs, "mfma")
+    buf = synth(2000, 2000, 23)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ctx.load(buf, w)
+    assert ctx.get_option("screen") == 1
+    seen = []
+    for thr in (0.002, 0.002, 0.001, 0.05, 0.001, 0.003):
+        ctx.run(thr)
+        st = ctx.stats()
+        seen.append((thr, st["screened"], st["candidate_tiles"], st["tiles"]))
+        compare_rows(ctx.rows(), O.all_pairs(buf, w, np.float32(thr)), np.float32(thr), buf=buf, w=w)
+    assert seen[0][1] == 1 and seen[0][2] * 2 > seen[0][3], seen
+    assert [x[1] for x in seen[1:]] == [0, 0, 1, 0, 1], seen
+    ctx.set_option("screen", 2)
+    rows2 = (ctx.run(0.001), ctx.rows(), ctx.stats()["screened"])
+    ctx.set_option("screen", 0)
+    rows0 = (ctx.run(0.001), ctx.rows())
+    ctx.set_option("screen", 1)
+    assert rows2[2] == 1 and rows2[0] == rows0[0]
+    _same_rows(rows2[1], rows0[1])
 
 
 def test_screen_rejects_random_tiles(W, ctxs):

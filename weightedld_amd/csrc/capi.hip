@@ -101,7 +101,9 @@ struct wld_ctx {
     unsigned long long *d_hcnt = nullptr;
     int kernel_pref = WLD_KERNEL_AUTO;
     // wld_set_option (include/weightedld.h)
-    bool opt_prefilter = true, opt_screen = true, opt_tile_rows = false, opt_all_planes = false;
+    bool opt_prefilter = true, opt_tile_rows = false, opt_all_planes = false;
+    int opt_screen = 1;             // WLD_OPT_SCREEN: 0 never, 1 auto (default), 2 always
+    float screen_bad_thr = -1.0f;   // auto: the largest threshold at which the screen left > half the tiles
     bool opt_wide_screen = false;  // WLD_OPT_WIDE_SCREEN: the i8 screen on 64x128 tiles (A/B: not faster)
     int opt_screen_fp4 = 0;        // WLD_OPT_SCREEN_FP4: 0 never (default: measured no faster), 1 always, 2 auto
     bool have_fp4 = false;         // frag4 holds this load's fp4 screen operands
@@ -263,6 +265,7 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
         // the fp4 screen's operands (screen_fp4.hip): nonnegative weights only
         c->have_fp4 = false;
         c->fp4_bad_thr = -1.0f;
+        c->screen_bad_thr = -1.0f;
         if (c->use_frag && c->opt_screen_fp4 && c->NP <= kFp4MaxNP && c->L > 0) {
             std::vector<float> hw(c->NP);
             HIP_TRY(hipMemcpyAsync(hw.data(), c->w_pad.p, c->NP * sizeof(float), hipMemcpyDeviceToHost, c->stream));
@@ -492,7 +495,9 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         m.nonneg = c->wst.nonneg;
         // both need a positive threshold to reject anything
         m.prefilter = c->opt_prefilter && thr > 0.0f;
-        m.screen = m.prefilter && c->opt_screen;
+        // auto: below a threshold at which the screen left more than half the
+        // tiles as candidates, every tile goes straight to the full kernel
+        m.screen = m.prefilter && (c->opt_screen == 2 || (c->opt_screen == 1 && thr > c->screen_bad_thr));
         for (int t = 0; t < 3; ++t) m.resid[t] = c->wst.resid[t];
         for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
         m.cand_list = ptr<uint32_t>(c->cand);
@@ -590,7 +595,11 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
     if (c->pend.active) return fail(WLD_E_STATE, "wld_set_option during a run");
     switch (option) {
         case WLD_OPT_PREFILTER: c->opt_prefilter = value != 0; break;
-        case WLD_OPT_SCREEN: c->opt_screen = value != 0; break;
+        case WLD_OPT_SCREEN:
+            if (value < 0 || value > 2) return fail(WLD_E_ARG, "WLD_OPT_SCREEN takes 0, 1 or 2");
+            c->opt_screen = (int)value;
+            c->screen_bad_thr = -1.0f;
+            break;
         case WLD_OPT_TILE_ORDER:
             c->opt_tile_rows = value != 0;
             c->tiles_lb = c->tiles_le = ~0u;  // rebuild the list at the next run
@@ -967,6 +976,10 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     // auto: a threshold at which the fp4 bound leaves > 10% of the tiles to the
     // exact kernel is screened on i8 from now on (and every lower one)
     if (c->screened && c->fp4_used && h[2] * 10 > c->n_tiles) c->fp4_bad_thr = std::max(c->fp4_bad_thr, r.thr);
+    // auto: a threshold at which even the i8 screen leaves more than half the
+    // tiles is not screened from now on (nor any lower one): the screen costs a
+    // third of the full three-plane kernel, the candidates as much again
+    if (c->screened && !c->fp4_used && h[2] * 2 > c->n_tiles) c->screen_bad_thr = std::max(c->screen_bad_thr, r.thr);
     c->stats.screen_ms = c->screened ? event_ms(c->ev[2], c->ev[6]) : 0.0;
     c->stats.candidate_tiles = c->screened ? h[2] : c->n_tiles;
     if (n_rows) *n_rows = rows;
