@@ -5,7 +5,9 @@
 // rounded up; nonneg ignored — the f32 form is for nonnegative weights only).
 // With argv[3] = "f32g": the screen kernel's split form (screen_consts from a
 // launch-wide bound Tg >= T, passed in the nonneg field, then r2_screen_terms;
-// skip iff both terms are <= 0).
+// skip iff both terms are <= 0).  "f32xy": the same from the accumulator form
+// (X0 = (T + B) / 2, Y0 = (T - B) / 2, X1 = (A + AB) / 2, Y1 = (A - AB) / 2;
+// r2_screen_terms_xy).
 #include <cmath>
 #include <cstdio>
 #include <string>
@@ -16,7 +18,8 @@
 int main(int argc, char **argv) {
     if (argc != 3 && argc != 4) return 2;
     const bool f32 = argc == 4 && std::string(argv[3]) == "f32";
-    const bool f32g = argc == 4 && std::string(argv[3]) == "f32g";
+    const bool f32xy = argc == 4 && std::string(argv[3]) == "f32xy";
+    const bool f32g = f32xy || (argc == 4 && std::string(argv[3]) == "f32g");
     FILE *f = fopen(argv[1], "rb");
     if (!f) return 3;
     std::vector<double> rec;
@@ -34,7 +37,11 @@ int main(int argc, char **argv) {
             float E, mloc, t2;
             wld::screen_consts(Tg, R, E, mloc);
             const float thr_c = (float)r[5] * (1.0f - 0x1p-7f);
-            const float t1 = wld::r2_screen_terms((float)r[0], (float)r[1], (float)r[2], (float)r[3], R, thr_c, E, mloc, t2);
+            const float t1 =
+                f32xy ? wld::r2_screen_terms_xy((float)((r[0] + r[2]) / 2), (float)((r[0] - r[2]) / 2),
+                                                (float)((r[1] + r[3]) / 2), (float)((r[1] - r[3]) / 2), R, thr_c, E,
+                                                mloc, t2)
+                      : wld::r2_screen_terms((float)r[0], (float)r[1], (float)r[2], (float)r[3], R, thr_c, E, mloc, t2);
             out[i] = t1 <= 0.0f && t2 <= 0.0f ? 1 : 0;
         } else if (f32) {
             float R = (float)r[4];

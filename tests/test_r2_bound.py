@@ -24,13 +24,13 @@ def harness(tmp_path_factory):
                     "-I", os.path.join(REPO, "include"), "-I", os.path.join(REPO, "weightedld_amd", "csrc"),
                     "-x", "hip", os.path.join(REPO, "tests", "cpp", "bound_check.cpp"), "-o", exe], check=True)
 
-    def run(T, A, B, AB, R, thr, nonneg=True, f32=False, Tg=None):
+    def run(T, A, B, AB, R, thr, nonneg=True, f32=False, Tg=None, xy=False):
         n = len(T)
         last = float(nonneg) if Tg is None else Tg
         rec = np.stack([np.asarray(x, np.float64) * np.ones(n) for x in (T, A, B, AB, R, thr, last)], 1)
         d = tmp_path_factory.mktemp("io")
         rec.tofile(str(d / "in.bin"))
-        mode = ["f32g"] if Tg is not None else ["f32"] if f32 else []
+        mode = ["f32xy" if xy else "f32g"] if Tg is not None else ["f32"] if f32 else []
         subprocess.run([exe, str(d / "in.bin"), str(d / "out.bin")] + mode, check=True)
         return np.fromfile(str(d / "out.bin"), dtype=np.uint8).astype(bool)
     return run
@@ -220,4 +220,48 @@ def test_screen_launch_constants_near_threshold(harness, thr):
         for R in (0.0, 1.0, 17.5):
             for Tg in (float(T.max()), float(T.max()) * 2.0):
                 viol += int((harness(T, A, B, AB, R, thr, Tg=Tg) & passes).sum())
+    assert viol == 0
+
+
+@pytest.mark.parametrize("rare", [False, True])
+def test_screen_accumulator_form_sound(harness, rare):
+    # r2_screen_terms_xy (the screen kernel's form, from the X/Y accumulators):
+    # sound for any Tg >= T, and it decides like the (T, A, B, AB) form except
+    # where the differently rounded numerator lands on the other side.
+    rng = np.random.default_rng(53 + rare)
+    viol = diff = total = 0
+    for it in range(12):
+        n = 200_000
+        scale = float(2 ** rng.integers(10, 21))
+        c = screen_tables(rng, n, scale, rare)
+        T, A, B, AB = c.sum(0), c[0] + c[1], c[0] + c[2], c[0]
+        thr = float(np.float32(rng.choice([0.001, 0.01, 0.05, 0.2, 0.6])))
+        R = rng.choice([0.0, 1e-4, 1e-3, 1e-2]) * scale * rng.random()
+        e = rng.random((4, n)) * rng.choice([-1.0, 1.0], (4, n))
+        e = np.trunc(e / np.maximum(np.abs(e).sum(0), 1e-12) * R * rng.random(n))
+        h = 2 * (c + e)  # doubled sums: X = (T + B) / 2 etc. are integers
+        args = (h.sum(0), h[0] + h[1], h[0] + h[2], h[0], 2 * R, thr)
+        with np.errstate(invalid="ignore"):
+            passes = f32_r2(T, A, B, AB) > np.float32(thr)
+        for f in (1.0, 2.0):
+            Tg = float(h.sum(0).max()) * f
+            sx = harness(*args, Tg=Tg, xy=True)
+            sg = harness(*args, Tg=Tg)
+            viol += int((sx & passes).sum())
+            diff += int((sx != sg).sum())
+            total += n
+    assert viol == 0
+    assert diff <= total // 10000, (diff, total)
+
+
+@pytest.mark.parametrize("thr", [0.05, 0.3])
+def test_screen_accumulator_form_near_threshold(harness, thr):
+    rng = np.random.default_rng(int(thr * 1000) + 11)
+    viol = 0
+    for _ in range(6):
+        T, A, B, AB = near_threshold_tables(rng, 1_000_000, thr, scale=2.0 ** 21, window=0.05)
+        passes = f32_r2(T, A, B, AB) > np.float32(thr)
+        for R in (0.0, 1.0, 17.5):
+            for Tg in (2 * float(T.max()), 4 * float(T.max())):
+                viol += int((harness(2 * T, 2 * A, 2 * B, 2 * AB, 2 * R, thr, Tg=Tg, xy=True) & passes).sum())
     assert viol == 0

@@ -115,6 +115,22 @@ __host__ __device__ __forceinline__ float r2_screen_terms(float T, float A, floa
     t2 = mloc - mlo;
     return nub * nub - thr_c * ((m1 * m2) * (m3 * m4));
 }
+// The same terms straight from the i8 kernel's accumulators in doubled units
+// (X0 = S(raw), Y0 = S(minor) of channel_a "in", X1, Y1 of "major"; T = X0 +
+// Y0, B = X0 - Y0, A = X1 + Y1, AB = X1 - Y1, all exact): T - B = 2 Y0 and
+// A B - AB T = 2 (X0 Y1 - X1 Y0).  The marginals round exactly as in
+// r2_screen_terms; the numerator by one FMA (error <= 2u (X0 Y1 + X1 Y0) <= 2u
+// T^2, inside the 4.02u Tb^2 the derivation allows) and nub = fl(2 |num'| + E)
+// rounds once, as fl(|num| + E) did.
+__host__ __device__ __forceinline__ float r2_screen_terms_xy(float X0, float Y0, float X1, float Y1, float R,
+                                                             float thr_c, float E, float mloc, float &t2) {
+    const float T = X0 + Y0, B = X0 - Y0, A = X1 + Y1;
+    const float m1 = A - R, m2 = (T - A) - R, m3 = B - R, m4 = fmaf(2.0f, Y0, -R);
+    const float mlo = fminf(fminf(m1, m2), fminf(m3, m4));
+    const float nub = fmaf(2.0f, fabsf(fmaf(X0, Y1, -(X1 * Y0))), E);
+    t2 = mloc - mlo;
+    return nub * nub - thr_c * ((m1 * m2) * (m3 * m4));
+}
 __host__ __device__ __forceinline__ float r2_screen_violation(float T, float A, float B, float AB, float R,
                                                               float thr_c) {
     float E, mloc, t2;
