@@ -416,8 +416,9 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
             // f32 bound as a violation margin, branch-free; every pair valid
             // unless the tile touches the diagonal or a filtered/padding site
             // E and 2^-12 Tb fixed per launch from Tg = 2 sum |top digits| >= every
-            // doubled T (screen_consts); each term's f32 bits as an int: the
-            // maximum is > 0 iff some term is > 0 (finite terms: integer sums <= 2^22)
+            // doubled T (screen_consts); the terms straight from X/Y
+            // (r2_screen_terms_xy); each term's f32 bits as an int: the maximum
+            // is > 0 iff some term is > 0 (finite terms: integer sums <= 2^22)
             const float thr_c = thr * (1.0f - 0x1p-7f), R2 = 2.0f * sc.Rf;
             int worst = -1;
             const bool full = okA == ~0ull && okB == ~0ull && ta != tb;
@@ -426,8 +427,8 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
                 for (int i = 0; i < Acc::kPairs; ++i) {
                     const int2 p0 = acc.raw(0, i), p1 = acc.raw(1, i);  // (X, Y) of channel_a in, major
                     float t2;
-                    const float t1 = r2_screen_terms((float)(p0.x + p0.y), (float)(p1.x + p1.y), (float)(p0.x - p0.y),
-                                                     (float)(p1.x - p1.y), R2, thr_c, sc.E, sc.mloc, t2);
+                    const float t1 = r2_screen_terms_xy((float)p0.x, (float)p0.y, (float)p1.x, (float)p1.y, R2, thr_c,
+                                                        sc.E, sc.mloc, t2);
                     worst = max(worst, max(__float_as_int(t1), __float_as_int(t2)));
                 }
             } else {
@@ -435,8 +436,8 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
                 for (int i = 0; i < Acc::kPairs; ++i) {
                     const int2 p0 = acc.raw(0, i), p1 = acc.raw(1, i);
                     float t2;
-                    const float t1 = r2_screen_terms((float)(p0.x + p0.y), (float)(p1.x + p1.y), (float)(p0.x - p0.y),
-                                                     (float)(p1.x - p1.y), R2, thr_c, sc.E, sc.mloc, t2);
+                    const float t1 = r2_screen_terms_xy((float)p0.x, (float)p0.y, (float)p1.x, (float)p1.y, R2, thr_c,
+                                                        sc.E, sc.mloc, t2);
                     const uint32_t a_local = Acc::a_local(i, wave, lane);
                     const uint32_t b_local = Acc::b_local(i, wave, lane);
                     const bool valid =
