@@ -158,9 +158,15 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *                      exactly; none with a single nonzero plane, e.g. equal
  *                      weights) and only candidate 64x64 tiles are recomputed
  *                      with every plane — unless at this or a higher threshold
- *                      the screen left more than half the tiles as candidates
- *                      (then every tile goes to the full kernel directly);
- *                      2: always screen; 0: every tile, every plane.
+ *                      the screen left more than half the tiles as candidates.
+ *                      Then (three or more active planes) the screen runs on
+ *                      the top two planes, the planes below bounded the same
+ *                      way, unless at this or a higher threshold that left more
+ *                      than a fifth of the tiles as candidates (then every
+ *                      tile goes to the full kernel directly); 2: always the
+ *                      one-plane screen; 3: always the two-plane screen (the
+ *                      one-plane one with fewer than three active planes);
+ *                      0: every tile, every plane.
  *   WLD_OPT_TILE_ORDER 0 (default): L2/XCD-aware tile launch order; 1: plain
  *                      (a-tile, b-tile) order.
  *   WLD_OPT_ALL_PLANES 0 (default): all-zero digit planes are skipped; 1: the
@@ -342,7 +348,8 @@ typedef struct {
     uint64_t tiles;          /* 64x64 site tiles of the last run                   */
     uint64_t candidate_tiles;/* tiles computed with every plane (= tiles unless screened) */
     double screen_ms;        /* HIP-event time of the screen launch (0 if none)    */
-    int screened;            /* 1: the last run ran the one-plane i8 screen; 2: the fp4 screen; 0: none */
+    int screened;            /* 1: the last run ran the one-plane i8 screen; 2: the fp4 screen;
+                                3: the two-plane i8 screen; 0: none */
 } wld_run_stats;
 int wld_last_stats(wld_ctx *ctx, wld_run_stats *out);
 

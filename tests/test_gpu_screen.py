@@ -129,7 +129,8 @@ def check_exact_model(ctx, buf, w, dense=None):
 
 def _run(ctx, thr, prefilter, screen, wide=0, fp4=0):
     ctx.set_option("prefilter", prefilter)
-    ctx.set_option("screen", 2 if screen else 0)  # 2: screen even where auto would not
+    # 1 -> option 2: the one-plane screen even where auto would not; 3: two planes
+    ctx.set_option("screen", {0: 0, 1: 2, 3: 3}[screen])
     ctx.set_option("wide_screen", wide)
     ctx.set_option("screen_fp4", fp4)
     ctx.run(thr)
@@ -223,6 +224,12 @@ def test_prefilter_and_screen_never_change_rows(W, ctxs, case):
         scr, st = _run(ctx, thr, 1, 1, 1, 0)   # the i8 screen on 64x128 tiles
         f4, st4 = _run(ctx, thr, 1, 1, 0, 1)   # the fp4 screen
         dft, _ = _run(ctx, thr, 1, 1, 0, 2)    # fp4 auto
+        two, st2 = _run(ctx, thr, 1, 3)        # the two-plane i8 screen
+        _same_rows(two, ref)
+        if ctx.stats()["mfma_planes"] >= 3:
+            assert st2["screened"] == 3, st2
+            # the top two planes leave a residual 2^8 times smaller
+            assert st2["candidate_tiles"] <= stn["candidate_tiles"] + 2, (thr, st2, stn)
         _same_rows(pre, ref)
         _same_rows(scr, ref)
         _same_rows(nar, ref)
@@ -316,7 +323,11 @@ def test_screen_auto_policy(W, ctxs):
         seen.append((thr, st["screened"], st["candidate_tiles"], st["tiles"]))
         compare_rows(ctx.rows(), O.all_pairs(buf, w, np.float32(thr)), np.float32(thr), buf=buf, w=w)
     assert seen[0][1] == 1 and seen[0][2] * 2 > seen[0][3], seen
-    assert [x[1] for x in seen[1:]] == [0, 0, 1, 0, 1], seen
+    # 0.002 again: the two-plane screen (3), which leaves more than a fifth
+    # (r2 ~ 1/N: most tiles hold a pair above 0.002), so 0.001 goes straight
+    # to the full kernel; 0.003 is above the one-plane screen's bad threshold
+    assert seen[1][1] == 3 and seen[1][2] * 5 > seen[1][3], seen
+    assert [x[1] for x in seen[2:]] == [0, 1, 0, 1], seen
     ctx.set_option("screen", 2)
     rows2 = (ctx.run(0.001), ctx.rows(), ctx.stats()["screened"])
     ctx.set_option("screen", 0)
@@ -324,6 +335,31 @@ def test_screen_auto_policy(W, ctxs):
     ctx.set_option("screen", 1)
     assert rows2[2] == 1 and rows2[0] == rows0[0]
     _same_rows(rows2[1], rows0[1])
+
+
+def test_two_plane_screen_at_low_threshold(W, ctxs):
+    # BASELINE-style random data at thr 0.01 (r2 ~ 1/N, a few pairs per
+    # hundred tiles pass): the one-plane screen's residual leaves most tiles
+    # undecided, the two-plane screen only a small fraction; rows bit-identical
+    # to the unscreened kernel and equal to the oracle's.
+    ctx = _ctx(ctxs, "mfma")
+    buf = synth(3000, 2000, 31)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ctx.load(buf, w)
+    assert ctx.stats()["mfma_planes"] == 3
+    for thr in (0.01, 0.02):
+        full, _ = _run(ctx, thr, 1, 0)
+        one, st1 = _run(ctx, thr, 1, 1)
+        two, st2 = _run(ctx, thr, 1, 3)
+        _same_rows(one, full)
+        _same_rows(two, full)
+        assert st1["screened"] == 1 and st2["screened"] == 3, (st1, st2)
+        print("thr %g: candidates one-plane %d, two-plane %d of %d tiles; pair phase %.3f / %.3f ms" % (
+            thr, st1["candidate_tiles"], st2["candidate_tiles"], st2["tiles"], st1["pair_kernel_ms"],
+            st2["pair_kernel_ms"]))
+        assert st2["candidate_tiles"] * 5 < st2["tiles"], st2
+        assert st2["candidate_tiles"] < st1["candidate_tiles"], (st1, st2)
+        compare_rows(two, O.all_pairs(buf, w, np.float32(thr)), np.float32(thr), buf=buf, w=w)
 
 
 def test_screen_rejects_random_tiles(W, ctxs):

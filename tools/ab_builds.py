@@ -50,7 +50,8 @@ def child(path, config, reps, thr, unweighted=False):
         sx = ctx.stats()
         t.append(sx["pair_kernel_ms"])
         ts.append(sx.get("screen_ms", 0.0))
-    out = {"ms": t, "rows": rows, "screen_ms": sorted(ts)[len(ts) // 2]}
+    out = {"ms": t, "rows": rows, "screen_ms": sorted(ts)[len(ts) // 2], "cand": ctx.stats()["candidate_tiles"],
+           "screened": ctx.stats()["screened"]}
     ops = 8.0 * ctx.stats()["mfma_planes"] * ((N + 63) // 64 * 64) * (Ls * (Ls - 1) / 2)
     out["tops"] = ops / (sorted(t)[len(t) // 2] * 1e-3) / 1e12
     if st is not None:
@@ -98,7 +99,8 @@ def main():
             res.setdefault(name, {"ms": [], "rows": r["rows"]})["ms"] += r["ms"]
             res[name].setdefault("screen_ms", []).append(r.get("screen_ms", 0.0))
             print(json.dumps({"build": name, "median_ms": statistics.median(r["ms"]), "rows": r["rows"], "tops": r["tops"],
-                              "screen_ms": r.get("screen_ms"), "stamps": r.get("stamps_per_wave")}), flush=True)
+                              "screen_ms": r.get("screen_ms"), "cand": r.get("cand"),
+                              "screened": r.get("screened"), "stamps": r.get("stamps_per_wave")}), flush=True)
     for name, r in res.items():
         print(json.dumps({"build": name, "median_ms": statistics.median(r["ms"]), "min_ms": min(r["ms"]),
                           "screen_ms": statistics.median(r.get("screen_ms", [0.0])), "rows": r["rows"],

@@ -102,8 +102,9 @@ struct wld_ctx {
     int kernel_pref = WLD_KERNEL_AUTO;
     // wld_set_option (include/weightedld.h)
     bool opt_prefilter = true, opt_tile_rows = false, opt_all_planes = false;
-    int opt_screen = 1;             // WLD_OPT_SCREEN: 0 never, 1 auto (default), 2 always
+    int opt_screen = 1;             // WLD_OPT_SCREEN: 0 never, 1 auto (default), 2 always, 3 always two-plane
     float screen_bad_thr = -1.0f;   // auto: the largest threshold at which the screen left > half the tiles
+    float screen2_bad_thr = -1.0f;  // auto: ... at which the two-plane screen left > a fifth of them
     bool opt_wide_screen = false;  // WLD_OPT_WIDE_SCREEN: the i8 screen on 64x128 tiles (A/B: not faster)
     int opt_screen_fp4 = 0;        // WLD_OPT_SCREEN_FP4: 0 never (default: measured no faster), 1 always, 2 auto
     bool have_fp4 = false;         // frag4 holds this load's fp4 screen operands
@@ -137,7 +138,8 @@ struct wld_ctx {
     uint32_t tiles_lb = ~0u, tiles_le = ~0u;  // linear chunk range the tile list covers
     uint32_t n_tiles = 0, n_wtiles = 0;  // wtiles: the screen's wide tiles (kWideSecond)
     bool have_rows = false;
-    bool screened = false;  // the last pass ran the one-plane screen
+    bool screened = false;  // the last pass ran a screen
+    bool screened2 = false; // ... on two digit planes
     uint64_t rows = 0;
     wld_run_stats stats{};
 
@@ -497,7 +499,16 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         m.prefilter = c->opt_prefilter && thr > 0.0f;
         // auto: below a threshold at which the screen left more than half the
         // tiles as candidates, every tile goes straight to the full kernel
-        m.screen = m.prefilter && (c->opt_screen == 2 || (c->opt_screen == 1 && thr > c->screen_bad_thr));
+        m.screen = m.prefilter && (c->opt_screen >= 2 || (c->opt_screen == 1 && thr > c->screen_bad_thr));
+        // ... where the one-plane screen proved ineffective, the two-plane one
+        // (>= 3 active planes), unless it proved ineffective too
+        if (m.prefilter && !m.screen && c->opt_screen == 1 && thr > c->screen2_bad_thr) m.screen = m.screen2 = true;
+        if (c->opt_screen == 3) m.screen2 = true;
+        if (m.screen2 && (__builtin_popcount(c->plane_mask & 15) < 3 || c->fp4_used)) {
+            m.screen2 = false;  // one or two active planes: the one-plane screen or the full kernel
+            m.screen = c->opt_screen >= 2;
+        }
+        c->screened2 = m.screen && m.screen2;
         for (int t = 0; t < 3; ++t) m.resid[t] = c->wst.resid[t];
         for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
         m.cand_list = ptr<uint32_t>(c->cand);
@@ -596,9 +607,9 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
     switch (option) {
         case WLD_OPT_PREFILTER: c->opt_prefilter = value != 0; break;
         case WLD_OPT_SCREEN:
-            if (value < 0 || value > 2) return fail(WLD_E_ARG, "WLD_OPT_SCREEN takes 0, 1 or 2");
+            if (value < 0 || value > 3) return fail(WLD_E_ARG, "WLD_OPT_SCREEN takes 0, 1, 2 or 3");
             c->opt_screen = (int)value;
-            c->screen_bad_thr = -1.0f;
+            c->screen_bad_thr = c->screen2_bad_thr = -1.0f;
             break;
         case WLD_OPT_TILE_ORDER:
             c->opt_tile_rows = value != 0;
@@ -879,7 +890,7 @@ int enqueue_pass(wld_ctx *c) {
     c->run_dirty = true;  // until run_complete has seen this pass's scan
     const OrderArgs o = order_args(c);
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-    c->screened = false;
+    c->screened = c->screened2 = false;
     if (c->n_tiles) WLD_TRY(launch_pairs(c, r.thr, o, nullptr, &c->screened));
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     c->h_cnt[0] = c->h_cnt[1] = lin_count ? ~0ull : 0ull;
@@ -972,14 +983,19 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     c->stats.order_ms = event_ms(c->ev[3], c->ev[order_end]);
     c->stats.pair_kernel_launches = c->n_tiles ? (c->screened ? 2 : 1) : 0;
     c->stats.tiles = c->n_tiles;
-    c->stats.screened = c->screened ? (c->fp4_used ? 2 : 1) : 0;
+    c->stats.screened = c->screened ? (c->fp4_used ? 2 : c->screened2 ? 3 : 1) : 0;
     // auto: a threshold at which the fp4 bound leaves > 10% of the tiles to the
     // exact kernel is screened on i8 from now on (and every lower one)
     if (c->screened && c->fp4_used && h[2] * 10 > c->n_tiles) c->fp4_bad_thr = std::max(c->fp4_bad_thr, r.thr);
     // auto: a threshold at which even the i8 screen leaves more than half the
     // tiles is not screened from now on (nor any lower one): the screen costs a
     // third of the full three-plane kernel, the candidates as much again
-    if (c->screened && !c->fp4_used && h[2] * 2 > c->n_tiles) c->screen_bad_thr = std::max(c->screen_bad_thr, r.thr);
+    if (c->screened && !c->fp4_used && !c->screened2 && h[2] * 2 > c->n_tiles)
+        c->screen_bad_thr = std::max(c->screen_bad_thr, r.thr);
+    // ... and one at which the two-plane screen (0.8 of the full kernel's
+    // time at BASELINE config 4, profiles/r02s2/) leaves more than a fifth
+    // goes to the full kernel
+    if (c->screened && c->screened2 && h[2] * 5 > c->n_tiles) c->screen2_bad_thr = std::max(c->screen2_bad_thr, r.thr);
     c->stats.screen_ms = c->screened ? event_ms(c->ev[2], c->ev[6]) : 0.0;
     c->stats.candidate_tiles = c->screened ? h[2] : c->n_tiles;
     if (n_rows) *n_rows = rows;

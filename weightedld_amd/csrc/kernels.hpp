@@ -99,6 +99,7 @@ struct MfmaLaunch {
     int nonneg;
     bool prefilter;  // thr > 0: skip pairs r2_bound_skip rejects
     bool screen;     // with the prefilter: one-plane screen, then candidates
+    bool screen2;    // the screen on the top two digit planes (>= 3 active planes)
     uint64_t resid[3];
     uint64_t dsum[4];
     uint32_t *cand_list;   // n_tiles entries
@@ -116,8 +117,9 @@ void launch_screen_fp4(const uint8_t *frag4, const uint64_t *ok_bits, const uint
                        size_t LP, size_t NP, float thr, float R, const OrderArgs &o, uint32_t *cand_list,
                        unsigned *cand_count, hipStream_t s);
 
-// Enqueues the MFMA pair kernel(s) of one pass; returns true when the screen
-// ran (then screen_done, if given, is recorded between the two launches).
+// Enqueues the MFMA pair kernel(s) of one pass; returns true when a screen
+// (one- or two-plane) ran (then screen_done, if given, is recorded between
+// the two launches).
 bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *dense, hipStream_t s,
                       hipEvent_t screen_done);
 

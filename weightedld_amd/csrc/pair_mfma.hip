@@ -410,7 +410,9 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
         // sums in units of the screened digit plane, within R of the exact
         // sums scaled to that unit (cells: sum_c |e_c| <= R)
         bool cand = false;
-        if (sc.f32 == 2) {
+        // the f32 tests need one plane's sums (<= 128 NP); two planes
+        // (Acc::kPlanes == 2, the low-threshold screen) always take r2_bound_skip
+        if (Acc::kPlanes == 1 && sc.f32 == 2) {
             // doubled sums straight from the X/Y accumulators (raw(x, i) =
             // {2T, 2SB} / {2SA, 2SAB}: exact integers <= 256 NP <= 2^22), the
             // f32 bound as a violation margin, branch-free; every pair valid
@@ -446,7 +448,7 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
                 }
             }
             cand = worst > 0;
-        } else if (sc.f32) {
+        } else if (Acc::kPlanes == 1 && sc.f32) {
 #pragma unroll
             for (int i = 0; i < Acc::kPairs; ++i) {
                 const uint32_t a_local = Acc::a_local(i, wave, lane);
@@ -655,8 +657,13 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
         }
         const bool narrow = NP <= 65024u;
         auto sum = [&](int x, int y, int i) {
-            if constexpr (MODE == kModeScreen) {
+            if constexpr (MODE == kModeScreen && NPL == 1) {
                 return acc.get(x, 0, y, i);  // units of the screened plane (int, exact)
+            } else if constexpr (MODE == kModeScreen) {
+                // two-plane screen (planes lo, lo + 1 = plane_idx's two slots):
+                // units of plane lo, |S| <= 2^15 * 128 NP, exact in f64
+                static_assert(NPL == 2, "the screen runs on one or two planes");
+                return fma(256.0, (double)acc.get(x, 1, y, i), (double)acc.get(x, 0, y, i));
             } else if constexpr (NPL >= 3) {
                 // S = sum_p 2^(8p) acc_p, integers below 2^53, exact in f64.
                 // |acc_p| <= 128 NP, so acc_1 + 2^8 acc_2 (and acc_2 + 2^8 acc_3)
@@ -1074,6 +1081,23 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     // are exact (R = 0): it only moves the per-pair work to the cheap f32
     // bound, and the candidate launch (two-plane instantiation) adds an
     // all-zero plane.
+    if (m.screen2 && n >= 3) {
+        // Two-plane screen (low thresholds, where the top plane's residual
+        // leaves most tiles undecided): planes lo = top - 1 and top, sums in
+        // units of plane lo, the planes below lo bounded by resid[lo - 1]
+        // (top >= 2 with three or more active planes, so lo >= 1).  Per pair
+        // r2_bound_skip in f64; candidates then get every plane as below.
+        const uint32_t lo = top - 1;
+        sc.R = ldexp((double)m.resid[lo - 1], -8 * (int)lo);
+        sc.Rf = (float)sc.R;
+        if ((double)sc.Rf < sc.R) sc.Rf = nextafterf(sc.Rf, INFINITY);
+        sc.f32 = 0;
+        launch_lds<kModeScreen, 2>(m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, lo | (top << 2), o, dn, sc, s);
+        if (screen_done) (void)hipEventRecord(screen_done, s);
+        const uint32_t grid = std::min<uint32_t>(m.n_tiles, kCandidateGrid);
+        launch_lds_planes<kModePrefilter, true>(n, m, ok_bits, m.cand_list, 0, m.cand_count, grid, idx, o, dn, sc, s);
+        return true;
+    }
     sc.R = top > 0 ? ldexp((double)m.resid[top - 1], -8 * (int)top) : 0.0;
     if (n == 1) idx = top | ((top == 0 ? 1u : 0u) << 2);
     sc.Rf = (float)sc.R;
