@@ -556,8 +556,8 @@ def test_mfma_lds_pipeline_race_screen(W):
     dev = torch.device("cuda", 0)
     # reference: the site-major register kernel, every pair through the f32
     # epilogue (no prefilter, no screen); under test: the LDS kernel behind the
-    # one-plane screen (at 0.001 nearly every tile is a candidate: the looping
-    # candidate launch) with the prefilter
+    # one- and two-plane screens (at 0.001 nearly every tile is a candidate:
+    # the looping candidate launch) with the prefilter
     ref_ctx = W.Context(0, W.KERNEL_MFMA)
     ref_ctx.set_option("prefilter", 0)
     ref_ctx.set_option("mfma_layout", 1)
@@ -568,10 +568,12 @@ def test_mfma_lds_pipeline_race_screen(W):
     ctx = W.Context(0, W.KERNEL_MFMA)
     ctx.load(buf, w)
     assert n_ref > 10_000_000
-    for _ in range(4):
+    # forced: auto would send 0.001 to the full kernel after the first run
+    for mode, kind in ((2, 1), (3, 3), (2, 1), (3, 3)):
+        ctx.set_option("screen", mode)
         n = ctx.run(0.001)
         assert n == n_ref
-        assert ctx.stats()["screened"] in (1, 2)
+        assert ctx.stats()["screened"] == kind
         got = wdist.pack_rows_device(ctx, n, dev)
         assert torch.equal(got, ref)
 
