@@ -134,6 +134,11 @@ def main():
     ap.add_argument("--thr", type=float, help="override the config's r2 threshold (non-headline lines)")
     ap.add_argument("--rehearse-dist", action="store_true",
                     help="at N=1: run the N>1 step path (RCCL group of one, ShardStep/pipelined steps)")
+    ap.add_argument("--pipe-depth", type=int, default=2, metavar="D",
+                    help="N>1 (or --rehearse-dist): contexts of the pipelined step loop, D - 1 steps in flight")
+    ap.add_argument("--rehearse-shard", type=int, default=0, metavar="K",
+                    help="with --rehearse-dist: run rank 0's shard of a K-way split (the per-rank work at "
+                         "N=K; value counts that shard's pairs); a rehearsal line, never the headline")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one step at a time (N=1: no second context; N>1: one ShardStep at a time)")
     ap.add_argument("--no-screen", action="store_true",
@@ -220,6 +225,8 @@ def main():
     load_ms = ctx.stats()["load_ms"]
     # contiguous run of the reference chunk sequence, balanced by pairs (weightedld_amd/dist.py)
     cb, ce = ctx.shard_chunks(L, world, rank)
+    if args.rehearse_dist and args.rehearse_shard > 1:
+        cb, ce = ctx.shard_chunks(L, args.rehearse_shard, 0)
 
     from weightedld_amd import dist as wdist
 
@@ -242,9 +249,13 @@ def main():
     if not dist_on and pipelined:
         ctx1b = new_ctx()
     if dist_on and pipelined:
-        ctx2 = new_ctx()
-        pipe = wdist.PipelinedShardStep([ctx, ctx2], rank, world, device,
-                                        serialize_kernels=bool(os.environ.get("WLD_PIPE_SERIALIZE")))
+        pipe = wdist.PipelinedShardStep([ctx] + [new_ctx() for _ in range(max(2, args.pipe_depth) - 1)], rank, world,
+                                        device,
+                                        # "pair" (default): step i's pair kernel waits on the device for
+                                        # step i-1's (wld_run_after); 0: may overlap it; 1: waits for
+                                        # step i-1's whole run (profiles/r02pc/)
+                                        serialize_kernels={"0": False, "1": True}.get(
+                                            os.environ.get("WLD_PIPE_SERIALIZE", "pair"), "pair"))
 
     def nrows(res):
         return int(res[1].shape[1]) if res is not None and res[1] is not None else 0
@@ -266,6 +277,8 @@ def main():
                 c = cs[i & 1]
                 if prev is not None and r > 0:
                     r, prev = prev.run_wait(), None
+                if prev is not None:
+                    c.run_after(prev)  # this pair kernel queued behind the previous one (device wait)
                 c.run_chunks_async(thr, cb, ce)
                 if prev is not None:
                     r = prev.run_wait()
@@ -344,8 +357,11 @@ def main():
         return
 
     total_pairs = L * (L - 1) // 2
-    value = total_pairs * args.steps / elapsed
     shard_pairs = ctx.pairs_in_chunks(L, cb, ce)
+    if args.rehearse_dist and args.rehearse_shard > 1:
+        total_pairs = shard_pairs  # one rank's shard of a K-way split, timed alone
+        desc += " (rehearsal: rank 0's shard of %d)" % args.rehearse_shard
+    value = total_pairs * args.steps / elapsed
     # Roofline of the dominant kernel: ALGORITHMIC work per
     # launch, SURVEY 8(d)'s 4 masked multiply-adds per (pair, sequence) =
     # 8 N ops per pair, over the launch's HIP-event time.  Screened runs: the

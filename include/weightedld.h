@@ -311,6 +311,14 @@ int wld_run_chunks(wld_ctx *ctx, float r2_threshold, uint32_t chunk_begin, uint3
 int wld_run_chunks_async(wld_ctx *ctx, float r2_threshold, uint32_t chunk_begin, uint32_t chunk_end,
                          void *d_count_out);
 int wld_run_wait(wld_ctx *ctx, uint64_t *n_rows);
+/* Orders ctx's next run after prev's enqueued one on the device, no host wait:
+ * ctx's stream waits until prev's pair kernels (for a screened pass: its
+ * screen kernel) have completed; prev's candidate launch, row count and
+ * assembly may still overlap ctx's kernels.  For callers that pipeline runs
+ * over several contexts (the N>1 step loop): one pair kernel at a time with
+ * the next one already queued.  A no-op when prev has no run in flight;
+ * WLD_E_STATE when ctx has one; WLD_E_ARG for device groups. */
+int wld_run_after(wld_ctx *ctx, wld_ctx *prev);
 /* The context's HIP stream (hipStream_t), for ordering caller work after a run. */
 void *wld_stream(wld_ctx *ctx);
 /* All pairs of the loaded set, any size, rows to host: runs the reference's

@@ -98,6 +98,9 @@ class OracleShardContext:
         if d_count_ptr:
             ctypes.c_int64.from_address(d_count_ptr).value = len(self.rows["r2"])
 
+    def run_after(self, prev):  # device-side ordering: program order on the host
+        pass
+
     def run_wait(self):
         assert self.pending, "run_wait with nothing in flight"
         self.pending = False
@@ -139,13 +142,15 @@ def _step_worker(rank, world, port, L, N, thrs, pipelined, q):
         lo, hi = wdist.shard_chunks(L, world, rank)
         results = []
         if pipelined:
-            pipe = wdist.PipelinedShardStep([OracleShardContext(buf, w), OracleShardContext(buf, w)], rank, world,
-                                            "cpu")
+            depth, mode = int(str(pipelined)[0]), ("pair" if str(pipelined).endswith("pair") else False)
+            pipe = wdist.PipelinedShardStep([OracleShardContext(buf, w) for _ in range(depth)], rank, world,
+                                            "cpu", serialize_kernels=mode)
             for t in thrs:
                 r = pipe.submit(t, lo, hi)
                 if r is not None:
                     results.append(r)
-            results.append(pipe.drain())
+            results += pipe.drain_all()
+            assert pipe.drain() is None
         else:
             step = wdist.ShardStep(OracleShardContext(buf, w), rank, world, "cpu")
             results = [step(t, lo, hi) for t in thrs]
@@ -165,13 +170,13 @@ def _step_worker(rank, world, port, L, N, thrs, pipelined, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pipelined", [False, True], ids=["step", "pipelined"])
+@pytest.mark.parametrize("pipelined", [0, 2, 3, "3pair"], ids=["step", "pipelined2", "pipelined3", "pipelined3pair"])
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_gloo_shard_steps_match_unsharded(world, pipelined):
     """ShardStep / PipelinedShardStep (the bench's N>1 step path) at world
     2-4 under gloo: per step, the count exchange, the row gather issued only
     when some rank has rows, and (pipelined) step i-1's gather issued after
-    step i's count exchange — every step's gathered rows equal the unsharded
+    step i's count exchange; depth 3: two steps in flight) — every step's gathered rows equal the unsharded
     oracle's, in reference order, with threshold sequences where no rank,
     one rank or every rank has rows, and nothing deadlocks."""
     L, N = 1200, 200

@@ -673,8 +673,8 @@ def test_shard_step_world1_rccl(W, ctxs):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("serialize", [False, True])
-def test_pipelined_shard_step_world1_rccl(W, serialize):
+@pytest.mark.parametrize("serialize,depth", [(False, 2), (True, 2), ("pair", 2), ("pair", 3), (False, 3)])
+def test_pipelined_shard_step_world1_rccl(W, serialize, depth):
     # PipelinedShardStep (the bench's N>1 timed loop): two contexts on the same
     # inputs, step i's kernel queued behind step i-1's on the device while
     # step i-1 completes.  Every step's rows equal the oracle's, in order,
@@ -686,7 +686,7 @@ def test_pipelined_shard_step_world1_rccl(W, serialize):
     L, N = 700, 256
     buf = synth(L, N, 79)
     w = np.random.default_rng(8).random(N).astype(np.float32) + 0.1
-    ctxs2 = [W.Context(0, W.KERNEL_MFMA), W.Context(0, W.KERNEL_MFMA)]
+    ctxs2 = [W.Context(0, W.KERNEL_MFMA) for _ in range(depth)]
     for c in ctxs2:
         c.load(buf, w)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -700,10 +700,10 @@ def test_pipelined_shard_step_world1_rccl(W, serialize):
         results = []
         for i, t in enumerate(thrs):
             r = pipe.submit(t, 0, 0)
-            assert (r is None) == (i == 0)
+            assert (r is None) == (i < depth - 1)
             if r is not None:
                 results.append(r)
-        results.append(pipe.drain())
+        results += pipe.drain_all()
         assert pipe.drain() is None
         assert len(results) == len(thrs)
         for t, (n, rows) in zip(thrs, results):

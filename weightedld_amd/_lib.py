@@ -121,6 +121,7 @@ SIGNATURES = {
     "wld_run_chunks": (_int, [_vp, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint32, _u64p]),
     "wld_run_chunks_async": (_int, [_vp, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint32, _vp]),
     "wld_run_wait": (_int, [_vp, _u64p]),
+    "wld_run_after": (_int, [_vp, _vp]),
     "wld_stream": (_vp, [_vp]),
     "wld_run_host": (_int, [_vp, ctypes.c_float, PROGRESS_FN, _vp, ctypes.POINTER(Pairs)]),
     "wld_rows_device": (_int, [_vp, ctypes.POINTER(Pairs)]),

@@ -317,6 +317,11 @@ class Context:
         check(lib().wld_run_wait(self._h, ctypes.byref(n)), "wld_run_wait")
         return int(n.value)
 
+    def run_after(self, prev):
+        """wld_run_after: this context's next run waits on the device for the
+        pair kernels of prev's run in flight (no host wait)."""
+        check(lib().wld_run_after(self._h, prev._h), "wld_run_after")
+
     def run_host(self, r2_threshold, progress_report=None):
         """wld_run_host: every pair of the loaded set, in batches of <= 2^31
         pairs, rows to host in reference order (a PairStore)."""

@@ -1042,6 +1042,18 @@ int wld_run_wait(wld_ctx *c, uint64_t *n_rows) {
     return run_complete(c, n_rows);
 }
 
+int wld_run_after(wld_ctx *c, wld_ctx *prev) {
+    if (!c || !prev) return fail(WLD_E_ARG, "null context");
+    if (!c->members.empty() || !prev->members.empty()) return fail(WLD_E_ARG, "wld_run_after on a device group");
+    if (c->pend.active) return fail(WLD_E_STATE, "wld_run_after during a run of ctx");
+    if (!prev->pend.active) return WLD_OK;  // nothing in flight
+    WLD_TRY(set_dev(c));
+    // ev[6] separates a screened pass's screen from its candidate launch;
+    // ev[3] follows the pair kernel(s) (enqueue_pass)
+    HIP_TRY(hipStreamWaitEvent(c->stream, prev->screened ? prev->ev[6] : prev->ev[3], 0));
+    return WLD_OK;
+}
+
 void *wld_stream(wld_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
 int wld_rows_device(wld_ctx *c, wld_pairs *v) {

@@ -10,6 +10,7 @@ backend; gloo in the CPU tests).  Because chunk rows DESCEND in the reference's
 triu_index order (lib.rs:623-632), rank 0 concatenates the shards in
 descending rank order.
 """
+import collections
 import contextlib
 
 import numpy as np
@@ -174,44 +175,61 @@ class ShardStep:
 
 
 class PipelinedShardStep:
-    """Back-to-back ShardSteps on two contexts loaded with the same inputs
-    (double-buffered staging and counts).  Step i runs on context i % 2, so
-    step i-1's count exchange, host read and (if any rank has rows) row gather
-    overlap step i's kernel, and step i's kernel may start in the tail of step
-    i-1's (the contexts share nothing the kernels write).  serialize_kernels=True
-    makes step i's kernel wait on the device (an event, no host wait) for step
-    i-1's, so kernels run one at a time; that is also done while the last
-    finished step had rows, so a step's row copies and gather do not compete
-    with two kernels.  submit() returns step i-1's result (None for the first step);
-    drain() completes the last one.  Collectives are issued in step order on
-    every rank."""
+    """Back-to-back ShardSteps on D >= 2 contexts loaded with the same inputs
+    (D-buffered staging and counts).  Step i runs on context i % D and up to
+    D - 1 steps are in flight: submit() enqueues step i, then completes the
+    oldest step once more than D - 1 are pending, so that step's count
+    exchange, host read and (if any rank has rows) row gather overlap the
+    kernels queued behind it.  serialize_kernels=False lets step i's kernel
+    start in the tail of step i-1's (the contexts share nothing the kernels
+    write); True makes it wait on the device (an event, no host wait) for
+    step i-1's whole run (pair kernels, row count, count all_gather); "pair"
+    only for step i-1's pair kernel (wld_run_after: the small kernels after
+    it overlap step i's), so pair kernels run one at a time with the next
+    already queued.  The full wait is also done while the last finished step
+    had rows, so a step's row copies and gather do not compete with two
+    kernels.  submit() returns the
+    completed step's result (None while the pipeline fills); drain_all()
+    completes the pending steps and returns their results in step order,
+    drain() the last of them (or None).  Collectives are issued in step order
+    on every rank (count all_gathers in submit order, a step's row gather when
+    it completes), so the sequence is the same everywhere."""
 
     def __init__(self, ctxs, rank, world, device, group=None, serialize_kernels=False):
         import torch
 
-        assert len(ctxs) == 2
+        assert len(ctxs) >= 2
         self.steps = [ShardStep(c, rank, world, device, group) for c in ctxs]
-        self.done = ([torch.cuda.Event(), torch.cuda.Event()] if torch.device(device).type == "cuda"
-                     else [_HostEvent(), _HostEvent()])
+        self.done = ([torch.cuda.Event() for _ in ctxs] if torch.device(device).type == "cuda"
+                     else [_HostEvent() for _ in ctxs])
         self.serialize = serialize_kernels  # False: step i's kernel may start in step i-1's tail
         self.i = 0
-        self.pending = None
+        self.pending = collections.deque()  # contexts of the enqueued, unfinished steps, oldest first
 
     def submit(self, thr, chunk_begin, chunk_end):
-        k = self.i & 1
-        prev = self.pending
-        if prev is not None and (self.serialize or any(st.rows_seen for st in self.steps)):
-            self.steps[k].stream.wait_event(self.done[prev])
+        D = len(self.steps)
+        k = self.i % D
+        assert k not in self.pending  # step i - D completed in an earlier submit
+        if self.pending:
+            prev = self.pending[-1]
+            if any(st.rows_seen for st in self.steps) or (self.serialize and self.serialize != "pair"):
+                self.steps[k].stream.wait_event(self.done[prev])
+            elif self.serialize == "pair":
+                self.steps[k].ctx.run_after(self.steps[prev].ctx)
         self.steps[k].enqueue(thr, chunk_begin, chunk_end, self.done[k])
         self.i += 1
-        self.pending = k
-        return self.steps[prev].finish() if prev is not None else None
+        self.pending.append(k)
+        return self.steps[self.pending.popleft()].finish() if len(self.pending) > D - 1 else None
+
+    def drain_all(self):
+        out = []
+        while self.pending:
+            out.append(self.steps[self.pending.popleft()].finish())
+        return out
 
     def drain(self):
-        if self.pending is None:
-            return None
-        k, self.pending = self.pending, None
-        return self.steps[k].finish()
+        out = self.drain_all()
+        return out[-1] if out else None
 
 
 def gather_rows(packed, rank, world, group=None):
