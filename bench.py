@@ -404,13 +404,17 @@ def main():
     roof["pair_phase_ms"] = kernel_ms
     roof["pair_phase_frac"] = alg_ops / (kernel_ms * 1e-3) / 1e12 / roof["peak"]
     if screened:
-        roof["screen"] = {"kind": "fp4" if screen_kind == 2 else "i8", "tiles": n_tiles,
+        roof["screen"] = {"kind": {2: "fp4", 3: "i8 two-plane"}.get(screen_kind, "i8"), "tiles": n_tiles,
                           "candidate_tiles": float(np.mean(cand)),
                           "candidate_launch_ms": kernel_ms - screen_ms, "unscreened_pair_kernel_ms": unscreened_ms,
                           "i8_screen_ms": i8_screen_ms,
                           "unscreened_frac": alg_ops / (unscreened_ms * 1e-3) / 1e12 / roof["peak"]}
+    # PMC traffic (profiles/traffic.json) was measured on the default C4 line's
+    # dominant kernel (the one-plane i8 screen); other lines report null
     tr = load_traffic(args.config + ("-unweighted" if args.unweighted else ""), kern_name)
-    roof["traffic"] = tr.get("hbm_bytes_per_launch") if tr else None
+    same_kernel = (screen_kind == 1 and args.thr is None and not args.wide_screen and not args.wide_weights
+                   and not (args.rehearse_dist and args.rehearse_shard > 1))
+    roof["traffic"] = tr.get("hbm_bytes_per_launch") if tr and same_kernel else None
     hbm_alg = shard_pairs * 2.0 * N / (kernel_ms * 1e-3) / 1e9  # 2N bytes per pair
     if kern_name == "mfma":
         dtype = ("i8 digit planes of 24-bit fixed-point weights (%d plane%s), exact i32 sums, f32 epilogue"

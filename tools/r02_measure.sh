@@ -15,6 +15,8 @@ tools/gpu_step.sh 200 $out/bench_c4_unweighted.log python bench.py --unweighted 
 tools/gpu_step.sh 200 $out/bench_c4_wide.log python bench.py --wide-weights --no-cpu-baseline || exit $?
 tools/gpu_step.sh 200 $out/bench_c4_valu.log python bench.py --kernel valu --steps 5 --warmup 1 --no-cpu-baseline || exit $?
 tools/gpu_step.sh 300 $out/bench_c5.log python bench.py --config c5 --steps 10 --warmup 3 --no-cpu-baseline || exit $?
+tools/gpu_step.sh 200 $out/bench_c4_rehearse.log python bench.py --rehearse-dist --no-cpu-baseline || exit $?
+tools/gpu_step.sh 200 $out/bench_c4_rehearse_s8.log python bench.py --rehearse-dist --rehearse-shard 8 --no-cpu-baseline || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o c4_nopipe -- \
   python3 bench.py --no-pipeline --steps 50 --warmup 5 --no-cpu-baseline > $out/prof.log 2>&1 || { echo "rocprof failed $?"; exit 1; }
 echo done
