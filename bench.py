@@ -134,6 +134,8 @@ def main():
     ap.add_argument("--thr", type=float, help="override the config's r2 threshold (non-headline lines)")
     ap.add_argument("--rehearse-dist", action="store_true",
                     help="at N=1: run the N>1 step path (RCCL group of one, ShardStep/pipelined steps)")
+    ap.add_argument("--tile-rows", action="store_true",
+                    help="plain (a-tile, b-tile) launch order instead of the XCD-aware one (WLD_OPT_TILE_ORDER 1; same rows)")
     ap.add_argument("--pipe-depth", type=int, default=2, metavar="D",
                     help="N>1 (or --rehearse-dist): contexts of the pipelined step loop, D - 1 steps in flight")
     ap.add_argument("--rehearse-shard", type=int, default=0, metavar="K",
@@ -218,6 +220,8 @@ def main():
             c.set_option("wide_screen", 1)
         if args.fp4_screen:
             c.set_option("screen_fp4", 1)
+        if args.tile_rows:
+            c.set_option("tile_order", 1)
         c.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
         return c
 
