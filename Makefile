@@ -13,7 +13,7 @@ ARCH ?= gfx950
 PKG := weightedld_amd
 CSRC := $(PKG)/csrc
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Iinclude -I$(CSRC)
-HIP_SRCS := $(CSRC)/encode.hip $(CSRC)/prepass.hip $(CSRC)/pair_valu.hip $(CSRC)/pair_mfma.hip $(CSRC)/screen_fp4.hip \
+HIP_SRCS := $(CSRC)/encode.hip $(CSRC)/prepass.hip $(CSRC)/pair_valu.hip $(CSRC)/pair_mfma.hip \
             $(CSRC)/order.hip $(CSRC)/capi.hip
 CXX_SRCS := $(CSRC)/host.cpp
 HDRS := include/weightedld.h $(CSRC)/common.hpp $(CSRC)/kernels.hpp $(CSRC)/pair_common.hpp

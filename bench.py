@@ -32,7 +32,6 @@ CONFIGS = {
 }
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 I8_MFMA_PEAK_TOPS = 5000.0  # dense i8 MFMA = 2x bf16 dense 2.5 PF (MI355X_MICROARCH.md Matrix cores)
-FP4_MFMA_PEAK_TOPS = 10000.0  # dense block-scaled fp4 (e2m1) MFMA = 4x bf16 dense (MI355X_MICROARCH.md Matrix cores)
 F32_VALU_PEAK_TFLOPS = 157.3  # FP32 vector peak (spec) = f32-input MFMA peak
 
 
@@ -145,10 +144,6 @@ def main():
                     help="one step at a time (N=1: no second context; N>1: one ShardStep at a time)")
     ap.add_argument("--no-screen", action="store_true",
                     help="every tile with every weight-digit plane (WLD_OPT_SCREEN 0; same rows)")
-    ap.add_argument("--fp4-screen", action="store_true",
-                    help="the screen on fp4 matrix cores (WLD_OPT_SCREEN_FP4 1; same rows)")
-    ap.add_argument("--wide-screen", action="store_true",
-                    help="the i8 screen on 64x128 tiles (WLD_OPT_WIDE_SCREEN 1; same rows)")
     ap.add_argument("--no-prefilter", action="store_true",
                     help="every pair through the f32 epilogue (WLD_OPT_PREFILTER 0, implies --no-screen; same rows)")
     args = ap.parse_args()
@@ -216,10 +211,6 @@ def main():
             c.set_option("screen", 0)
         if args.no_prefilter:
             c.set_option("prefilter", 0)
-        if args.wide_screen:
-            c.set_option("wide_screen", 1)
-        if args.fp4_screen:
-            c.set_option("screen_fp4", 1)
         if args.tile_rows:
             c.set_option("tile_order", 1)
         c.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
@@ -319,21 +310,12 @@ def main():
         sms.append(st["screen_ms"])
         cand.append(st["candidate_tiles"])
         gms.append((time.perf_counter() - tg) * 1e3 - st["pair_kernel_ms"])
-    screen_kind = ctx.stats()["screened"]  # 0 none, 1 i8 one-plane screen, 2 fp4 screen
+    screen_kind = ctx.stats()["screened"]  # 0 none, 1 i8 one-plane screen, 3 two-plane screen
     screened = bool(screen_kind)
     n_tiles = ctx.stats()["tiles"]
     # the same steps without the screen (every tile, every plane; same rows),
     # reported alongside: a few sequential runs after the timed region
     unscreened_ms = None
-    i8_screen_ms = None
-    if screen_kind == 2:  # the i8 screen on the same steps, for the record
-        ctx.set_option("screen_fp4", 0)
-        ims = []
-        for _ in range(5):
-            step()
-            ims.append(ctx.stats()["screen_ms"])
-        ctx.set_option("screen_fp4", 1)
-        i8_screen_ms = float(np.mean(ims[1:]))
     if screened:
         ctx.set_option("screen", 0)
         ums = []
@@ -374,27 +356,22 @@ def main():
     # candidate launch recomputes the few tiles it cannot reject.
     alg_ops = shard_pairs * 8.0 * N
     if kern_name == "mfma":
-        # the dominant kernel's peak: dense fp4 MFMA for the fp4 screen, dense
-        # i8 MFMA otherwise (no sparsity in either)
-        peak, unit = (FP4_MFMA_PEAK_TOPS if screen_kind == 2 else I8_MFMA_PEAK_TOPS), "TFLOP/s"
+        # the dominant kernel's peak: dense i8 MFMA (no sparsity)
+        peak, unit = I8_MFMA_PEAK_TOPS, "TFLOP/s"
         dom_ms = screen_ms if screened else kernel_ms
         achieved = alg_ops / (dom_ms * 1e-3) / 1e12
-        if screen_kind == 2:
-            kname = "screen_fp4_kernel (64x128 tiles, e2m1 weights, f32 sums)"
-        elif screened:
-            kname = ("pair_screen_kernel (64x128 tiles, 1 plane)" if args.wide_screen else
-                     "pair_mfma_kernel<screen,1 plane>")
+        if screened:
+            kname = "pair_mfma_kernel<screen,%d plane%s>" % ((2, "s") if screen_kind == 3 else (1, ""))
         else:
             kname = "pair_mfma_kernel<%d planes>" % planes
         roof = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak,
                 "work": "algorithmic: 8*N ops per site pair (4 masked weighted sums)",
                 "kernel": kname, "kernel_ms": dom_ms}
         # what the matrix cores executed: P digit planes x 8 N per pair (one
-        # fp4 or one i8 plane when screened)
-        ex_planes = 1 if screened else planes
+        # or two i8 planes when screened)
+        ex_planes = (2 if screen_kind == 3 else 1) if screened else planes
         roof["executed_frac"] = shard_pairs * 8.0 * ex_planes * N / (dom_ms * 1e-3) / 1e12 / peak
-        roof["executed_work"] = ("fp4 operands, 8*N ops per pair" if screen_kind == 2 else
-                                 "%d i8 digit plane(s) x 8*N ops per pair" % ex_planes)
+        roof["executed_work"] = "%d i8 digit plane(s) x 8*N ops per pair" % ex_planes
         # against the i8 peak as well (the integer kernels' roofline)
         roof["frac_of_i8_peak"] = achieved / I8_MFMA_PEAK_TOPS
     else:
@@ -408,23 +385,20 @@ def main():
     roof["pair_phase_ms"] = kernel_ms
     roof["pair_phase_frac"] = alg_ops / (kernel_ms * 1e-3) / 1e12 / roof["peak"]
     if screened:
-        roof["screen"] = {"kind": {2: "fp4", 3: "i8 two-plane"}.get(screen_kind, "i8"), "tiles": n_tiles,
+        roof["screen"] = {"kind": {3: "i8 two-plane"}.get(screen_kind, "i8"), "tiles": n_tiles,
                           "candidate_tiles": float(np.mean(cand)),
                           "candidate_launch_ms": kernel_ms - screen_ms, "unscreened_pair_kernel_ms": unscreened_ms,
-                          "i8_screen_ms": i8_screen_ms,
                           "unscreened_frac": alg_ops / (unscreened_ms * 1e-3) / 1e12 / roof["peak"]}
     # PMC traffic (profiles/traffic.json) was measured on the default C4 line's
     # dominant kernel (the one-plane i8 screen); other lines report null
     tr = load_traffic(args.config + ("-unweighted" if args.unweighted else ""), kern_name)
-    same_kernel = (screen_kind == 1 and args.thr is None and not args.wide_screen and not args.wide_weights
+    same_kernel = (screen_kind == 1 and args.thr is None and not args.wide_weights
                    and not (args.rehearse_dist and args.rehearse_shard > 1))
     roof["traffic"] = tr.get("hbm_bytes_per_launch") if tr and same_kernel else None
     hbm_alg = shard_pairs * 2.0 * N / (kernel_ms * 1e-3) / 1e9  # 2N bytes per pair
     if kern_name == "mfma":
         dtype = ("i8 digit planes of 24-bit fixed-point weights (%d plane%s), exact i32 sums, f32 epilogue"
                  % (planes, "s" if planes > 1 else ""))
-        if screen_kind == 2:
-            dtype = ("screen: fp4 (e2m1) weights, exact f32 sums, rigorous r2 bound; rows: " + dtype)
     else:
         dtype = "f32"
     out = {

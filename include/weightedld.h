@@ -125,7 +125,8 @@ int wld_create(int device, wld_ctx **out);
  * concatenated in descending shard order).  Options and the kernel choice
  * apply to every member; wld_last_stats reports member 0's kernel with the
  * group's pair/row totals.  Other device entry points fail with WLD_E_STATE
- * on such a context.  With n_devices == 1 it behaves like wld_create. */
+ * on such a context.  With n_devices == 1 it returns a plain single-device
+ * context (wld_create(devices[0], out)), on which every entry point works. */
 int wld_create_multi(const int *devices, int n_devices, wld_ctx **out);
 int wld_n_devices(const wld_ctx *ctx); /* 1, or the member count of a multi-device context */
 void wld_destroy(wld_ctx *ctx);
@@ -179,17 +180,8 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *   WLD_OPT_STAGING_ROWS   initial staging capacity in rows (default 2^25;
  *                      grown on overflow by a re-run).
  *   WLD_OPT_HOST_BATCH_PAIRS  pairs per batch of wld_run_host (default 2^31).
- *   WLD_OPT_SCREEN_FP4 0 (default): the i8 one-plane screen; 2 (auto): with
- *                      nonnegative weights the screen runs on fp4 matrix cores
- *                      (weights rounded to e2m1, the rounding bounded exactly),
- *                      unless at this or a higher threshold it left > 10% of
- *                      the tiles as candidates (then the i8 screen); 1: the fp4
- *                      screen whenever possible.  The fp4 operands are built at
- *                      load when this is not 0 (measured: as fast as the i8
- *                      screen at BASELINE config 4, 1.5% slower at config 5).
- *   WLD_OPT_WIDE_SCREEN 0 (default): the one-plane i8 screen on 64x64 tiles;
- *                      1: on 64x128 tiles (two 64x64 tiles per workgroup,
- *                      f32 bound only; measured no faster). */
+ *                      (Ids 9 and 10, an experimental 64x128-tile screen and an fp4
+ *                      screen of round 2, are retired: WLD_E_ARG.) */
 #define WLD_OPT_PREFILTER 1
 #define WLD_OPT_SCREEN 2
 #define WLD_OPT_TILE_ORDER 3
@@ -198,8 +190,6 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
 #define WLD_OPT_VALU_PLAIN 6
 #define WLD_OPT_STAGING_ROWS 7
 #define WLD_OPT_HOST_BATCH_PAIRS 8
-#define WLD_OPT_WIDE_SCREEN 9
-#define WLD_OPT_SCREEN_FP4 10
 int wld_set_option(wld_ctx *ctx, int option, int64_t value);
 int wld_get_option(wld_ctx *ctx, int option, int64_t *value);
 
@@ -356,8 +346,8 @@ typedef struct {
     uint64_t tiles;          /* 64x64 site tiles of the last run                   */
     uint64_t candidate_tiles;/* tiles computed with every plane (= tiles unless screened) */
     double screen_ms;        /* HIP-event time of the screen launch (0 if none)    */
-    int screened;            /* 1: the last run ran the one-plane i8 screen; 2: the fp4 screen;
-                                3: the two-plane i8 screen; 0: none */
+    int screened;            /* 1: the last run ran the one-plane i8 screen; 3: the two-plane
+                                i8 screen; 0: none */
 } wld_run_stats;
 int wld_last_stats(wld_ctx *ctx, wld_run_stats *out);
 

@@ -127,18 +127,14 @@ def check_exact_model(ctx, buf, w, dense=None):
     return int(m.sum())
 
 
-def _run(ctx, thr, prefilter, screen, wide=0, fp4=0):
+def _run(ctx, thr, prefilter, screen):
     ctx.set_option("prefilter", prefilter)
     # 1 -> option 2: the one-plane screen even where auto would not; 3: two planes
     ctx.set_option("screen", {0: 0, 1: 2, 3: 3}[screen])
-    ctx.set_option("wide_screen", wide)
-    ctx.set_option("screen_fp4", fp4)
     ctx.run(thr)
     rows, st = ctx.rows(), ctx.stats()
     ctx.set_option("prefilter", 1)
     ctx.set_option("screen", 1)
-    ctx.set_option("wide_screen", 0)
-    ctx.set_option("screen_fp4", 0)
     return rows, st
 
 
@@ -202,7 +198,6 @@ def test_prefilter_and_screen_never_change_rows(W, ctxs, case):
         neg = rng.random(600) < 0.1
         w[neg] = -(0.1 + 0.2 * rng.random(int(neg.sum()))).astype(np.float32)
         thrs = [0.01, 0.05, 0.2]
-    ctx.set_option("screen_fp4", 2)  # build the fp4 screen's operands at load
     ctx.load(buf, w)
     assert ctx.stats()["kernel"] == W.KERNEL_MFMA
     # thresholds on the pairs' own r2 values: rows sitting exactly on the cut
@@ -220,31 +215,15 @@ def test_prefilter_and_screen_never_change_rows(W, ctxs, case):
     for thr in thrs:
         ref, _ = _run(ctx, thr, 0, 0)       # every pair through the f32 epilogue
         pre, _ = _run(ctx, thr, 1, 0)       # prefilter only
-        nar, stn = _run(ctx, thr, 1, 1, 0, 0)  # the i8 screen on 64x64 tiles
-        scr, st = _run(ctx, thr, 1, 1, 1, 0)   # the i8 screen on 64x128 tiles
-        f4, st4 = _run(ctx, thr, 1, 1, 0, 1)   # the fp4 screen
-        dft, _ = _run(ctx, thr, 1, 1, 0, 2)    # fp4 auto
+        scr, st = _run(ctx, thr, 1, 1)         # the one-plane i8 screen
         two, st2 = _run(ctx, thr, 1, 3)        # the two-plane i8 screen
         _same_rows(two, ref)
         if ctx.stats()["mfma_planes"] >= 3:
             assert st2["screened"] == 3, st2
             # the top two planes leave a residual 2^8 times smaller
-            assert st2["candidate_tiles"] <= stn["candidate_tiles"] + 2, (thr, st2, stn)
+            assert st2["candidate_tiles"] <= st["candidate_tiles"] + 2, (thr, st2, st)
         _same_rows(pre, ref)
         _same_rows(scr, ref)
-        _same_rows(nar, ref)
-        _same_rows(f4, ref)
-        _same_rows(dft, ref)
-        if st4["screened"]:
-            # fp4 operands exist only for nonnegative weights
-            assert st4["screened"] == (1 if case == "mixed_sign" else 2), st4
-            assert st4["candidate_tiles"] <= st4["tiles"]
-        # the 64x128 screen bounds each pair with its own T; the 64x64 screen
-        # with launch-wide constants (E and the marginal floor from T <= 2 sum
-        # of the top digits, screen_consts), a little looser on sites with many
-        # "out" sequences
-        assert stn["candidate_tiles"] <= st["candidate_tiles"] + max(2, st["candidate_tiles"] // 8), (
-            thr, stn["candidate_tiles"], st["candidate_tiles"])
         _rows_equal_dense(scr, dense, thr, L)
         screened_any |= st["screened"] == 1
         assert st["candidate_tiles"] <= st["tiles"]
@@ -274,36 +253,6 @@ def test_prefilter_and_screen_never_change_rows(W, ctxs, case):
         for k, f in enumerate(("d", "d_prime", "r2")):
             agree(dense[k][iu][m & ~well], odense[k][iu][m & ~well], truth[k][iu][m & ~well], field=f + "@rare",
                   escape=True)
-
-
-def test_fp4_screen_auto_policy(W, ctxs):
-    # BASELINE-style random data: at 0.05 the fp4 screen rejects (nearly) every
-    # tile; at 0.002 its coarser bound leaves most tiles, so auto falls back to
-    # the i8 screen for that and every lower threshold — rows identical throughout
-    ctx = _ctx(ctxs, "mfma")
-    buf = synth(2500, 1500, 21)
-    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
-    ctx.set_option("screen_fp4", 2)
-    ctx.load(buf, w)
-    st = ctx.stats()
-    ctx.run(0.05)
-    st = ctx.stats()
-    assert st["screened"] == 2 and st["candidate_tiles"] <= st["tiles"] // 100, st
-    ref = O.all_pairs(buf, w, np.float32(0.05))
-    assert len(ctx.rows()) == len(ref["r2"])
-    seen = []
-    for thr in (0.002, 0.002, 0.001, 0.05):
-        ctx.run(thr)
-        st = ctx.stats()
-        seen.append((thr, st["screened"], st["candidate_tiles"], st["tiles"]))
-        rows = ctx.rows()
-        i8, _ = _run(ctx, thr, 1, 1, 0, 0)
-        ctx.set_option("screen_fp4", 2)
-        _same_rows(rows, i8)
-    # first run at 0.002: fp4 with many candidates; then i8 at <= 0.002; fp4 again at 0.05
-    assert seen[0][1] == 2 and seen[0][2] * 10 > seen[0][3], seen
-    assert seen[1][1] == 1 and seen[2][1] == 1 and seen[3][1] == 2, seen
-    ctx.set_option("screen_fp4", 0)
 
 
 def test_screen_auto_policy(W, ctxs):
@@ -372,7 +321,7 @@ def test_screen_rejects_random_tiles(W, ctxs):
     assert ctx.stats()["mfma_planes"] == 3
     n = ctx.run(0.05)
     st = ctx.stats()
-    assert st["screened"] in (1, 2) and st["pair_kernel_launches"] == 2
+    assert st["screened"] == 1 and st["pair_kernel_launches"] == 2
     assert st["candidate_tiles"] <= st["tiles"] // 100, st
     ref = O.all_pairs(buf, w, np.float32(0.05))
     assert n == len(ref["r2"])

@@ -5,10 +5,10 @@
 set -e
 cd "$(dirname "$0")/.."
 name=$1; flags=$2
-make -s build/obj/encode.o build/obj/prepass.o build/obj/pair_valu.o build/obj/screen_fp4.o build/obj/order.o build/obj/capi.o build/obj/host.o
+make -s build/obj/encode.o build/obj/prepass.o build/obj/pair_valu.o build/obj/order.o build/obj/capi.o build/obj/host.o
 out=build/exp/$name; mkdir -p $out
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Iinclude \
   -Iweightedld_amd/csrc $flags -c weightedld_amd/csrc/pair_mfma.hip -o $out/pair_mfma.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/libweightedld.so build/obj/encode.o build/obj/prepass.o \
-  build/obj/pair_valu.o $out/pair_mfma.o build/obj/screen_fp4.o build/obj/order.o build/obj/capi.o build/obj/host.o -lpthread
+  build/obj/pair_valu.o $out/pair_mfma.o build/obj/order.o build/obj/capi.o build/obj/host.o -lpthread
 echo "$out/libweightedld.so"

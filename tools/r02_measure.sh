@@ -7,7 +7,6 @@ out=gpurun_out/${1:-r02m}
 mkdir -p $out
 export TMPDIR=/tmp
 tools/gpu_step.sh 600 $out/gpu_tests.txt python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread || exit $?
-tools/gpu_step.sh 200 $out/bench_c4_fp4.log python bench.py --fp4-screen --no-cpu-baseline || exit $?
 tools/gpu_step.sh 300 $out/bench_c4.log python bench.py || exit $?
 tools/gpu_step.sh 200 $out/bench_c4_nopipe.log python bench.py --no-pipeline --no-cpu-baseline || exit $?
 tools/gpu_step.sh 200 $out/bench_c2.log python bench.py --config c2 --no-cpu-baseline || exit $?

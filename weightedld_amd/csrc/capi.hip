@@ -105,19 +105,13 @@ struct wld_ctx {
     int opt_screen = 1;             // WLD_OPT_SCREEN: 0 never, 1 auto (default), 2 always, 3 always two-plane
     float screen_bad_thr = -1.0f;   // auto: the largest threshold at which the screen left > half the tiles
     float screen2_bad_thr = -1.0f;  // auto: ... at which the two-plane screen left > a fifth of them
-    bool opt_wide_screen = false;  // WLD_OPT_WIDE_SCREEN: the i8 screen on 64x128 tiles (A/B: not faster)
-    int opt_screen_fp4 = 0;        // WLD_OPT_SCREEN_FP4: 0 never (default: measured no faster), 1 always, 2 auto
-    bool have_fp4 = false;         // frag4 holds this load's fp4 screen operands
-    float R4 = 0.0f;               // their weights' residual bound
-    float fp4_bad_thr = -1.0f;     // auto: the largest threshold at which the fp4 screen left > 10% candidates
-    bool fp4_used = false;         // the last pass screened on fp4
     bool opt_site_major = false, opt_valu_plain = false;
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
 
     // loaded SiteSet
     bool loaded = false;
     size_t L = 0, N = 0, LP = 0, NP = 0;
-    DevBuf raw, wraw, codes, w_pad, wstats, site_ok, site_map, planes, frag, frag4, w4;
+    DevBuf raw, wraw, codes, w_pad, wstats, site_ok, site_map, planes, frag;
     DevBuf keep, htab, htab_kept, site_index;  // device pre-pass (prepass.hip)
     std::vector<uint64_t> kept_map;  // parent indices of the kept sites (wld_site_map_copy)
     bool prepass_loaded = false;
@@ -131,12 +125,12 @@ struct wld_ctx {
     MfmaWeightStats wst{7, 1, {0, 0, 0}, {0, 0, 0, 0}};  // digit-plane statistics of the load (MFMA)
 
     // run state
-    DevBuf tiles, wtiles, cand, seg_cnt, seg_off, chunk_total, chunk_base, counters;
+    DevBuf tiles, cand, seg_cnt, seg_off, chunk_total, chunk_base, counters;
     DevBuf st_a, st_b, st_d, st_dp, st_r2;
     DevBuf out_a, out_b, out_d, out_dp, out_r2;
     uint64_t st_capacity = 0;
     uint32_t tiles_lb = ~0u, tiles_le = ~0u;  // linear chunk range the tile list covers
-    uint32_t n_tiles = 0, n_wtiles = 0;  // wtiles: the screen's wide tiles (kWideSecond)
+    uint32_t n_tiles = 0;
     bool have_rows = false;
     bool screened = false;  // the last pass ran a screen
     bool screened2 = false; // ... on two digit planes
@@ -147,7 +141,7 @@ struct wld_ctx {
         for (wld_ctx *m : members) delete m;
         if (!members.empty()) return;
         (void)hipSetDevice(device);
-        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &frag4, &w4, &tiles, &wtiles, &cand,
+        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &tiles, &cand,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
@@ -196,6 +190,9 @@ int weight_shift(float maxabs, int planes) {
 int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint64_t *site_map,
                 const uint32_t *d_site_index = nullptr) {
     const size_t L = c->L, N = c->N;
+    // a new data set: the auto screen policy (thresholds learned on the last
+    // one) starts over
+    c->screen_bad_thr = c->screen2_bad_thr = -1.0f;
     c->LP = round_up(std::max<size_t>(L, 1), kChunk);
     c->NP = round_up(std::max<size_t>(N, 1), kSeqPad);
     WLD_TRY(ensure(c->codes, c->LP * c->NP));
@@ -256,33 +253,11 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
         // WLD_OPT_MFMA_LAYOUT = 1 keeps the site-major reads (tests)
         c->use_frag = !c->opt_site_major;
         if (c->use_frag) {
-            // two copies: the selector-coded one (A operands, and B in the
-            // v_perm build) and the 0/1/2-coded one the B side reads raw
-            // + 4 KB: the wide screen's copy of a partial last group reads past
-            // the last block's stages (into LDS stages it never reads)
-            WLD_TRY(ensure(c->frag, 2 * c->LP * c->NP + 4096));
+            // two copies: the selector-coded one (A operands) and the
+            // 0/1/2-coded one the B side reads raw
+            WLD_TRY(ensure(c->frag, 2 * c->LP * c->NP));
             launch_frag(ptr<uint8_t>(c->codes), c->LP, c->NP, ptr<uint8_t>(c->frag), c->stream);
             HIP_TRY(hipGetLastError());
-        }
-        // the fp4 screen's operands (screen_fp4.hip): nonnegative weights only
-        c->have_fp4 = false;
-        c->fp4_bad_thr = -1.0f;
-        c->screen_bad_thr = -1.0f;
-        if (c->use_frag && c->opt_screen_fp4 && c->NP <= kFp4MaxNP && c->L > 0) {
-            std::vector<float> hw(c->NP);
-            HIP_TRY(hipMemcpyAsync(hw.data(), c->w_pad.p, c->NP * sizeof(float), hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(hipStreamSynchronize(c->stream));
-            std::vector<uint8_t> packed;
-            if (fp4_weights(hw.data(), N, c->NP, packed, &c->R4) == 0) {
-                WLD_TRY(ensure(c->w4, packed.size()));
-                HIP_TRY(hipMemcpyAsync(c->w4.p, packed.data(), packed.size(), hipMemcpyHostToDevice, c->stream));
-                WLD_TRY(ensure(c->frag4, screen_fp4_frag_bytes(c->LP, c->NP)));
-                launch_frag4(ptr<uint8_t>(c->codes), ptr<uint8_t>(c->w4), c->LP, c->NP, ptr<uint8_t>(c->frag4),
-                             c->stream);
-                HIP_TRY(hipGetLastError());
-                HIP_TRY(hipStreamSynchronize(c->stream));  // packed is freed on return
-                c->have_fp4 = true;
-            }
         }
     }
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
@@ -372,18 +347,15 @@ void rows_to_linear(uint32_t n, uint32_t rb, uint32_t re, uint32_t &lb, uint32_t
 // the ~64 tiles resident on its 32 CUs read 8 A and 8 B tile columns (2 MB at
 // C4) that fit its 4 MB L2.  Short queues are padded with kNoTile entries,
 // which the pair kernels skip.
-// (ta_mask: 0x7FFF for wide screen tiles, whose bit 31 is kWideSecond)
-std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t, uint32_t ta_mask = 0xFFFFu) {
+std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t) {
     constexpr uint32_t kX = 8, kS = 8;
     std::vector<std::vector<uint32_t>> blocks;
     uint64_t last = ~0ull;
     std::vector<uint32_t> sorted(t);
-    auto block_of = [ta_mask](uint32_t v) {
-        return (((v >> 16) & ta_mask) / kS) << 16 | ((v & 0xFFFFu) / kS);
-    };
+    auto block_of = [](uint32_t v) { return ((v >> 16) / kS) << 16 | ((v & 0xFFFFu) / kS); };
     std::sort(sorted.begin(), sorted.end(), [&](uint32_t x, uint32_t y) {
         const uint32_t bx = block_of(x), by = block_of(y);
-        return bx != by ? bx < by : (x & ~kWideSecond) < (y & ~kWideSecond);
+        return bx != by ? bx < by : x < y;
     });
     for (uint32_t v : sorted) {
         const uint64_t key = block_of(v);
@@ -421,24 +393,9 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
                 t.push_back((ta << 16) | tb);
     }
     std::sort(t.begin(), t.end());
-    // the screen's wide tiles: (ta, tb) with (ta, tb + 1) when both are in the
-    // list (rows of the list are runs of consecutive tb)
-    std::vector<uint32_t> w;
-    if (T_used < 32768) {
-        for (size_t i = 0; i < t.size(); ++i) {
-            const bool pair = i + 1 < t.size() && t[i + 1] == t[i] + 1;
-            w.push_back(pair ? t[i] | kWideSecond : t[i]);
-            i += pair;
-        }
-    }
     // only with many rounds of resident tiles: whole super-blocks per XCD
     // leave up to one super-block of imbalance (C2's 528 tiles: +14%)
-    if (!c->opt_tile_rows && w.size() >= 4096) w = xcd_order(w, 0x7FFFu);
     if (!c->opt_tile_rows && t.size() >= 4096 && T_used < 65535) t = xcd_order(t);
-    c->n_wtiles = (uint32_t)w.size();
-    WLD_TRY(ensure(c->wtiles, std::max<size_t>(w.size(), 1) * sizeof(uint32_t)));
-    if (!w.empty())
-        HIP_TRY(hipMemcpyAsync(c->wtiles.p, w.data(), w.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     c->n_tiles = (uint32_t)t.size();
     WLD_TRY(ensure(c->tiles, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));
     WLD_TRY(ensure(c->cand, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));  // screen candidates
@@ -479,17 +436,9 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         m.wplanes = ptr<int8_t>(c->planes);
         m.tiles = ptr<uint32_t>(c->tiles);
         m.n_tiles = c->n_tiles;
-        m.wtiles = c->opt_wide_screen && c->n_wtiles ? ptr<uint32_t>(c->wtiles) : nullptr;
-        m.n_wtiles = c->n_wtiles;
         m.L = (uint32_t)c->L;
         m.NP = (uint32_t)c->NP;
         m.LP = (uint32_t)c->LP;
-        // the fp4 screen: when built, unless (auto) it proved ineffective at a
-        // threshold >= this one (then the i8 screen)
-        c->fp4_used = c->have_fp4 && c->n_wtiles && !dense &&
-                      (c->opt_screen_fp4 == 1 || (c->opt_screen_fp4 == 2 && thr > c->fp4_bad_thr));
-        m.frag4 = c->fp4_used ? ptr<uint8_t>(c->frag4) : nullptr;
-        m.R4 = c->R4;
         m.n_chunk_rows = n;
         m.thr = thr;
         m.shift = c->shift;
@@ -504,7 +453,7 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         // (>= 3 active planes), unless it proved ineffective too
         if (m.prefilter && !m.screen && c->opt_screen == 1 && thr > c->screen2_bad_thr) m.screen = m.screen2 = true;
         if (c->opt_screen == 3) m.screen2 = true;
-        if (m.screen2 && (__builtin_popcount(c->plane_mask & 15) < 3 || c->fp4_used)) {
+        if (m.screen2 && __builtin_popcount(c->plane_mask & 15) < 3) {
             m.screen2 = false;  // one or two active planes: the one-plane screen or the full kernel
             m.screen = c->opt_screen >= 2;
         }
@@ -572,6 +521,7 @@ int wld_create_multi(const int *devices, int n_devices, wld_ctx **out) {
     if (!out) return fail(WLD_E_ARG, "wld_create_multi: null out");
     *out = nullptr;
     if (!devices || n_devices < 1) return fail(WLD_E_ARG, "wld_create_multi: need at least one device");
+    if (n_devices == 1) return wld_create(devices[0], out);  // a plain context: every entry point works
     auto *g = new wld_ctx;
     g->device = devices[0];
     for (int k = 0; k < n_devices; ++k) {
@@ -631,11 +581,6 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
             if (value < 1) return fail(WLD_E_ARG, "WLD_OPT_HOST_BATCH_PAIRS must be >= 1");
             c->opt_host_batch_pairs = (uint64_t)value;
             break;
-        case WLD_OPT_WIDE_SCREEN: c->opt_wide_screen = value != 0; break;
-        case WLD_OPT_SCREEN_FP4:
-            if (value < 0 || value > 2) return fail(WLD_E_ARG, "WLD_OPT_SCREEN_FP4 must be 0, 1 or 2");
-            c->opt_screen_fp4 = (int)value;  // operands are built at the next load
-            break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }
     return WLD_OK;
@@ -652,8 +597,6 @@ int wld_get_option(wld_ctx *c, int option, int64_t *value) {
         case WLD_OPT_VALU_PLAIN: *value = c->opt_valu_plain; break;
         case WLD_OPT_STAGING_ROWS: *value = (int64_t)c->opt_staging_rows; break;
         case WLD_OPT_HOST_BATCH_PAIRS: *value = (int64_t)c->opt_host_batch_pairs; break;
-        case WLD_OPT_WIDE_SCREEN: *value = c->opt_wide_screen; break;
-        case WLD_OPT_SCREEN_FP4: *value = c->opt_screen_fp4; break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }
     return WLD_OK;
@@ -983,14 +926,11 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     c->stats.order_ms = event_ms(c->ev[3], c->ev[order_end]);
     c->stats.pair_kernel_launches = c->n_tiles ? (c->screened ? 2 : 1) : 0;
     c->stats.tiles = c->n_tiles;
-    c->stats.screened = c->screened ? (c->fp4_used ? 2 : c->screened2 ? 3 : 1) : 0;
-    // auto: a threshold at which the fp4 bound leaves > 10% of the tiles to the
-    // exact kernel is screened on i8 from now on (and every lower one)
-    if (c->screened && c->fp4_used && h[2] * 10 > c->n_tiles) c->fp4_bad_thr = std::max(c->fp4_bad_thr, r.thr);
+    c->stats.screened = c->screened ? (c->screened2 ? 3 : 1) : 0;
     // auto: a threshold at which even the i8 screen leaves more than half the
     // tiles is not screened from now on (nor any lower one): the screen costs a
     // third of the full three-plane kernel, the candidates as much again
-    if (c->screened && !c->fp4_used && !c->screened2 && h[2] * 2 > c->n_tiles)
+    if (c->screened && !c->screened2 && h[2] * 2 > c->n_tiles)
         c->screen_bad_thr = std::max(c->screen_bad_thr, r.thr);
     // ... and one at which the two-plane screen (0.8 of the full kernel's
     // time at BASELINE config 4, profiles/r02s2/) leaves more than a fifth
@@ -1218,13 +1158,17 @@ int run_host_group(wld_ctx *g, float thr, wld_progress_fn progress, void *user, 
     std::mutex mu;
     std::condition_variable cv;
     std::vector<int> finished;
+    // every shard's range before any thread starts: an early return must not
+    // leave a joinable std::thread behind (std::terminate)
+    std::vector<uint32_t> lb(G), le(G);
+    for (int k = 0; k < G; ++k) {
+        WLD_TRY(wld_shard_chunks(L, G, k, &lb[k], &le[k]));
+        pairs[k] = pairs_in_chunks(L, lb[k], le[k]);
+    }
     std::vector<std::thread> th;
     for (int k = 0; k < G; ++k) {
-        uint32_t lb = 0, le = 0;
-        WLD_TRY(wld_shard_chunks(L, G, k, &lb, &le));
-        pairs[k] = pairs_in_chunks(L, lb, le);
-        th.emplace_back([&, k, lb, le] {
-            const int st = run_host_range(g->members[k], thr, lb, le, nullptr, nullptr, &part[k]);
+        th.emplace_back([&, k] {
+            const int st = run_host_range(g->members[k], thr, lb[k], le[k], nullptr, nullptr, &part[k]);
             std::lock_guard<std::mutex> lk(mu);
             status[k] = st;
             if (st != WLD_OK) msg[k] = wld_last_error();

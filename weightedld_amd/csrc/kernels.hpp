@@ -15,9 +15,6 @@ constexpr int kSeqPad = 64;      // sequences padded to a multiple of this
 constexpr int kTilesPerChunk = kChunk / kTile;
 // an empty slot of a reordered tile list (never a real tile: T_used < 65535 there)
 constexpr uint32_t kNoTile = 0xFFFFFFFFu;
-// wide screen tiles (ta << 16 | tb, ta < 2^15): the 64x64 tile (ta, tb + 1)
-// is part of the entry too
-constexpr uint32_t kWideSecond = 0x80000000u;
 
 // Code byte per (site, sequence): bit0 = sequence is major or minor at the site
 // ("in" the pair mask, lib.rs:435), bit1 = sequence is major (lib.rs:430,432).
@@ -89,10 +86,7 @@ struct MfmaLaunch {
     const uint8_t *frag_b;  // fragment-major 0/1/2-coded copy (B operands)
     const int8_t *wplanes;
     const uint32_t *tiles;
-    const uint32_t *wtiles;  // the same tiles paired along b (kWideSecond), for the screen; or null
-    const uint8_t *frag4;    // fp4 screen operands (screen_fp4.hip): screen on fp4 MFMA; or null
-    float R4;                // the fp4 weights' residual bound
-    uint32_t n_tiles, n_wtiles, L, LP, NP, n_chunk_rows;
+    uint32_t n_tiles, L, LP, NP, n_chunk_rows;
     float thr;
     int shift;
     unsigned plane_mask;
@@ -105,18 +99,6 @@ struct MfmaLaunch {
     uint32_t *cand_list;   // n_tiles entries
     unsigned *cand_count;  // 0 before the launch (chunk_scan_kernel resets it)
 };
-// screen_fp4.hip: the screen on fp4 (e2m1) matrix cores, nonnegative
-// weights, NP <= kFp4MaxNP (doubled sums <= 18 NP stay exact below 2^22)
-constexpr size_t kFp4MaxNP = 196608;
-size_t screen_fp4_frag_bytes(size_t LP, size_t NP);
-// fp4 codes of w * s (packed two per byte, NP / 2 bytes) and the residual
-// bound R (f32, rounded up); -1 if some weight is negative, non-finite or all zero
-int fp4_weights(const float *w, size_t N, size_t NP, std::vector<uint8_t> &packed, float *R);
-void launch_frag4(const uint8_t *codes, const uint8_t *w4, size_t LP, size_t NP, uint8_t *frag4, hipStream_t s);
-void launch_screen_fp4(const uint8_t *frag4, const uint64_t *ok_bits, const uint32_t *wtiles, uint32_t n_wtiles,
-                       size_t LP, size_t NP, float thr, float R, const OrderArgs &o, uint32_t *cand_list,
-                       unsigned *cand_count, hipStream_t s);
-
 // Enqueues the MFMA pair kernel(s) of one pass; returns true when a screen
 // (one- or two-plane) ran (then screen_done, if given, is recorded between
 // the two launches).

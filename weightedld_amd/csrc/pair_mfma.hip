@@ -361,6 +361,9 @@ __device__ __forceinline__ void zero_acc(Acc16<NPL, NB> &acc) {
 //                  kModePrefilter launch), the others write their zero counts
 enum : int { kModeDense = 0, kModeAll = 1, kModePrefilter = 2, kModeScreen = 3 };
 
+// the one-plane screen's doubled sums |2S| <= 256 NP stay exact in f32 up to here
+constexpr uint32_t kScrF32MaxNP = 16384;
+
 // per-launch screen/candidate arguments
 struct ScreenArgs {
     double R;               // kModeScreen: residual bound in top-digit units
@@ -632,11 +635,7 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this group landed
             __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
             asm volatile("" ::: "memory");
-#ifdef WLD_DIAG_NODMA
-            if (grp + 1 < min(n_groups, 2u)) issue(grp + 1, buf ^ 1);
-#else
             if (grp + 1 < n_groups) issue(grp + 1, buf ^ 1);
-#endif
             const uint8_t *gb = smem + buf * KGB;
             const uint32_t n_st = min((uint32_t)KG, NKB - grp * KG);
             for (uint32_t st = 0; st < n_st; st += 2) {  // n_st is even: NP is a multiple of 64
@@ -710,225 +709,6 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
             asm volatile("" : "+v"(tid));
             compute_tile(tiles[bi], tid);
             __syncthreads();  // the next tile's first DMA reuses buffer 0 and the compaction state
-        }
-    }
-}
-
-// ---- the one-plane screen on wide tiles ------------------------------------
-// The screen (kModeScreen) over 64 x 128 site tiles: a workgroup covers the
-// 64x64 tiles (ta, tb) and (ta, tb + 1) of the shard's list (wide list built
-// by the host: kWideSecond marks the second one present).  Wave w computes a
-// rows 32 (w & 1) .. +31 against b columns 64 (w >> 1) .. +63 of the wide
-// tile: two A operands (16 a rows each) x four B blocks, 32 MFMAs per 64
-// sequences (1 VALU per MFMA for the operands, against 1.5 with 16-row wave
-// tiles) and 6 KB of operands per 32-sequence stage for 8192 pairs (4 KB for
-// 4096 on 64x64 tiles).  128 accumulators, two workgroups (two waves per
-// SIMD) per CU.  The per-pair test is r2_screen_skip_f32 on the doubled sums
-// (2T = X + Y ... exact integers, no halving) while 256 NP <= 2^22, else
-// r2_bound_skip in f64.  A 64x64 half with any pair the bound cannot reject
-// is appended to the candidate list (the full kernel recomputes it with every
-// plane); the others write their zero segment counts.
-#ifndef WLD_SCR_KG
-#define WLD_SCR_KG 4
-#endif
-constexpr int kScrKG = WLD_SCR_KG;                                 // 32-sequence stages per LDS group (even)
-constexpr int kScrStage = 6144;                                    // A0 A1 B0 B1 B2 B3, 1 KB each
-constexpr int kScrGroup = kScrKG * kScrStage + kDigGroup;          // + the group's digit records
-constexpr uint32_t kScrF32MaxNP = 16384;                           // doubled sums |2S| <= 256 NP <= 2^22
-
-#ifndef WLD_SCR_WG
-#define WLD_SCR_WG 2
-#endif
-__global__ __launch_bounds__(256, WLD_SCR_WG) void pair_screen_kernel(const uint8_t *__restrict__ frag,
-                                                             const uint8_t *__restrict__ frag_b,
-                                                             const int8_t *__restrict__ planes,
-                                                             const uint64_t *__restrict__ ok_bits,
-                                                             const uint32_t *__restrict__ wtiles, uint32_t NP,
-                                                             float thr, uint32_t plane, OrderArgs o, ScreenArgs sc) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kScrGroup];
-    __shared__ uint32_t sCand[2];
-    const uint32_t e = wtiles[blockIdx.x];
-    if (e == kNoTile) return;  // padding of an XCD-ordered list (whole workgroup)
-    const bool two = (e & kWideSecond) != 0;
-    const uint32_t ta = (e >> 16) & 0x7FFFu, tb = e & 0xFFFFu;
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t ah = wave & 1, bh = wave >> 1;
-    const uint32_t NKB = NP / 32;
-    const uint32_t n_groups = (NKB + kScrKG - 1) / kScrKG;
-    if (tid < 2) sCand[tid] = 0;  // ordered before the epilogue by the loop's barriers
-
-    // operand blocks of a stage: 0/1 = a sites 32-block 2ta, 2ta + 1 (selector
-    // copy), 2..5 = b 32-blocks 2tb .. 2tb + 3 (0/1/2 copy; without a second
-    // half, blocks 4/5 repeat tb's and their sums are never used).  A group's
-    // 6 kScrKG one-KB pieces go round-robin to the waves: piece i = 6 st + b to
-    // wave i % 4, the same (st, b) slots every group, so each wave keeps its
-    // slots' block bases in SGPRs and adds the group's offset to one VGPR.
-    // The copy of a partial last group reads past NKB into the allocation's
-    // padding (capi.hip pads frag by kScrKG KB) into stages never read.
-    static_assert((kScrKG * 6) % 4 == 0, "pieces per wave");
-    constexpr int kPieces = kScrKG * 6 / 4;
-    const size_t blk = (size_t)NKB * 1024;
-    const uint32_t tb2 = two ? tb + 1 : tb;
-    const uint8_t *pbase[kPieces];
-    uint32_t plds[kPieces];
-#pragma unroll
-    for (int j = 0; j < kPieces; ++j) {
-        const uint32_t i = 4 * j + wave, st = i / 6, b = i % 6;  // wave-uniform
-        const uint32_t g = b < 2 ? 2 * ta + b : b < 4 ? 2 * tb + (b - 2) : 2 * tb2 + (b - 4);
-        pbase[j] = (b < 2 ? frag : frag_b) + g * blk + st * 1024;
-        plds[j] = st * kScrStage + b * 1024;
-    }
-    const int8_t *digf = planes + digf_offset(NP);
-    const uint32_t smem_lds = lds_addr(smem);
-    auto issue = [&](uint32_t grp, uint32_t buf) {
-        const uint32_t gb = smem_lds + buf * kScrGroup;
-        const uint32_t voff = grp * (kScrKG * 1024) + lane * 16;
-#pragma unroll
-        for (int j = 0; j < kPieces; ++j) glds16_s(pbase[j], voff, gb + plds[j]);
-        if (wave == 0) glds16(digf + digf_stage(grp * kScrKG) + lane * 16, gb + kScrKG * kScrStage);
-    };
-
-    // lane group g = lane >> 4 reads stage 2s + (g >> 1), half g & 1, of each
-    // 64-sequence step (the fragment layout re-addressed as in pair_mfma_kernel)
-    const uint32_t g4 = lane >> 4, so = g4 >> 1, hh = g4 & 1;
-    const uint32_t lrow = so * kScrStage + (32 * hh + (lane & 15)) * 16;
-    const uint32_t offA = lrow + ah * 1024;                // + r * 256
-    const uint32_t offB = lrow + (2 + 2 * bh) * 1024;      // + (n >> 1) * 1024 + (n & 1) * 256
-    const uint32_t offD = kScrKG * kScrStage + so * kDigStage + (2 * plane + hh) * 16;
-
-    v4i acc[2][4][2][2];  // [a block r][b block n][channel_a][X, Y]
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-            for (int x = 0; x < 2; ++x)
-#pragma unroll
-                for (int y = 0; y < 2; ++y) acc[r][n][x][y] = v4i{0, 0, 0, 0};
-
-    // Register pipeline over 64-sequence steps: step t's operands are read
-    // from LDS while step t - 1's 32 MFMAs run.  One barrier per group, placed
-    // before the group's last step: after it (every wave's s_waitcnt vmcnt(0)
-    // and lgkmcnt(0)) the next group has landed, so the last step can prefetch
-    // its first operands, and the group's own buffer has no reader left, so
-    // the group after next is copied into it.
-    struct Ops {
-        v4i ca[2], cb[4], dp;
-    };
-    auto load = [&](uint32_t t) {  // operands of step t (stages 2t, 2t + 1)
-        const uint32_t grp = t / (kScrKG / 2), st = 2 * (t % (kScrKG / 2));
-        const uint8_t *gb = smem + (grp & 1) * kScrGroup;
-        const uint8_t *s_ = gb + st * kScrStage;
-        Ops x;
-        x.dp = *reinterpret_cast<const v4i *>(gb + st * kDigStage + offD);
-#pragma unroll
-        for (int r = 0; r < 2; ++r) x.ca[r] = *reinterpret_cast<const v4i *>(s_ + offA + r * 256);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) x.cb[n] = *reinterpret_cast<const v4i *>(s_ + offB + (n >> 1) * 1024 + (n & 1) * 256);
-        return x;
-    };
-    auto sync_groups = [&](uint32_t grp) {  // next group landed, buffer of grp free
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (grp + 2 < n_groups) issue(grp + 2, grp & 1);
-    };
-    constexpr unsigned kOnes = 0x01010101u;
-    const uint32_t n_steps = NKB / 2, spg = kScrKG / 2;
-    issue(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (n_groups > 1) issue(1, 1);
-    Ops cur = load(0);
-    for (uint32_t t = 0; t < n_steps; ++t) {
-#ifdef WLD_SCR_NOPREFETCH
-        if (t > 0) {
-            if (t % spg == 0) sync_groups(t / spg - 1);
-            cur = load(t);
-        }
-#else
-        Ops nxt;
-        if (t + 1 < n_steps) {
-            if ((t + 1) % spg == 0) sync_groups(t / spg);
-            nxt = load(t + 1);
-        }
-#endif
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            v4i ai, am;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                ai[k] = (int)__builtin_amdgcn_perm((unsigned)cur.dp[k], (unsigned)cur.dp[k], (unsigned)cur.ca[r][k]);
-                am[k] = (int)__builtin_amdgcn_perm((unsigned)cur.dp[k], 0u, (unsigned)cur.ca[r][k]);
-            }
-#pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                v4i bm;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) bm[k] = cur.cb[n][k] & (int)kOnes;
-                acc[r][n][0][0] = mfma_i8_16(ai, cur.cb[n], acc[r][n][0][0]);
-                acc[r][n][0][1] = mfma_i8_16(ai, bm, acc[r][n][0][1]);
-                acc[r][n][1][0] = mfma_i8_16(am, cur.cb[n], acc[r][n][1][0]);
-                acc[r][n][1][1] = mfma_i8_16(am, bm, acc[r][n][1][1]);
-            }
-        }
-#ifndef WLD_SCR_NOPREFETCH
-        cur = nxt;
-#endif
-    }
-
-    // ---- per-pair bound: lane holds a = 32 ah + 16 r + 4 g4 + k, b = 16 n + (lane & 15) of half bh.
-    // r2_screen_skip_f32 on the doubled sums, branch-free: a pair is undecided
-    // when viol = max(lhs - rhs, 2^-12 Tb - mlo) > 0 (the launch guarantees
-    // nonnegative weights and NP <= kScrF32MaxNP; the 64x64 screen covers the
-    // rest).  Bits of pairs whose sites are not both valid (or a >= b on the
-    // diagonal) are masked out.
-    const uint32_t tbh = tb + bh;
-    const bool here = bh == 0 || two;  // this wave's 64x64 half exists
-    const uint64_t okA = ok_bits[ta], okB = ok_bits[here ? tbh : tb];
-    // valid bit r*16 + n*4 + k
-    const uint32_t asel = (uint32_t)(okA >> (32 * ah + 4 * g4));    // bits k (r = 0), 16 + k (r = 1)
-    const uint64_t bsel = okB >> (lane & 15);                       // bits 16 n
-    uint32_t vmask = 0;
-#pragma unroll
-    for (int n = 0; n < 4; ++n) vmask |= ((bsel >> (16 * n)) & 1) ? (asel & 0x000F000Fu) << (4 * n) : 0u;
-    if (ta == tbh) {  // diagonal half: a < b only
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-            const uint32_t r = i >> 4, n = (i >> 2) & 3, k = i & 3;
-            if (!(32 * ah + 16 * r + 4 * g4 + k < 16 * n + (lane & 15))) vmask &= ~(1u << i);
-        }
-    }
-    if (!here) vmask = 0;
-    const float R2 = 2.0f * sc.Rf;  // exact: the doubled sums' residual bound
-    const float thr_c = thr * (1.0f - 0x1p-7f);
-    float worst = -1.0f;
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int X0 = acc[r][n][0][0][k], Y0 = acc[r][n][0][1][k];
-                const int X1 = acc[r][n][1][0][k], Y1 = acc[r][n][1][1][k];
-                // doubled sums 2T, 2SA, 2SB, 2SAB (exact integers, exact in f32)
-                const float T = (float)(X0 + Y0), B = (float)(X0 - Y0), A = (float)(X1 + Y1), AB = (float)(X1 - Y1);
-                const float viol = r2_screen_violation(T, A, B, AB, R2, thr_c);
-                const int i = 16 * r + 4 * n + k;
-                worst = fmaxf(worst, ((vmask >> i) & 1) ? viol : -1.0f);
-            }
-    const bool cand = !(worst <= 0.0f);  // some valid pair r2_screen_skip_f32 does not skip
-    if (__builtin_amdgcn_ballot_w64(cand) != 0 && lane == 0) sCand[bh] = 1;
-    __syncthreads();
-    const uint32_t half = tid >> 6;  // threads 0-63: tile (ta, tb); 64-127: (ta, tb + 1)
-    if (half < 2 && (half == 0 || two)) {
-        const uint32_t t = tb + half;
-        if (sCand[half]) {
-            if (lane == 0) sc.cand_list[atomicAdd(sc.cand_count, 1u)] = (ta << 16) | t;
-        } else {
-            o.seg_cnt[(size_t)(ta * kTile + lane) * o.T + t] = 0;
         }
     }
 }
@@ -1106,14 +886,7 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     sc.f32 = m.nonneg ? (m.NP <= kScrF32MaxNP ? 2 : m.NP <= kScreenF32MaxNP ? 1 : 0) : 0;
     // every doubled one-plane T <= 2 sum_k |d_top,k| <= 256 NP <= 2^22 (exact in f32)
     if (sc.f32 == 2) screen_consts((float)(2 * m.dsum[top]), 2.0f * sc.Rf, sc.E, sc.mloc);
-    if (m.frag4 && m.wtiles && m.n_wtiles)
-        launch_screen_fp4(m.frag4, ok_bits, m.wtiles, m.n_wtiles, m.LP, m.NP, m.thr, m.R4, o, m.cand_list,
-                          m.cand_count, s);
-    else if (m.wtiles && m.n_wtiles && m.nonneg && m.NP <= kScrF32MaxNP)
-        hipLaunchKernelGGL(pair_screen_kernel, dim3(m.n_wtiles), dim3(256), 0, s, m.frag, m.frag_b, m.wplanes, ok_bits,
-                           m.wtiles, m.NP, m.thr, top, o, sc);
-    else
-        launch_lds<kModeScreen, 1>(m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, top, o, dn, sc, s);
+    launch_lds<kModeScreen, 1>(m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, top, o, dn, sc, s);
     if (screen_done) (void)hipEventRecord(screen_done, s);
     const uint32_t grid = std::min<uint32_t>(m.n_tiles, kCandidateGrid);
     launch_lds_planes<kModePrefilter, true>(n, m, ok_bits, m.cand_list, 0, m.cand_count, grid, idx, o, dn, sc, s);
