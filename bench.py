@@ -49,6 +49,76 @@ def synth(L, N, seed=0x5EED, block=4096):
     return out
 
 
+def ld_blocks(L, N, seed=0x1DB1, min_block=20, max_block=200, p_missing=0.1, p_mut=0.02):
+    """Linkage-structured alignment (--data ldblocks): consecutive blocks of
+    20-200 sites; in each block every sequence copies one of 3-8 founder
+    haplotypes (random proportions), every site gives each founder a major
+    or minor symbol (a random 0/1 pattern, minor frequency 0.2-0.5 among
+    founders' carriers), each copy mutates w.p. p_mut and is '-' w.p.
+    p_missing.  Pairs inside a block are in strong LD (many rows at 0.05),
+    pairs across blocks near r2 ~ 1/N."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = np.empty((L, N), dtype=np.uint8)
+    s0 = 0
+    while s0 < L:
+        s1 = min(L, s0 + int(rng.integers(min_block, max_block + 1)))
+        H = int(rng.integers(3, 9))
+        founder = rng.choice(H, size=N, p=rng.dirichlet(np.ones(H)))
+        n = s1 - s0
+        maj = rng.integers(0, 4, size=n)
+        mnr = (maj + rng.integers(1, 4, size=n)) % 4
+        pat = rng.random((n, H)) < rng.uniform(0.2, 0.5, size=(n, 1))  # founder carries the minor
+        pat[np.arange(n), rng.integers(0, H, size=n)] ^= ~pat.any(axis=1)  # every site polymorphic
+        allele = pat[:, founder] ^ (rng.random((n, N), dtype=np.float32) < p_mut)
+        col = np.where(allele, mnr[:, None], maj[:, None])
+        out[s0:s1] = np.where(rng.random((n, N), dtype=np.float32) < p_missing, 4, col)
+        s0 = s1
+    return out
+
+
+def vcf_like(L, n_hap=5008, seed=0x1000, p_missing=0.002, p_rare=0.5):
+    """1000-Genomes-like biallelic haplotypes (BASELINE config 3 at scale):
+    a Kingman coalescent over n_hap haplotypes, sites = mutations dropped on
+    its branches in proportion to their lengths (allele-frequency spectrum
+    ~1/k, LD as the tree makes it: sites on one branch in perfect LD, nested
+    clades partial), plus a fraction p_rare of recent variants carried by 1-4
+    random haplotypes (the excess of singletons and doubletons a growing
+    population shows: about 60% of sites have an allele count <= 4).
+    Symbols as handle_vcf makes them (WeightedLD.py:348-363): 0 ref, 1 alt,
+    4 missing ('.')."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n = n_hap
+    lineages = list(range(n))
+    members = [np.array([i], dtype=np.int32) for i in range(n)]
+    born = [0.0] * n
+    length = [0.0] * n
+    t = 0.0
+    while len(lineages) > 1:
+        k = len(lineages)
+        t += rng.exponential(2.0 / (k * (k - 1)))
+        i, j = sorted(rng.choice(k, size=2, replace=False))
+        a, b = lineages[i], lineages[j]
+        length[a] = t - born[a]
+        length[b] = t - born[b]
+        members.append(np.concatenate([members[a], members[b]]))
+        born.append(t)
+        length.append(0.0)
+        lineages[j] = lineages[-1]
+        lineages.pop()
+        lineages[i] = len(members) - 1
+    p = np.asarray(length) / np.sum(length)
+    branch = rng.choice(len(members), size=L, p=p)
+    out = np.zeros((L, n), dtype=np.uint8)
+    rare = rng.random(L) < p_rare
+    for s, br in enumerate(branch):
+        if rare[s]:
+            out[s, rng.choice(n, size=int(rng.integers(1, 5)), replace=False)] = 1
+        else:
+            out[s, members[br]] = 1
+    out[rng.random((L, n), dtype=np.float32) < p_missing] = 4
+    return out
+
+
 def pairs_in_rows(L, rb, re_):
     a0, a1 = min(L, rb * 256), min(L, re_ * 256)
     return (a1 - a0) * (L - 1) - (a1 - 1 + a0) * (a1 - a0) // 2 if a1 > a0 else 0

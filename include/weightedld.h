@@ -146,9 +146,9 @@ void wld_destroy(wld_ctx *ctx);
 #define WLD_KERNEL_MFMA 2
 int wld_set_kernel(wld_ctx *ctx, int kernel);
 
-/* Per-context options (the library reads no environment variables).  None
- * changes a result: every setting gives bit-identical rows; they exist for
- * A/B measurements and tests.  Set between runs; WLD_E_ARG for an unknown
+/* Per-context options (the library reads no environment variables).  Except
+ * WLD_OPT_REF_SUMS none changes a result: every setting gives bit-identical
+ * rows; they exist for A/B measurements and tests.  Set between runs; WLD_E_ARG for an unknown
  * option or a bad value.
  *   WLD_OPT_PREFILTER  1 (default): with r2_threshold > 0 the MFMA kernel
  *                      skips the f32 epilogue of pairs that a rigorous bound
@@ -177,6 +177,21 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *                      next load).
  *   WLD_OPT_VALU_PLAIN 0 (default): the f32 fallback multiplies on f32-input
  *                      MFMA; 1: a VALU fmaf loop (same sums, same order).
+ *   WLD_OPT_REF_SUMS   0 (default): each of the four masked sums is computed
+ *                      exactly (integer MFMA) or with error below the
+ *                      reference's own (f32 kernel), then rounded once; 1: the
+ *                      sums are formed in lib.rs's own f32 order (8 lane sums
+ *                      of sequences k = j mod 8, lib.rs:416-445, their ordered
+ *                      horizontal sum, packed_simd's x86 f32x8::sum(),
+ *                      :447-452, then the scalar tail, :461-480) on the f32
+ *                      kernel, so rows are bit-identical to lib.rs's even where
+ *                      its f32 sums are inaccurate (minor alleles carried by a
+ *                      few low-weight sequences).  With the MFMA kernel and a
+ *                      positive threshold the i8 screen still runs first, its
+ *                      bound widened by the reference's rounding, and only
+ *                      candidate tiles take the f32 kernel.  The one option
+ *                      that changes results (in the last bits, or more where
+ *                      the reference's sums are ill-conditioned).
  *   WLD_OPT_STAGING_ROWS   initial staging capacity in rows (default 2^25;
  *                      grown on overflow by a re-run).
  *   WLD_OPT_HOST_BATCH_PAIRS  pairs per batch of wld_run_host (default 2^31).
@@ -190,6 +205,7 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
 #define WLD_OPT_VALU_PLAIN 6
 #define WLD_OPT_STAGING_ROWS 7
 #define WLD_OPT_HOST_BATCH_PAIRS 8
+#define WLD_OPT_REF_SUMS 11
 int wld_set_option(wld_ctx *ctx, int option, int64_t value);
 int wld_get_option(wld_ctx *ctx, int option, int64_t *value);
 
@@ -348,6 +364,7 @@ typedef struct {
     double screen_ms;        /* HIP-event time of the screen launch (0 if none)    */
     int screened;            /* 1: the last run ran the one-plane i8 screen; 3: the two-plane
                                 i8 screen; 0: none */
+    int ref_sums;            /* 1: the last run summed in lib.rs's f32 order (WLD_OPT_REF_SUMS) */
 } wld_run_stats;
 int wld_last_stats(wld_ctx *ctx, wld_run_stats *out);
 

@@ -27,8 +27,12 @@
  *     pinned by the lib.rs unit-test known answers and by golden vectors from
  *     the Python reference (tests/golden/, made by oracle/gen_golden.py).
  *   - packed_simd's f32x8::sum() horizontal order is not pinned by any
- *     reference test; we use the ordered reduction ((((0+x0)+x1)+...)+x7).
- *     Any order is within the 1e-5 tolerance.
+ *     reference test.  packed_simd_2 0.3.5 (Cargo.lock:531-534)
+ *     documents a tree reduction but implements sum() on x86 as
+ *     simd_reduce_add_ordered(v, 0.0), i.e. ((((0+x0)+x1)+...)+x7) — the
+ *     default here.  wldo_set_hsum_order(1) selects the documented tree
+ *     ((x0+x1)+(x2+x3))+((x4+x5)+(x6+x7)) so tests can report how much the
+ *     choice matters.
  *   - Compiled with -ffp-contract=off: Rust does not contract a*b+c.
  */
 #include <math.h>
@@ -196,6 +200,18 @@ void wldo_henikoff_weights(const uint8_t *buf, size_t n_sites, size_t n_seqs, fl
     free(contrib);
 }
 
+/* Horizontal f32x8 sum (lib.rs:447-452): 0 = ordered from 0.0 (default), 1 = tree. */
+static int g_hsum_tree = 0;
+void wldo_set_hsum_order(int tree) { g_hsum_tree = tree != 0; }
+int wldo_get_hsum_order(void) { return g_hsum_tree; }
+
+static float hsum8(f32x8 v) {
+    if (g_hsum_tree) return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+    float s = 0.0f;
+    for (int j = 0; j < 8; ++j) s += v[j];
+    return s;
+}
+
 /* lib.rs:390-521.  Returns 1 (Some) and fills out[0..3] = {d, d_prime, r2},
  * or 0 (None) when either site lacks a major or a minor symbol. */
 int wldo_single_pair_mm(const uint8_t *a, int a_maj, int a_min, const uint8_t *b, int b_maj,
@@ -228,14 +244,8 @@ int wldo_single_pair_mm(const uint8_t *a, int a_maj, int a_min, const uint8_t *b
         pb += (f32x8)(wbits & b_maj);
         l3 += (f32x8)(wbits & (a_maj & b_maj));
     }
-    /* :447-452 — horizontal sums (ordered; see header) */
-    float total_weight = 0.0f, PA = 0.0f, PB = 0.0f, ld3 = 0.0f;
-    for (int j = 0; j < 8; ++j) {
-        total_weight += tw[j];
-        PA += pa[j];
-        PB += pb[j];
-        ld3 += l3[j];
-    }
+    /* :447-452 — horizontal sums (see header) */
+    float total_weight = hsum8(tw), PA = hsum8(pa), PB = hsum8(pb), ld3 = hsum8(l3);
     /* :461-480 — scalar tail */
     for (size_t seq = simd_end; seq < n; ++seq) {
         if (!(a[seq] == am || a[seq] == an)) continue;

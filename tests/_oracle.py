@@ -72,8 +72,27 @@ def lib():
     L.wldo_triu_index.argtypes = [sz, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     f64p = ctypes.POINTER(ctypes.c_double)
     L.wldo_all_pairs_dense_f64.argtypes = [u8p, sz, sz, f32p, f64p, f64p, f64p, u8p]
+    L.wldo_set_hsum_order.argtypes = [ctypes.c_int]
+    L.wldo_get_hsum_order.restype = ctypes.c_int
     _lib = L
     return L
+
+
+class hsum_order:
+    """Context manager selecting the f32x8 horizontal-sum order of the oracle's
+    lane sums (lib.rs:447-452): "ordered" (((0+x0)+x1)+...+x7, packed_simd's
+    x86 implementation, the default) or "tree" (its documented order)."""
+
+    def __init__(self, order):
+        self.tree = {"ordered": 0, "tree": 1}[order]
+
+    def __enter__(self):
+        self.prev = lib().wldo_get_hsum_order()
+        lib().wldo_set_hsum_order(self.tree)
+        return self
+
+    def __exit__(self, *exc):
+        lib().wldo_set_hsum_order(self.prev)
 
 
 def _p(arr, ct):
@@ -152,7 +171,8 @@ def all_pairs(buf, weights, thr, site_map=None, n_threads=None, chunk_lo=0, chun
     w = np.ascontiguousarray(weights, dtype=np.float32)
     sm = None if site_map is None else np.ascontiguousarray(site_map, dtype=np.uint64)
     rows = _Rows()
-    nt = n_threads or (os.cpu_count() or 1)
+    # OMP_NUM_THREADS: the GPU box's CPU share (16) when cpu_count() shows the whole machine
+    nt = n_threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
     hi = ctypes.c_size_t(-1).value if chunk_hi is None else chunk_hi
     n = L.wldo_all_pairs_range(_p(buf, ctypes.c_uint8), n_sites, n_seqs,
                                None if sm is None else _p(sm, ctypes.c_uint64), _p(w, ctypes.c_float),

@@ -45,9 +45,17 @@ class ParityReport:
 
 
 PARITY = ParityReport()
+# free-form lines for the session summary (tests/test_gpu_refsums.py: how far
+# the default path's rows and TSV lines are from lib.rs's on each input, and
+# the reference-order path's distance under either horizontal-sum order)
+REF_REPORT = []
 
 
 def pytest_terminal_summary(terminalreporter):
+    if REF_REPORT:
+        terminalreporter.write_line("reference-parity report (rows and %.3f TSV lines against the oracle):")
+        for line in REF_REPORT:
+            terminalreporter.write_line("  " + line)
     if not PARITY.f:
         return
     terminalreporter.write_line("parity report (GPU vs oracle, tolerance 1e-5):")

@@ -23,7 +23,7 @@ STATUS = {
 KERNEL_AUTO, KERNEL_VALU, KERNEL_MFMA = 0, 1, 2
 # wld_set_option ids (include/weightedld.h)
 OPTIONS = {"prefilter": 1, "screen": 2, "tile_order": 3, "all_planes": 4, "mfma_layout": 5, "valu_plain": 6,
-           "staging_rows": 7, "host_batch_pairs": 8}
+           "staging_rows": 7, "host_batch_pairs": 8, "ref_sums": 11}
 
 
 class WldError(RuntimeError):
@@ -59,6 +59,7 @@ class RunStats(ctypes.Structure):
         ("candidate_tiles", ctypes.c_uint64),
         ("screen_ms", ctypes.c_double),
         ("screened", ctypes.c_int),
+        ("ref_sums", ctypes.c_int),
     ]
 
 

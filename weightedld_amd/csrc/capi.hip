@@ -106,12 +106,17 @@ struct wld_ctx {
     float screen_bad_thr = -1.0f;   // auto: the largest threshold at which the screen left > half the tiles
     float screen2_bad_thr = -1.0f;  // auto: ... at which the two-plane screen left > a fifth of them
     bool opt_site_major = false, opt_valu_plain = false;
+    bool opt_ref_sums = false;  // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
 
     // loaded SiteSet
     bool loaded = false;
     size_t L = 0, N = 0, LP = 0, NP = 0;
     DevBuf raw, wraw, codes, w_pad, wstats, site_ok, site_map, planes, frag;
+    DevBuf rcodes, rw;       // WLD_OPT_REF_SUMS: codes and weights in lane-class order (ref_layout_kernel)
+    bool have_ref = false;   // rcodes/rw hold this load's layout
+    uint32_t ref_cls = 0;    // its positions per lane class
+    size_t NPr = 0;          // its positions per site
     DevBuf keep, htab, htab_kept, site_index;  // device pre-pass (prepass.hip)
     std::vector<uint64_t> kept_map;  // parent indices of the kept sites (wld_site_map_copy)
     bool prepass_loaded = false;
@@ -141,7 +146,7 @@ struct wld_ctx {
         for (wld_ctx *m : members) delete m;
         if (!members.empty()) return;
         (void)hipSetDevice(device);
-        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &tiles, &cand,
+        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &rcodes, &rw, &tiles, &cand,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
@@ -191,8 +196,9 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
                 const uint32_t *d_site_index = nullptr) {
     const size_t L = c->L, N = c->N;
     // a new data set: the auto screen policy (thresholds learned on the last
-    // one) starts over
+    // one) starts over; the reference-order layout is rebuilt when needed
     c->screen_bad_thr = c->screen2_bad_thr = -1.0f;
+    c->have_ref = false;
     c->LP = round_up(std::max<size_t>(L, 1), kChunk);
     c->NP = round_up(std::max<size_t>(N, 1), kSeqPad);
     WLD_TRY(ensure(c->codes, c->LP * c->NP));
@@ -423,12 +429,59 @@ OrderArgs order_args(wld_ctx *c) {
     return o;
 }
 
+// WLD_OPT_REF_SUMS: the codes and weights in the reference's lane-class order
+// (pair_valu.hip), built once per load on first use
+int ensure_ref_layout(wld_ctx *c) {
+    if (c->have_ref) return WLD_OK;
+    uint32_t tail = 0;
+    ref_layout_dims(c->N, &c->ref_cls, &tail, &c->NPr);
+    WLD_TRY(ensure(c->rcodes, c->LP * c->NPr));
+    WLD_TRY(ensure(c->rw, c->NPr * sizeof(float)));
+    launch_ref_layout(ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), c->LP, c->NP, c->N, ptr<uint8_t>(c->rcodes),
+                      ptr<float>(c->rw), c->stream);
+    HIP_TRY(hipGetLastError());
+    c->have_ref = true;
+    return WLD_OK;
+}
+
+// How far (2x2-cell L1, fixed-point units of the weight planes) the
+// reference's f32 sums can lie from the fixed-point sums the screen bounds:
+// each weight is within 0.5 of w 2^shift (every sequence in one cell), and
+// each of the four f32 sums within gamma_m sum|w| of its exact value
+// (recursive summation: every term passes through at most m = N/8 + 16
+// roundings — its lane chain, the horizontal sum, the scalar tail); the
+// cells are n11 = SAB, n10 = SA - SAB, n01 = SB - SAB, n00 = T - SA - SB +
+// SAB, so their L1 error is at most 9 times a sum's.  sum|q| <= sum_p 2^(8p)
+// sum|d_p|.
+double ref_extra_residual(const wld_ctx *c) {
+    const double u = 0x1p-24, m = (double)(c->N / 8) + 16.0;
+    const double gamma = m * u / (1.0 - m * u);
+    double qsum = 0.0;
+    for (int p = 0; p < 4; ++p) qsum += std::ldexp((double)c->wst.dsum[p], 8 * p);
+    const double r = 9.0 * gamma * (qsum + 0.5 * (double)c->N) + 0.5 * (double)c->N;
+    return r * (1.0 + 1e-9) + 1.0;  // slack for this evaluation's own rounding
+}
+
 // Enqueues the pair kernel(s) of a pass; *screened tells whether the MFMA
 // screen ran (then ev[6] separates it from the candidate launch).
 int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *dense, bool *screened = nullptr) {
     const uint32_t n = chunk_rows_of(c->L);
     bool sc = false;
-    if (c->kernel == WLD_KERNEL_MFMA) {
+    ValuLaunch rv{};
+    if (c->opt_ref_sums) {
+        WLD_TRY(ensure_ref_layout(c));
+        rv = ValuLaunch{ptr<uint8_t>(c->rcodes), ptr<float>(c->rw), ptr<uint8_t>(c->site_ok), ptr<uint32_t>(c->tiles),
+                        c->n_tiles, nullptr, (uint32_t)c->L, (uint32_t)c->NPr, n, thr, c->safe, false, true,
+                        c->ref_cls};
+    }
+    // reference order without a screen in front (no positive threshold, the
+    // f32 kernel, dense stats, or the auto policy's full-kernel thresholds):
+    // every tile on the reference-order f32 kernel
+    const bool ref_screen = c->opt_ref_sums && c->kernel == WLD_KERNEL_MFMA && !dense && c->use_frag &&
+                            c->opt_prefilter && thr > 0.0f && c->opt_screen != 0;
+    if (c->opt_ref_sums && !ref_screen) {
+        launch_pair_valu(rv, o, dense, c->stream);
+    } else if (c->kernel == WLD_KERNEL_MFMA) {
         MfmaLaunch m{};
         m.codes = ptr<uint8_t>(c->codes);
         m.frag = c->use_frag ? ptr<uint8_t>(c->frag) : nullptr;
@@ -462,11 +515,21 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
         m.cand_list = ptr<uint32_t>(c->cand);
         m.cand_count = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 2);
-        sc = launch_pair_mfma(m, o, dense, c->stream, c->ev[6]);
-    } else
-        launch_pair_valu(ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), ptr<uint8_t>(c->site_ok),
-                         ptr<uint32_t>(c->tiles), c->n_tiles, (uint32_t)c->L, (uint32_t)c->NP, n, thr, c->safe,
-                         c->opt_valu_plain, o, dense, c->stream);
+        if (ref_screen) {
+            m.ref_valu = &rv;
+            m.r_extra_q = ref_extra_residual(c);
+        }
+        if (ref_screen && !m.screen) {
+            launch_pair_valu(rv, o, nullptr, c->stream);  // the policy sends this threshold to the full kernel
+        } else {
+            sc = launch_pair_mfma(m, o, dense, c->stream, c->ev[6]);
+        }
+    } else {
+        launch_pair_valu(ValuLaunch{ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), ptr<uint8_t>(c->site_ok),
+                                    ptr<uint32_t>(c->tiles), c->n_tiles, nullptr, (uint32_t)c->L, (uint32_t)c->NP, n,
+                                    thr, c->safe, c->opt_valu_plain, false, 0},
+                         o, dense, c->stream);
+    }
     HIP_TRY(hipGetLastError());
     if (screened) *screened = sc;
     return WLD_OK;
@@ -573,6 +636,7 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
             break;
         case WLD_OPT_MFMA_LAYOUT: c->opt_site_major = value != 0; break;
         case WLD_OPT_VALU_PLAIN: c->opt_valu_plain = value != 0; break;
+        case WLD_OPT_REF_SUMS: c->opt_ref_sums = value != 0; break;
         case WLD_OPT_STAGING_ROWS:
             if (value < 1) return fail(WLD_E_ARG, "WLD_OPT_STAGING_ROWS must be >= 1");
             c->opt_staging_rows = (uint64_t)value;
@@ -595,6 +659,7 @@ int wld_get_option(wld_ctx *c, int option, int64_t *value) {
         case WLD_OPT_ALL_PLANES: *value = c->opt_all_planes; break;
         case WLD_OPT_MFMA_LAYOUT: *value = c->opt_site_major; break;
         case WLD_OPT_VALU_PLAIN: *value = c->opt_valu_plain; break;
+        case WLD_OPT_REF_SUMS: *value = c->opt_ref_sums; break;
         case WLD_OPT_STAGING_ROWS: *value = (int64_t)c->opt_staging_rows; break;
         case WLD_OPT_HOST_BATCH_PAIRS: *value = (int64_t)c->opt_host_batch_pairs; break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
@@ -927,6 +992,7 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     c->stats.pair_kernel_launches = c->n_tiles ? (c->screened ? 2 : 1) : 0;
     c->stats.tiles = c->n_tiles;
     c->stats.screened = c->screened ? (c->screened2 ? 3 : 1) : 0;
+    c->stats.ref_sums = c->opt_ref_sums ? 1 : 0;
     // auto: a threshold at which even the i8 screen leaves more than half the
     // tiles is not screened from now on (nor any lower one): the screen costs a
     // third of the full three-plane kernel, the candidates as much again

@@ -54,9 +54,25 @@ void launch_henikoff(const uint8_t *raw, const uint32_t *site_index, size_t n_ke
 void launch_fill_ones(float *w, size_t N, hipStream_t s);
 
 // pair_valu.hip
-void launch_pair_valu(const uint8_t *codes, const float *w, const uint8_t *site_ok, const uint32_t *tiles,
-                      uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, bool safe,
-                      bool plain, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
+struct ValuLaunch {
+    const uint8_t *codes;    // site-major codes, NP bytes per site (REF: the lane-class layout)
+    const float *w;          // NP weights (REF: the lane-class layout)
+    const uint8_t *site_ok;
+    const uint32_t *tiles;   // tile list (or the candidate list with tile_count)
+    uint32_t n_tiles;        // list length, or (tile_count) its capacity
+    const unsigned *tile_count;  // device tile count: the looping candidate launch; else null
+    uint32_t L, NP, n_chunk_rows;
+    float thr;
+    bool safe;   // non-finite weights: the select loop
+    bool plain;  // WLD_OPT_VALU_PLAIN: the VALU fmaf loop instead of f32 MFMA
+    bool ref;    // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order
+    uint32_t ref_cls;  // REF: sequence positions per lane class (multiple of 64, 0 when N < 8)
+};
+void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
+// the lane-class layout of REF: cls positions per class, the tail stage, NPr
+void ref_layout_dims(size_t N, uint32_t *cls, uint32_t *tail, size_t *NPr);
+void launch_ref_layout(const uint8_t *codes, const float *w_pad, size_t LP, size_t NP, size_t N, uint8_t *rcodes,
+                       float *rw, hipStream_t s);
 
 // pair_mfma.hip
 bool mfma_supported();
@@ -98,6 +114,12 @@ struct MfmaLaunch {
     uint64_t dsum[4];
     uint32_t *cand_list;   // n_tiles entries
     unsigned *cand_count;  // 0 before the launch (chunk_scan_kernel resets it)
+    // WLD_OPT_REF_SUMS: the candidate tiles go to the reference-order f32
+    // kernel (ref_valu, tiles/tile_count filled in here) and the screen's
+    // residual bound grows by r_extra_q (fixed-point units: how far the
+    // reference's f32 sums can lie from the fixed-point sums, 2x2-cell L1)
+    const ValuLaunch *ref_valu;
+    double r_extra_q;
 };
 // Enqueues the MFMA pair kernel(s) of one pass; returns true when a screen
 // (one- or two-plane) ran (then screen_done, if given, is recorded between

@@ -810,6 +810,22 @@ void launch_lds_planes(uint32_t n_planes, const MfmaLaunch &m, const uint64_t *o
     else
         launch_lds<MODE, 1, false>(m, ok_bits, tiles, n_tiles, tile_count, grid, plane_idx, o, dn, sc, s);
 }
+// The candidate launch after a screen: a grid-stride loop over the candidate
+// list (length on the device) with every digit plane and the exact
+// prefilter, or (WLD_OPT_REF_SUMS) the reference-order f32 kernel.
+void launch_candidates(const MfmaLaunch &m, uint32_t n, uint32_t idx, const uint64_t *ok_bits, const OrderArgs &o,
+                       const DenseArgs &dn, const ScreenArgs &sc, hipStream_t s) {
+    if (m.ref_valu) {
+        ValuLaunch v = *m.ref_valu;
+        v.tiles = m.cand_list;
+        v.n_tiles = m.n_tiles;
+        v.tile_count = m.cand_count;
+        launch_pair_valu(v, o, nullptr, s);
+        return;
+    }
+    const uint32_t grid = std::min<uint32_t>(m.n_tiles, kCandidateGrid);
+    launch_lds_planes<kModePrefilter, true>(n, m, ok_bits, m.cand_list, 0, m.cand_count, grid, idx, o, dn, sc, s);
+}
 }  // namespace
 
 bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *dense, hipStream_t s,
@@ -868,17 +884,16 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
         // (top >= 2 with three or more active planes, so lo >= 1).  Per pair
         // r2_bound_skip in f64; candidates then get every plane as below.
         const uint32_t lo = top - 1;
-        sc.R = ldexp((double)m.resid[lo - 1], -8 * (int)lo);
+        sc.R = ldexp((double)m.resid[lo - 1] + m.r_extra_q, -8 * (int)lo);
         sc.Rf = (float)sc.R;
         if ((double)sc.Rf < sc.R) sc.Rf = nextafterf(sc.Rf, INFINITY);
         sc.f32 = 0;
         launch_lds<kModeScreen, 2>(m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, lo | (top << 2), o, dn, sc, s);
         if (screen_done) (void)hipEventRecord(screen_done, s);
-        const uint32_t grid = std::min<uint32_t>(m.n_tiles, kCandidateGrid);
-        launch_lds_planes<kModePrefilter, true>(n, m, ok_bits, m.cand_list, 0, m.cand_count, grid, idx, o, dn, sc, s);
+        launch_candidates(m, n, idx, ok_bits, o, dn, sc, s);
         return true;
     }
-    sc.R = top > 0 ? ldexp((double)m.resid[top - 1], -8 * (int)top) : 0.0;
+    sc.R = ldexp((top > 0 ? (double)m.resid[top - 1] : 0.0) + m.r_extra_q, -8 * (int)top);
     if (n == 1) idx = top | ((top == 0 ? 1u : 0u) << 2);
     sc.Rf = (float)sc.R;
     if ((double)sc.Rf < sc.R) sc.Rf = nextafterf(sc.Rf, INFINITY);
@@ -888,8 +903,7 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     if (sc.f32 == 2) screen_consts((float)(2 * m.dsum[top]), 2.0f * sc.Rf, sc.E, sc.mloc);
     launch_lds<kModeScreen, 1>(m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, top, o, dn, sc, s);
     if (screen_done) (void)hipEventRecord(screen_done, s);
-    const uint32_t grid = std::min<uint32_t>(m.n_tiles, kCandidateGrid);
-    launch_lds_planes<kModePrefilter, true>(n, m, ok_bits, m.cand_list, 0, m.cand_count, grid, idx, o, dn, sc, s);
+    launch_candidates(m, n, idx, ok_bits, o, dn, sc, s);
     return true;
 }
 

@@ -1,8 +1,8 @@
-// f32 pair kernel: the exact-f32 path (and the fallback for weights the
-// integer MFMA kernel's fixed-point planes cannot hold exactly).  For finite
-// weights the products and sums run on f32-input MFMA (MF below); the VALU
-// loop described next is the SAFE (non-finite weights) path and the
-// WLD_VALU_PLAIN=1 variant.
+// f32 pair kernel: the exact-f32 path, the fallback for weights the integer
+// MFMA kernel's fixed-point planes cannot hold exactly, and the reference-order
+// path (WLD_OPT_REF_SUMS).  For finite weights the products and sums run on
+// f32-input MFMA (MF below); the VALU loop described next is the SAFE
+// (non-finite weights) path and the WLD_VALU_PLAIN=1 variant.
 //
 // Replaces the inner loop of single_weighted_ld_pair (lib.rs:416-480) for a
 // 64x64 tile of site pairs per 256-thread workgroup.  Each thread owns a 4x4
@@ -14,11 +14,30 @@
 //     SAB += w  where a == maj and b == maj
 // as fmaf(u, f, acc) with u = w or 0 (a side) and f = 1.0 or 0.0 (b side):
 // w*1 and w*0 are exact, so each sum is an f32 sum over sequences in order
-// (64-sequence stage sums added into a running total; the same terms in the
-// same order for all four sums, so SA == T still implies SAB == SB exactly and
-// degenerate pairs stay NaN as in the reference).  (The SAFE variant uses selects, for non-finite weights
-// where 0*inf would differ from the reference's select.)  Codes of both 64-site
+// (the same terms in the same order for all four sums, so SA == T still
+// implies SAB == SB exactly and degenerate pairs stay NaN as in the
+// reference).  (The SAFE variant uses selects, for non-finite weights where
+// 0*inf would differ from the reference's select.)  Codes of both 64-site
 // panels and the weights are staged through LDS 64 sequences at a time.
+//
+// Summation blocks.  acc holds the current block of 64-sequence stages, tot
+// the running total:
+//   * default: blocks of `flush` stages (about sqrt(N) sequences), tot += acc
+//     after each (~2 sqrt(N) 2^-24 relative error, below the reference's own);
+//   * REF (WLD_OPT_REF_SUMS): the reference's own f32 order, lib.rs:416-480.
+//     The sequences are permuted at load (ref_layout_kernel) into the lane
+//     classes of the 8-lane loop: block j (j = 0..7) holds sequences j, j+8,
+//     j+16, ... < 8 floor(N/8) in order, zero padded to `cs` stages, then one
+//     stage with the scalar tail (sequences 8 floor(N/8) .. N-1).  Block j's
+//     chain from 0 is lane j's f32x8 sum (lib.rs:441-444: each add rounds
+//     once, adding a masked-out 0 is exact); tot += acc after block j is the
+//     ordered horizontal sum ((((0 + l0) + l1) + ...) + l7) that packed_simd's
+//     f32x8::sum() computes on x86 (lib.rs:447-452); the tail stage continues
+//     the chain on tot itself (acc = tot before it, tot = acc after it), as
+//     the scalar loop adds onto the horizontal sums (lib.rs:461-480).  With
+//     the epilogue op for op, the rows are bit-identical to lib.rs.
+// With LOOP the workgroup strides over a tile list whose length is known only
+// on the device (the candidate tiles of the i8 screen, pair_mfma.hip).
 #include "pair_common.hpp"
 
 namespace wld {
@@ -31,283 +50,353 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 
 // MF = true: the products and f32 sums of the non-SAFE path on the matrix
 // cores, v_mfma_f32_16x16x4_f32 (f32 inputs, exact products, an f32 fma chain
-// over k: the same terms in the same sequence order as the VALU loop).  Wave w
-// owns a rows 16w..16w+15 against the tile's 64 b columns in four 16x16
-// blocks; lane l = 16g + r carries a row r (A) / b column r (B) at sequence
-// kk + g, and holds the sums of pairs (a = 16w + 4g + e, b = 16n + r) — the
-// same thread -> (4 a rows, 4 b columns) shape as the VALU mapping (a = ty +
-// 16i), so the epilogue and compaction only change how a row slot maps to a.
-// The VALU's code extraction then overlaps the matrix pipe instead of
+// over k, bitwise equal to a sequential fmaf loop: MI355X_MICROARCH.md, Matrix
+// cores).  Wave w owns a rows 16w..16w+15 against the tile's 64 b columns in
+// four 16x16 blocks; lane l = 16g + r carries a row r (A) / b column r (B) at
+// sequence kk + g, and holds the sums of pairs (a = 16w + 4g + e, b = 16n + r)
+// — the same thread -> (4 a rows, 4 b columns) shape as the VALU mapping (a =
+// ty + 16i), so the epilogue and compaction only change how a row slot maps
+// to a.  The VALU's code extraction then overlaps the matrix pipe instead of
 // competing with the FMAs for VALU issue.
 #ifndef WLD_VALU_MF_WG
 #define WLD_VALU_MF_WG 2  // MF: 164 VGPRs would fit 3 per CU; measured equal
 #endif
-template <bool DENSE, bool SAFE, bool MF>
-__global__ __launch_bounds__(256, MF ? WLD_VALU_MF_WG : 2) void pair_valu_kernel(const uint8_t *__restrict__ codes,
-                                                         const float *__restrict__ w,
-                                                         const uint8_t *__restrict__ site_ok,
-                                                         const uint32_t *__restrict__ tiles, uint32_t L, uint32_t NP,
-                                                         uint32_t flush, uint32_t n_chunk_rows, float thr, OrderArgs o,
-                                                         DenseArgs dn) {
+template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
+__global__ __launch_bounds__(256, MF ? WLD_VALU_MF_WG : 2) void pair_valu_kernel(
+    const uint8_t *__restrict__ codes, const float *__restrict__ w, const uint8_t *__restrict__ site_ok,
+    const uint32_t *__restrict__ tiles, const unsigned *tile_count, uint32_t L, uint32_t NP, uint32_t flush,
+    uint32_t ref_cs, uint32_t n_chunk_rows, float thr, OrderArgs o, DenseArgs dn) {
     __shared__ __attribute__((aligned(16))) uint8_t sA[kTile * kStride];
     __shared__ __attribute__((aligned(16))) uint8_t sB[kTile * kStride];
     __shared__ __attribute__((aligned(16))) float sW[64];
-
-    const uint32_t tile = tiles[blockIdx.x];
-    if (tile == kNoTile) return;  // padding of an XCD-ordered list (whole workgroup)
-    const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
-    const uint32_t a0 = ta * kTile, b0 = tb * kTile;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t tx = tid & 15, ty = tid >> 4;
-
-    // Two-level summation: acc holds a block of `flush` 64-sequence stages,
-    // tot the running total (tot += acc after every block).  A plain running
-    // sum over thousands of sequences loses ~N*2^-24 relative (e.g. 5008
-    // Henikoff weights of ~0.002 into a total of ~10); the reference's 8 lane
-    // sums (lib.rs:418-445) lose N/8*2^-24; blocks of ~sqrt(N) sequences
-    // (flush = round(sqrt(NP)/64), launch_pair_valu) leave ~2 sqrt(N)*2^-24.
-    float acc[4][4][4], tot[4][4][4];
-    v4f accM[4][4];  // MF: [b block n][sum q], element e = a row slot
-    // a row of the tile for row slot i of this thread (b = tx + 16 j either way)
-    auto arow = [&](int i) -> uint32_t { return MF ? 4 * ty + i : ty + 16 * i; };
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) tot[i][j][q] = 0.0f;
-
-    const uint32_t lr = tid >> 2, part = tid & 3;  // loader: site row, 16-byte part
-    const uint8_t *gA = codes + (size_t)(a0 + lr) * NP + part * 16;
-    const uint8_t *gB = codes + (size_t)(b0 + lr) * NP + part * 16;
-
-    uint32_t left = 0;  // stages until the next flush of acc into tot
-    for (uint32_t k0 = 0; k0 < NP; k0 += 64) {
-        const uint4 va = *reinterpret_cast<const uint4 *>(gA + k0);
-        const uint4 vb = *reinterpret_cast<const uint4 *>(gB + k0);
-        const float wv = tid < 64 ? w[k0 + tid] : 0.0f;
-        __syncthreads();
-        uint32_t *pa = reinterpret_cast<uint32_t *>(sA + lr * kStride + part * 16);
-        uint32_t *pb = reinterpret_cast<uint32_t *>(sB + lr * kStride + part * 16);
-        pa[0] = va.x; pa[1] = va.y; pa[2] = va.z; pa[3] = va.w;
-        pb[0] = vb.x; pb[1] = vb.y; pb[2] = vb.z; pb[3] = vb.w;
-        if (tid < 64) sW[tid] = wv;
-        __syncthreads();
-        if (left == 0) {
-            left = flush;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        acc[i][j][q] = 0.0f;
-                        accM[j][q][i] = 0.0f;
-                    }
-        }
-
-        if constexpr (MF) {
-            const uint32_t lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
-            const uint8_t *rowA = sA + (16 * wave + r) * kStride + g;
-            const uint8_t *rowB = sB + r * kStride + g;
-#pragma unroll 4
-            for (int kk = 0; kk < 64; kk += 4) {
-                const float we = sW[kk + g];
-                const uint32_t ca = rowA[kk];
-                const float u = (ca & kCodeIn) ? we : 0.0f;
-                const float v = (ca & kCodeMaj) ? we : 0.0f;
-#pragma unroll
-                for (int n = 0; n < 4; ++n) {
-                    const uint32_t cb = rowB[16 * n * kStride + kk];
-                    const float fi = (float)(cb & 1u), fm = (float)(cb >> 1);
-                    accM[n][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fi, accM[n][0], 0, 0, 0);
-                    accM[n][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fi, accM[n][1], 0, 0, 0);
-                    accM[n][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fm, accM[n][2], 0, 0, 0);
-                    accM[n][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fm, accM[n][3], 0, 0, 0);
-                }
-            }
-        } else
-
-#pragma unroll 2
-        for (int kk = 0; kk < 64; kk += 4) {
-            uint32_t A[4], B[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) A[i] = *reinterpret_cast<const uint32_t *>(sA + (ty + 16 * i) * kStride + kk);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) B[j] = *reinterpret_cast<const uint32_t *>(sB + (tx + 16 * j) * kStride + kk);
-            const float4 w4 = *reinterpret_cast<const float4 *>(sW + kk);
-            const float wk[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float we = wk[e];
-                float u[4], v[4];
-                uint32_t ca[4], cb[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    ca[i] = (A[i] >> (8 * e)) & 3u;
-                    u[i] = (ca[i] & kCodeIn) ? we : 0.0f;
-                    v[i] = (ca[i] & kCodeMaj) ? we : 0.0f;
-                }
-#pragma unroll
-                for (int j = 0; j < 4; ++j) cb[j] = (B[j] >> (8 * e)) & 3u;
-                if constexpr (!SAFE) {
-                    float fi[4], fm[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        fi[j] = (float)(cb[j] & 1u);
-                        fm[j] = (float)(cb[j] >> 1);
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            acc[i][j][0] = __builtin_fmaf(u[i], fi[j], acc[i][j][0]);
-                            acc[i][j][1] = __builtin_fmaf(v[i], fi[j], acc[i][j][1]);
-                            acc[i][j][2] = __builtin_fmaf(u[i], fm[j], acc[i][j][2]);
-                            acc[i][j][3] = __builtin_fmaf(v[i], fm[j], acc[i][j][3]);
-                        }
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const bool bi = cb[j] & 1u, bm = cb[j] & 2u;
-                            acc[i][j][0] += bi ? u[i] : 0.0f;
-                            acc[i][j][1] += bi ? v[i] : 0.0f;
-                            acc[i][j][2] += bm ? u[i] : 0.0f;
-                            acc[i][j][3] += bm ? v[i] : 0.0f;
-                        }
-                }
-            }
-        }
-        if (--left == 0 || k0 + 64 >= NP) {
-            left = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) tot[i][j][q] += MF ? accM[j][q][i] : acc[i][j][q];
-        }
-    }
-
-    // ---- epilogue ------------------------------------------------------
-    uint32_t passmask[4] = {0, 0, 0, 0};  // bit j per row i
-    float res[4][4][3];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t a = a0 + arow(i);
-        const bool oka = a < L && site_ok[a];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t b = b0 + tx + 16 * j;
-            float d, dp, r2;
-            ld_epilogue(tot[i][j][0], tot[i][j][1], tot[i][j][2], tot[i][j][3], d, dp, r2);
-            res[i][j][0] = d;
-            res[i][j][1] = dp;
-            res[i][j][2] = r2;
-            const bool valid = oka && a < b && b < L && site_ok[b];
-            if constexpr (DENSE) {
-                if (a < b && b < L) {
-                    const size_t k = (size_t)a * L + b;
-                    dn.d[k] = d;
-                    dn.dp[k] = dp;
-                    dn.r2[k] = r2;
-                    dn.valid[k] = valid ? 1 : 0;
-                }
-            } else {
-                if (valid && r2 > thr) passmask[i] |= 1u << j;  // lib.rs:660 strict '>'
-            }
-        }
-    }
-    if constexpr (DENSE) return;
-
-    // ---- compaction: rows of each a in b order, tile slice of the staging ----
     __shared__ uint8_t sMask[kTile][16];
     __shared__ uint16_t sRowM[kTile][4];
     __shared__ uint16_t sRowP[kTile][4];
     __shared__ uint32_t sRowBase[kTile];
+
+    auto compute_tile = [&](uint32_t tile, uint32_t tid) {
+        const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
+        const uint32_t a0 = ta * kTile, b0 = tb * kTile;
+        const uint32_t tx = tid & 15, ty = tid >> 4;
+
+        float acc[4][4][4], tot[4][4][4];
+        v4f accM[4][4];  // MF: [b block n][sum q], element e = a row slot
+        // a row of the tile for row slot i of this thread (b = tx + 16 j either way)
+        auto arow = [&](int i) -> uint32_t { return MF ? 4 * ty + i : ty + 16 * i; };
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sMask[arow(i)][tx] = (uint8_t)passmask[i];
-    __syncthreads();
-    if (tid < kTile) {
-        const uint32_t r = tid;
-        uint32_t M[4] = {0, 0, 0, 0};
-        for (int x = 0; x < 16; ++x) {
-            const uint32_t nib = sMask[r][x];
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) M[j] |= ((nib >> j) & 1u) << x;
-        }
-        uint32_t p = 0;
+            for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            sRowM[r][j] = (uint16_t)M[j];
-            sRowP[r][j] = (uint16_t)p;
-            p += __popc(M[j]);
-        }
-        const uint32_t cnt = p;
-        const uint32_t incl = wave_inclusive_scan(cnt);
-        const uint32_t excl = incl - cnt;
-        const uint32_t total = __shfl(incl, 63, 64);
-        unsigned long long base = 0;
-        if (r == 63 && total) base = atomicAdd(o.cursor, (unsigned long long)total);
-        base = __shfl(base, 63, 64);
-        sRowBase[r] = (uint32_t)base + excl;
-        const uint32_t a = a0 + r;
-        o.seg_cnt[(size_t)a * o.T + tb] = (uint8_t)cnt;
-        o.seg_off[(size_t)a * o.T + tb] = (uint32_t)base + excl;
-        if (r == 63 && total)
-            atomicAdd(&o.chunk_total[chunk_linear(n_chunk_rows, ta / kTilesPerChunk, tb / kTilesPerChunk)], total);
-    }
-    __syncthreads();
+                for (int q = 0; q < 4; ++q) tot[i][j][q] = 0.0f;
+
+        const uint32_t lr = tid >> 2, part = tid & 3;  // loader: site row, 16-byte part
+        const uint8_t *gA = codes + (size_t)(a0 + lr) * NP + part * 16;
+        const uint8_t *gB = codes + (size_t)(b0 + lr) * NP + part * 16;
+
+        // REF: stages [0, 8 cs) are the eight lane classes, the stage after them the tail
+        const uint32_t class_end = 8 * ref_cs;
+        uint32_t left = 0;  // default: stages until the next flush of acc into tot
+        uint32_t st = 0;
+        for (uint32_t k0 = 0; k0 < NP; k0 += 64, ++st) {
+            const uint4 va = *reinterpret_cast<const uint4 *>(gA + k0);
+            const uint4 vb = *reinterpret_cast<const uint4 *>(gB + k0);
+            const float wv = tid < 64 ? w[k0 + tid] : 0.0f;
+            __syncthreads();
+            uint32_t *pa = reinterpret_cast<uint32_t *>(sA + lr * kStride + part * 16);
+            uint32_t *pb = reinterpret_cast<uint32_t *>(sB + lr * kStride + part * 16);
+            pa[0] = va.x; pa[1] = va.y; pa[2] = va.z; pa[3] = va.w;
+            pb[0] = vb.x; pb[1] = vb.y; pb[2] = vb.z; pb[3] = vb.w;
+            if (tid < 64) sW[tid] = wv;
+            __syncthreads();
+            const bool tail = REF && st >= class_end;
+            const bool blk_start = REF ? (tail || (ref_cs && st % ref_cs == 0)) : left == 0;
+            if (blk_start) {
+                left = flush;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        if (!passmask[i]) continue;
-        const uint32_t r = arow(i);
+                for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (!(passmask[i] & (1u << j))) continue;
-            const uint64_t pos = (uint64_t)sRowBase[r] + sRowP[r][j] + __popc(sRowM[r][j] & ((1u << tx) - 1u));
-            if (pos < o.st_capacity) {
-                o.st_a[pos] = a0 + r;
-                o.st_b[pos] = b0 + tx + 16 * j;
-                o.st_d[pos] = res[i][j][0];
-                o.st_dp[pos] = res[i][j][1];
-                o.st_r2[pos] = res[i][j][2];
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            // the tail continues the chain on the horizontal sums
+                            const float v = tail ? tot[i][j][q] : 0.0f;
+                            acc[i][j][q] = v;
+                            accM[j][q][i] = v;
+                        }
             }
+
+            if constexpr (MF) {
+                const uint32_t lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
+                const uint8_t *rowA = sA + (16 * wave + r) * kStride + g;
+                const uint8_t *rowB = sB + r * kStride + g;
+#pragma unroll 4
+                for (int kk = 0; kk < 64; kk += 4) {
+                    const float we = sW[kk + g];
+                    const uint32_t ca = rowA[kk];
+                    const float u = (ca & kCodeIn) ? we : 0.0f;
+                    const float v = (ca & kCodeMaj) ? we : 0.0f;
+#pragma unroll
+                    for (int n = 0; n < 4; ++n) {
+                        const uint32_t cb = rowB[16 * n * kStride + kk];
+                        const float fi = (float)(cb & 1u), fm = (float)(cb >> 1);
+                        accM[n][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fi, accM[n][0], 0, 0, 0);
+                        accM[n][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fi, accM[n][1], 0, 0, 0);
+                        accM[n][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fm, accM[n][2], 0, 0, 0);
+                        accM[n][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fm, accM[n][3], 0, 0, 0);
+                    }
+                }
+            } else {
+#pragma unroll 2
+                for (int kk = 0; kk < 64; kk += 4) {
+                    uint32_t A[4], B[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        A[i] = *reinterpret_cast<const uint32_t *>(sA + (ty + 16 * i) * kStride + kk);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        B[j] = *reinterpret_cast<const uint32_t *>(sB + (tx + 16 * j) * kStride + kk);
+                    const float4 w4 = *reinterpret_cast<const float4 *>(sW + kk);
+                    const float wk[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float we = wk[e];
+                        float u[4], v[4];
+                        uint32_t ca[4], cb[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            ca[i] = (A[i] >> (8 * e)) & 3u;
+                            u[i] = (ca[i] & kCodeIn) ? we : 0.0f;
+                            v[i] = (ca[i] & kCodeMaj) ? we : 0.0f;
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) cb[j] = (B[j] >> (8 * e)) & 3u;
+                        if constexpr (!SAFE) {
+                            float fi[4], fm[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                fi[j] = (float)(cb[j] & 1u);
+                                fm[j] = (float)(cb[j] >> 1);
+                            }
+#pragma unroll
+                            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                                for (int j = 0; j < 4; ++j) {
+                                    acc[i][j][0] = __builtin_fmaf(u[i], fi[j], acc[i][j][0]);
+                                    acc[i][j][1] = __builtin_fmaf(v[i], fi[j], acc[i][j][1]);
+                                    acc[i][j][2] = __builtin_fmaf(u[i], fm[j], acc[i][j][2]);
+                                    acc[i][j][3] = __builtin_fmaf(v[i], fm[j], acc[i][j][3]);
+                                }
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                                for (int j = 0; j < 4; ++j) {
+                                    const bool bi = cb[j] & 1u, bm = cb[j] & 2u;
+                                    acc[i][j][0] += bi ? u[i] : 0.0f;
+                                    acc[i][j][1] += bi ? v[i] : 0.0f;
+                                    acc[i][j][2] += bm ? u[i] : 0.0f;
+                                    acc[i][j][3] += bm ? v[i] : 0.0f;
+                                }
+                        }
+                    }
+                }
+            }
+            const bool blk_end = REF ? (tail || (ref_cs && st % ref_cs == ref_cs - 1)) : (--left == 0 || k0 + 64 >= NP);
+            if (blk_end) {
+                left = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const float v = MF ? accM[j][q][i] : acc[i][j][q];
+                            tot[i][j][q] = tail ? v : tot[i][j][q] + v;
+                        }
+            }
+        }
+
+        // ---- epilogue ------------------------------------------------------
+        uint32_t passmask[4] = {0, 0, 0, 0};  // bit j per row i
+        float res[4][4][3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t a = a0 + arow(i);
+            const bool oka = a < L && site_ok[a];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t b = b0 + tx + 16 * j;
+                float d, dp, r2;
+                ld_epilogue(tot[i][j][0], tot[i][j][1], tot[i][j][2], tot[i][j][3], d, dp, r2);
+                res[i][j][0] = d;
+                res[i][j][1] = dp;
+                res[i][j][2] = r2;
+                const bool valid = oka && a < b && b < L && site_ok[b];
+                if constexpr (DENSE) {
+                    if (a < b && b < L) {
+                        const size_t k = (size_t)a * L + b;
+                        dn.d[k] = d;
+                        dn.dp[k] = dp;
+                        dn.r2[k] = r2;
+                        dn.valid[k] = valid ? 1 : 0;
+                    }
+                } else {
+                    if (valid && r2 > thr) passmask[i] |= 1u << j;  // lib.rs:660 strict '>'
+                }
+            }
+        }
+        if constexpr (DENSE) return;
+
+        // ---- compaction: rows of each a in b order, tile slice of the staging ----
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sMask[arow(i)][tx] = (uint8_t)passmask[i];
+        __syncthreads();
+        if (tid < kTile) {
+            const uint32_t r = tid;
+            uint32_t M[4] = {0, 0, 0, 0};
+            for (int x = 0; x < 16; ++x) {
+                const uint32_t nib = sMask[r][x];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) M[j] |= ((nib >> j) & 1u) << x;
+            }
+            uint32_t p = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                sRowM[r][j] = (uint16_t)M[j];
+                sRowP[r][j] = (uint16_t)p;
+                p += __popc(M[j]);
+            }
+            const uint32_t cnt = p;
+            const uint32_t incl = wave_inclusive_scan(cnt);
+            const uint32_t excl = incl - cnt;
+            const uint32_t total = __shfl(incl, 63, 64);
+            unsigned long long base = 0;
+            if (r == 63 && total) base = atomicAdd(o.cursor, (unsigned long long)total);
+            base = __shfl(base, 63, 64);
+            sRowBase[r] = (uint32_t)base + excl;
+            const uint32_t a = a0 + r;
+            o.seg_cnt[(size_t)a * o.T + tb] = (uint8_t)cnt;
+            o.seg_off[(size_t)a * o.T + tb] = (uint32_t)base + excl;
+            if (r == 63 && total)
+                atomicAdd(&o.chunk_total[chunk_linear(n_chunk_rows, ta / kTilesPerChunk, tb / kTilesPerChunk)], total);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (!passmask[i]) continue;
+            const uint32_t r = arow(i);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (!(passmask[i] & (1u << j))) continue;
+                const uint64_t pos = (uint64_t)sRowBase[r] + sRowP[r][j] + __popc(sRowM[r][j] & ((1u << tx) - 1u));
+                if (pos < o.st_capacity) {
+                    o.st_a[pos] = a0 + r;
+                    o.st_b[pos] = b0 + tx + 16 * j;
+                    o.st_d[pos] = res[i][j][0];
+                    o.st_dp[pos] = res[i][j][1];
+                    o.st_r2[pos] = res[i][j][2];
+                }
+            }
+        }
+    };
+
+    if constexpr (!LOOP) {
+        const uint32_t tile = tiles[blockIdx.x];
+        if (tile != kNoTile) compute_tile(tile, threadIdx.x);  // kNoTile: padding of an XCD-ordered list
+    } else {
+        const uint32_t nt = *tile_count;
+        for (uint32_t bi = blockIdx.x; bi < nt; bi += gridDim.x) {
+            compute_tile(tiles[bi], threadIdx.x);
+            __syncthreads();  // the next tile's staging and compaction reuse the LDS
         }
     }
 }
 
-void launch_pair_valu(const uint8_t *codes, const float *w, const uint8_t *site_ok, const uint32_t *tiles,
-                      uint32_t n_tiles, uint32_t L, uint32_t NP, uint32_t n_chunk_rows, float thr, bool safe,
-                      bool plain, const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
-    DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
-    const uint32_t flush = (uint32_t)std::max(1.0, std::floor(std::sqrt((double)NP) / 64.0 + 0.5));
+// The reference-order layout (REF): sequence seq -> position p of the lane-
+// class order.  Block j < 8 (cls positions each, cls = 0 when N < 8) holds
+// seq = 8t + j at p = j cls + t (t < floor(N/8)); the tail seq = 8 floor(N/8)
+// + t at p = 8 cls + t; every other position is padding (code 0, weight 0).
+// One thread per (site, position).
+__global__ __launch_bounds__(256) void ref_layout_kernel(const uint8_t *__restrict__ codes, const float *__restrict__ w,
+                                                         uint32_t LP, uint32_t NP, uint32_t N, uint32_t NPr,
+                                                         uint32_t cls, uint8_t *__restrict__ rcodes,
+                                                         float *__restrict__ rw) {
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (size_t)LP * NPr) return;
+    const uint32_t s = (uint32_t)(idx / NPr), p = (uint32_t)(idx % NPr);
+    const uint32_t n8 = N / 8;
+    uint32_t seq = 0xFFFFFFFFu;
+    if (p < 8 * cls) {
+        const uint32_t blk = p / cls, t = p % cls;
+        if (t < n8) seq = 8 * t + blk;
+    } else if (p - 8 * cls < N - 8 * n8) {
+        seq = 8 * n8 + (p - 8 * cls);
+    }
+    rcodes[idx] = seq < N ? codes[(size_t)s * NP + seq] : 0;
+    if (s == 0) rw[p] = seq < N ? w[seq] : 0.0f;
+}
+
+void ref_layout_dims(size_t N, uint32_t *cls, uint32_t *tail, size_t *NPr) {
+    const size_t stages = (N / 8 + 63) / 64;  // 64-sequence stages per lane class (0 when N < 8)
+    *cls = (uint32_t)(stages * 64);
+    *tail = (N % 8) ? 1u : 0u;
+    *NPr = 8 * (size_t)*cls + (*tail ? 64 : 0);
+    if (*NPr == 0) *NPr = 64;  // N == 0: one all-padding stage (a tail stage: T = 0, every pair NaN)
+}
+
+void launch_ref_layout(const uint8_t *codes, const float *w_pad, size_t LP, size_t NP, size_t N, uint8_t *rcodes,
+                       float *rw, hipStream_t s) {
+    uint32_t cls, tail;
+    size_t NPr;
+    ref_layout_dims(N, &cls, &tail, &NPr);
+    const size_t n = LP * NPr;
+    hipLaunchKernelGGL(ref_layout_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, codes, w_pad,
+                       (uint32_t)LP, (uint32_t)NP, (uint32_t)N, (uint32_t)NPr, cls, rcodes, rw);
+}
+
+namespace {
+template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
+void launch_v(const ValuLaunch &v, uint32_t grid, uint32_t flush, uint32_t cs, const OrderArgs &o,
+              const DenseArgs &dn, hipStream_t s) {
+    hipLaunchKernelGGL((pair_valu_kernel<DENSE, SAFE, MF, REF, LOOP>), dim3(grid), dim3(256), 0, s, v.codes, v.w,
+                       v.site_ok, v.tiles, v.tile_count, v.L, v.NP, flush, cs, v.n_chunk_rows, v.thr, o,
+                       dn);
+}
+}  // namespace
+
+void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
+    const DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
+    const uint32_t flush = (uint32_t)std::max(1.0, std::floor(std::sqrt((double)v.NP) / 64.0 + 0.5));
+    const uint32_t grid = v.tile_count ? std::min<uint32_t>(v.n_tiles, kCandidateGrid) : v.n_tiles;
+    if (grid == 0) return;
+    if (v.ref) {
+        // the reference's f32 order: f32-input MFMA for finite weights, the
+        // select loop otherwise (both sequential fmaf/add chains per block)
+        const uint32_t cs = v.ref_cls / 64;
+        if (dense) {
+            if (v.safe) launch_v<true, true, false, true, false>(v, grid, flush, cs, o, dn, s);
+            else launch_v<true, false, true, true, false>(v, grid, flush, cs, o, dn, s);
+        } else if (v.tile_count) {
+            if (v.safe) launch_v<false, true, false, true, true>(v, grid, flush, cs, o, dn, s);
+            else launch_v<false, false, true, true, true>(v, grid, flush, cs, o, dn, s);
+        } else {
+            if (v.safe) launch_v<false, true, false, true, false>(v, grid, flush, cs, o, dn, s);
+            else launch_v<false, false, true, true, false>(v, grid, flush, cs, o, dn, s);
+        }
+        return;
+    }
     // finite weights: products and sums on the matrix cores (plain, option
     // WLD_OPT_VALU_PLAIN: the VALU loop, for A/B); non-finite weights keep the
     // select loop
-    const dim3 g(n_tiles), b(256);
     if (dense) {
-        if (safe)
-            hipLaunchKernelGGL((pair_valu_kernel<true, true, false>), g, b, 0, s, codes, w, site_ok, tiles, L, NP,
-                               flush, n_chunk_rows, thr, o, dn);
-        else if (plain)
-            hipLaunchKernelGGL((pair_valu_kernel<true, false, false>), g, b, 0, s, codes, w, site_ok, tiles, L, NP,
-                               flush, n_chunk_rows, thr, o, dn);
-        else
-            hipLaunchKernelGGL((pair_valu_kernel<true, false, true>), g, b, 0, s, codes, w, site_ok, tiles, L, NP,
-                               flush, n_chunk_rows, thr, o, dn);
+        if (v.safe) launch_v<true, true, false, false, false>(v, grid, flush, 1, o, dn, s);
+        else if (v.plain) launch_v<true, false, false, false, false>(v, grid, flush, 1, o, dn, s);
+        else launch_v<true, false, true, false, false>(v, grid, flush, 1, o, dn, s);
     } else {
-        if (safe)
-            hipLaunchKernelGGL((pair_valu_kernel<false, true, false>), g, b, 0, s, codes, w, site_ok, tiles, L, NP,
-                               flush, n_chunk_rows, thr, o, dn);
-        else if (plain)
-            hipLaunchKernelGGL((pair_valu_kernel<false, false, false>), g, b, 0, s, codes, w, site_ok, tiles, L, NP,
-                               flush, n_chunk_rows, thr, o, dn);
-        else
-            hipLaunchKernelGGL((pair_valu_kernel<false, false, true>), g, b, 0, s, codes, w, site_ok, tiles, L, NP,
-                               flush, n_chunk_rows, thr, o, dn);
+        if (v.safe) launch_v<false, true, false, false, false>(v, grid, flush, 1, o, dn, s);
+        else if (v.plain) launch_v<false, false, false, false, false>(v, grid, flush, 1, o, dn, s);
+        else launch_v<false, false, true, false, false>(v, grid, flush, 1, o, dn, s);
     }
 }
 
