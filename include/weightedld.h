@@ -225,7 +225,10 @@ typedef struct {
 void wld_pairs_free(wld_pairs *p); /* only for host results made by this library */
 
 /* progress_report (lib.rs:582, main.rs:184-188).  Called on the calling
- * thread (never from a worker) with the running number of evaluated pairs. */
+ * thread (never from a worker): once with 0 before any work (lib.rs:584, by
+ * wld_all_weighted_ld_pairs), then once per completed 256x256 chunk with the
+ * number of pairs in the chunks completed before it — the previous value of
+ * lib.rs's fetch_add counter (lib.rs:670-674); values never decrease. */
 typedef void (*wld_progress_fn)(uint64_t pairs_done, void *user);
 
 /* Drop-in for all_weighted_ld_pairs (lib.rs:578-684).  Blocking.  sites is
@@ -330,8 +333,10 @@ void *wld_stream(wld_ctx *ctx);
 /* All pairs of the loaded set, any size, rows to host: runs the reference's
  * chunk sequence in batches of at most 2^31 pairs (one wld_run_chunks each),
  * appending each batch's rows to library-allocated host arrays in reference
- * order (release with wld_pairs_free); progress (may be NULL) gets the running
- * pair count after each batch, on the calling thread. */
+ * order (release with wld_pairs_free); progress (may be NULL) is called per
+ * completed chunk as in wld_progress_fn: the kernels count down each chunk's
+ * tiles and log finished chunks to mapped host memory, which the calling
+ * thread polls while the batch runs. */
 int wld_run_host(wld_ctx *ctx, float r2_threshold, wld_progress_fn progress, void *user, wld_pairs *out);
 /* Device pointers of the last run's rows (valid until the next run/load or
  * destroy; do not free). */

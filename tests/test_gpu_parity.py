@@ -42,6 +42,12 @@ def _ctx(ctxs, kern):
     return ctxs[kern]
 
 
+def sys_path_bench():
+    import sys
+    if REPO not in sys.path:
+        sys.path.insert(0, REPO)
+
+
 def synth(L, N, seed, p_missing=0.1, p_major=0.6, unknown=0.0):
     """bench_weighted_pair_ld.rs:8-28 distribution, seeded."""
     rng = np.random.default_rng(seed)
@@ -433,7 +439,8 @@ def test_all_weighted_ld_pairs_api_on_fixture(W):
     rows = list(store)
     assert len(rows) == 1 and rows[0][:2] == (0, 1)
     assert "%.3f %.3f %.3f" % (rows[0][2].d, rows[0][2].d_prime, rows[0][2].r2) == "0.107 0.345 0.237"
-    assert seen[0] == 0 and seen[-1] == 1
+    # lib.rs:584 then :670-674 for its one chunk: the counter before that chunk's add
+    assert seen == [0, 0]
 
 
 @pytest.mark.parametrize("name", ["synth_n200_l24.fasta", "synth_n500_l40.fasta", "synth_n2000_l30.fasta"])
@@ -733,7 +740,8 @@ def test_run_host_batches_concatenate(W, ctxs):
     ctx.set_option("host_batch_pairs", 70000)  # about one chunk per batch
     seen = []
     got = ctx.run_host(0.01, seen.append)
-    assert len(seen) > 5 and seen == sorted(seen) and seen[-1] == L * (L - 1) // 2
+    # one call per chunk (lib.rs:670-674) across batches, the counter before each chunk's add
+    assert len(seen) == ctx.chunks(L) and seen == sorted(seen) and seen[0] == 0 and seen[-1] < L * (L - 1) // 2
     for f in ("site_a", "site_b", "d", "d_prime", "r2"):
         assert np.array_equal(getattr(got, f).view(np.uint32), getattr(whole, f).view(np.uint32)), f
     compare_rows(got, ref, 0.01, buf=buf, w=w)
@@ -741,3 +749,35 @@ def test_run_host_batches_concatenate(W, ctxs):
     assert np.array_equal(store.site_a, got.site_a) and np.array_equal(store.r2.view(np.uint32),
                                                                        got.r2.view(np.uint32))
     ctx.set_option("host_batch_pairs", 1 << 31)
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0], [0, 0, 0]])
+def test_progress_once_per_chunk_config2(W, devices):
+    """lib.rs reports progress once per 256x256 chunk (lib.rs:670-674, after
+    the initial 0 of :584): at BASELINE config 2 (2000 sites: 36 chunks) the
+    drop-in calls back 37 times, on the calling thread, with the running
+    count of pairs in the chunks finished before each one — values that never
+    decrease and step by whole chunks — single-device and as a device group."""
+    import threading
+    sys_path_bench()
+    from bench import synth as bench_synth
+    from bench import chunk_pairs
+    L, N = 2000, 500
+    buf = bench_synth(L, N)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ctx = W.Context(0, devices=devices) if devices else W.Context(0)
+    seen, threads = [], set()
+
+    def cb(n):
+        seen.append(n)
+        threads.add(threading.get_ident())
+    store = W.all_weighted_ld_pairs(W.SiteSet.from_buffer(buf), w, 0.0, progress_report=cb, ctx=ctx)
+    n_chunks = ctx.chunks(L)
+    assert n_chunks == 36
+    assert len(seen) == 1 + n_chunks, len(seen)
+    assert seen[0] == 0 and seen[1] == 0 and seen == sorted(seen)
+    assert threads == {threading.get_ident()}
+    steps = sorted(np.diff(seen[1:]).tolist() + [L * (L - 1) // 2 - seen[-1]])
+    assert steps == sorted(chunk_pairs(L, i) for i in range(n_chunks))
+    assert len(store) > 1_990_000
+

@@ -10,9 +10,12 @@
 // point fails with WLD_E_NODEV.
 #include <algorithm>
 #include <cmath>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -141,18 +144,27 @@ struct wld_ctx {
     bool screened2 = false; // ... on two digit planes
     uint64_t rows = 0;
     wld_run_stats stats{};
+    // per-chunk progress (wld_run_host with a callback): the run's chunk
+    // countdowns and log slot counter on the device, the log in mapped pinned
+    // host memory (one u64 pair count per completed chunk, ~0 until written)
+    DevBuf chunk_left, prog_n;
+    unsigned long long *h_plog = nullptr, *d_plog = nullptr;
+    size_t plog_cap = 0;
+    const std::function<void(uint64_t)> *on_chunk = nullptr;  // set by run_host_range for its runs
+    bool prog_pass = false;  // the pass in flight logs its chunks
 
     ~wld_ctx() {
         for (wld_ctx *m : members) delete m;
         if (!members.empty()) return;
         (void)hipSetDevice(device);
         DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &rcodes, &rw, &tiles, &cand,
-                         &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &st_a, &st_b, &st_d,
+                         &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &chunk_left, &prog_n, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         if (h_cnt) (void)hipHostFree(h_cnt);
+        if (h_plog) (void)hipHostFree(h_plog);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -426,6 +438,10 @@ OrderArgs order_args(wld_ctx *c) {
     o.T = (uint32_t)(c->LP / kTile);
     o.chunk_total = ptr<uint32_t>(c->chunk_total);
     o.cursor = ptr<unsigned long long>(c->counters);
+    o.chunk_left = c->prog_pass ? ptr<unsigned>(c->chunk_left) : nullptr;
+    o.prog_n = c->prog_pass ? ptr<unsigned>(c->prog_n) : nullptr;
+    o.prog_log = c->prog_pass ? c->d_plog : nullptr;
+    o.L = (uint32_t)c->L;
     return o;
 }
 
@@ -941,7 +957,55 @@ int run_enqueue(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uns
     WLD_TRY(ensure(c->counters, 4 * sizeof(unsigned long long)));
     if (c->chunk_total.bytes != ct_bytes || c->counters.bytes != cn_bytes) c->run_dirty = true;  // fresh memory
     c->pend = RunPending{true, thr, lin_begin, lin_end, pairs, count_out};
+    c->prog_pass = false;
+    if (c->on_chunk && lin_end > lin_begin) {
+        // per-chunk progress: countdowns of the range's chunks, an empty log
+        const uint32_t cnt = lin_end - lin_begin;
+        WLD_TRY(ensure(c->chunk_left, std::max<size_t>(n_chunks, 1) * sizeof(unsigned)));
+        WLD_TRY(ensure(c->prog_n, sizeof(unsigned)));
+        if (c->plog_cap < cnt) {
+            if (c->h_plog) (void)hipHostFree(c->h_plog);
+            c->h_plog = c->d_plog = nullptr;
+            c->plog_cap = 0;
+            HIP_TRY(hipHostMalloc((void **)&c->h_plog, (size_t)cnt * sizeof(unsigned long long),
+                                  hipHostMallocMapped | hipHostMallocCoherent));
+            HIP_TRY(hipHostGetDevicePointer((void **)&c->d_plog, c->h_plog, 0));
+            c->plog_cap = cnt;
+        }
+        memset(c->h_plog, 0xFF, (size_t)cnt * sizeof(unsigned long long));
+        launch_progress_init(ptr<unsigned>(c->chunk_left), lin_begin, cnt, n, (uint32_t)c->L, ptr<unsigned>(c->prog_n),
+                             c->stream);
+        HIP_TRY(hipGetLastError());
+        c->prog_pass = true;
+    }
     return enqueue_pass(c);
+}
+
+// The progress log of a pass with per-chunk progress: every chunk pair count
+// logged so far, in slot order, to on_chunk (on the calling thread), polled
+// while the pass runs; then the rest once it has completed.
+int drain_progress(wld_ctx *c, uint32_t n_chunks) {
+    uint32_t seen = 0;
+    auto drain = [&] {
+        while (seen < n_chunks) {
+            const unsigned long long v = __atomic_load_n(&c->h_plog[seen], __ATOMIC_ACQUIRE);
+            if (v == ~0ull) break;
+            (*c->on_chunk)(v);
+            ++seen;
+        }
+    };
+    for (;;) {
+        const hipError_t q = hipStreamQuery(c->stream);
+        drain();
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) HIP_TRY(q);
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+    // the pass has completed: every chunk's entry is written (system-scope
+    // stores); allow the last ones a moment to land
+    for (int spin = 0; seen < n_chunks && spin < 100000; ++spin) drain();
+    if (seen < n_chunks) return fail(WLD_E_HIP, "internal: %u of %u chunk progress entries arrived", seen, n_chunks);
+    return WLD_OK;
 }
 
 // Phase 2: one host wait, the overflow re-run if needed, then (only when rows
@@ -954,6 +1018,10 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     const uint32_t lin_count = r.lin_end - r.lin_begin;
     unsigned long long h[3] = {0, 0, 0};
     for (int attempt = 0; attempt < 2; ++attempt) {
+        if (c->prog_pass) {
+            c->prog_pass = false;  // a re-run after a staging overflow does not report again
+            WLD_TRY(drain_progress(c, lin_count));
+        }
         HIP_TRY(hipStreamSynchronize(c->stream));
         c->run_dirty = false;  // the pass completed: its scan cleaned the run state
         h[0] = __atomic_load_n(&c->h_cnt[0], __ATOMIC_ACQUIRE);
@@ -1155,10 +1223,10 @@ namespace {
 // The chunks [lb, le) of the loaded set, rows to host: batches of whole
 // chunks, contiguous in the reference order, of at most opt_host_batch_pairs
 // (2^31) pairs each (a run's staging positions are 32-bit); their rows
-// concatenate in order.  progress (may be null) gets the running pair count
-// per batch.
-int run_host_range(wld_ctx *c, float r2_threshold, uint32_t lb, uint32_t le, wld_progress_fn progress, void *user,
-                   wld_pairs *out) {
+// concatenate in order.  on_chunk (may be null) gets each chunk's pair count
+// as the chunk completes, on the calling thread.
+int run_host_range(wld_ctx *c, float r2_threshold, uint32_t lb, uint32_t le,
+                   const std::function<void(uint64_t)> *on_chunk, wld_pairs *out) {
     memset(out, 0, sizeof(*out));
     WLD_TRY(set_dev(c));
     if (!c->loaded) return fail(WLD_E_STATE, "wld_run_host before wld_load");
@@ -1188,7 +1256,10 @@ int run_host_range(wld_ctx *c, float r2_threshold, uint32_t lb, uint32_t le, wld
             ++e;
         }
         uint64_t rows = 0;
-        if ((st = run_chunks(c, r2_threshold, b, e, &rows)) != WLD_OK) break;
+        c->on_chunk = on_chunk;
+        st = run_chunks(c, r2_threshold, b, e, &rows);
+        c->on_chunk = nullptr;
+        if (st != WLD_OK) break;
         if ((st = grow(done + rows)) != WLD_OK) break;
         if (rows &&
             (st = wld_rows_copy(c, out->site_a + done, out->site_b + done, out->d + done, out->d_prime + done,
@@ -1196,7 +1267,6 @@ int run_host_range(wld_ctx *c, float r2_threshold, uint32_t lb, uint32_t le, wld
             break;
         done += rows;
         pairs_done += pairs;
-        if (progress) progress(pairs_done, user);
         b = e;
     }
     if (st != WLD_OK) {
@@ -1211,10 +1281,11 @@ int run_host_range(wld_ctx *c, float r2_threshold, uint32_t lb, uint32_t le, wld
 
 // wld_run_host on a device group: member k runs shard k of the reference's
 // chunk sequence (wld_shard_chunks: contiguous, balanced by pair count) on
-// its own host thread (each run blocks on its device); the calling thread
-// reports progress as shards complete and concatenates the shards' rows in
-// DESCENDING shard order (shard 0 holds the last chunks).
-int run_host_group(wld_ctx *g, float thr, wld_progress_fn progress, void *user, wld_pairs *out) {
+// its own host thread (each run blocks on its device); the members' chunk
+// completions queue up for the calling thread, which reports them (on_chunk)
+// and concatenates the shards' rows in DESCENDING shard order (shard 0 holds
+// the last chunks).
+int run_host_group(wld_ctx *g, float thr, const std::function<void(uint64_t)> *on_chunk, wld_pairs *out) {
     const int G = (int)g->members.size();
     const size_t L = g->members[0]->L;
     std::vector<wld_pairs> part(G);
@@ -1231,10 +1302,16 @@ int run_host_group(wld_ctx *g, float thr, wld_progress_fn progress, void *user, 
         WLD_TRY(wld_shard_chunks(L, G, k, &lb[k], &le[k]));
         pairs[k] = pairs_in_chunks(L, lb[k], le[k]);
     }
+    std::deque<uint64_t> events;  // chunk pair counts from the members, in completion order
+    const std::function<void(uint64_t)> push = [&](uint64_t p) {
+        std::lock_guard<std::mutex> lk(mu);
+        events.push_back(p);
+        cv.notify_one();
+    };
     std::vector<std::thread> th;
     for (int k = 0; k < G; ++k) {
         th.emplace_back([&, k] {
-            const int st = run_host_range(g->members[k], thr, lb[k], le[k], nullptr, nullptr, &part[k]);
+            const int st = run_host_range(g->members[k], thr, lb[k], le[k], on_chunk ? &push : nullptr, &part[k]);
             std::lock_guard<std::mutex> lk(mu);
             status[k] = st;
             if (st != WLD_OK) msg[k] = wld_last_error();
@@ -1243,17 +1320,23 @@ int run_host_group(wld_ctx *g, float thr, wld_progress_fn progress, void *user, 
         });
     }
     uint64_t pairs_done = 0;
-    for (int n = 0; n < G; ++n) {  // progress on the calling thread, as shards complete
-        int k;
+    for (;;) {  // progress on the calling thread, chunk by chunk
+        std::deque<uint64_t> batch;
+        bool all_done;
         {
             std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return (int)finished.size() > n; });
-            k = finished[n];
+            cv.wait(lk, [&] { return !events.empty() || (int)finished.size() == G; });
+            batch.swap(events);
+            all_done = (int)finished.size() == G;
         }
-        pairs_done += pairs[k];
-        if (progress && status[k] == WLD_OK) progress(pairs_done, user);
+        for (uint64_t p : batch) (*on_chunk)(p);
+        if (all_done) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (events.empty()) break;
+        }
     }
     for (auto &t : th) t.join();
+    for (int k = 0; k < G; ++k) pairs_done += pairs[k];
     int st = WLD_OK;
     for (int k = 0; k < G; ++k)
         if (status[k] != WLD_OK && st == WLD_OK) st = fail(status[k], "device %d (shard %d): %s", g->members[k]->device, k, msg[k].c_str());
@@ -1300,12 +1383,20 @@ int wld_run_host(wld_ctx *c, float r2_threshold, wld_progress_fn progress, void 
     if (!out) return fail(WLD_E_ARG, "null out");
     memset(out, 0, sizeof(*out));
     if (!c) return fail(WLD_E_ARG, "null context");
+    // lib.rs:670-674: per chunk, the running count of pairs in the chunks
+    // completed BEFORE it (fetch_add's previous value)
+    uint64_t before = 0;
+    const std::function<void(uint64_t)> on_chunk = [&](uint64_t p) {
+        progress(before, user);
+        before += p;
+    };
+    const std::function<void(uint64_t)> *oc = progress ? &on_chunk : nullptr;
     if (!c->members.empty()) {
         for (wld_ctx *m : c->members)
             if (!m->loaded) return fail(WLD_E_STATE, "wld_run_host before wld_load");
-        return run_host_group(c, r2_threshold, progress, user, out);
+        return run_host_group(c, r2_threshold, oc, out);
     }
-    return run_host_range(c, r2_threshold, 0, chunks_of(c->L), progress, user, out);
+    return run_host_range(c, r2_threshold, 0, chunks_of(c->L), oc, out);
 }
 
 int wld_all_weighted_ld_pairs(wld_ctx *c, const uint8_t *sites, size_t n_sites, size_t n_seqs,

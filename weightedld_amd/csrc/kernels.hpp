@@ -32,6 +32,14 @@ struct OrderArgs {
     uint32_t T;         // number of 64-wide tiles (LP / 64)
     uint32_t *chunk_total;  // [n_chunks_total] rows per reference chunk (linear triu index)
     unsigned long long *cursor;  // staging allocation cursor
+    // per-chunk progress (lib.rs:670-674; wld_run_host with a callback, else
+    // null): tiles left per linear chunk; the workgroup that finishes a
+    // chunk's last tile appends the chunk's pair count to the mapped host log
+    // at slot atomicAdd(prog_n, 1) (tile_done, pair_common.hpp)
+    unsigned *chunk_left;
+    unsigned *prog_n;
+    unsigned long long *prog_log;
+    uint32_t L;  // sites of the loaded set (a chunk's pair count)
 };
 
 struct DenseArgs {
@@ -128,6 +136,10 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
                       hipEvent_t screen_done);
 
 // order.hip
+// per-chunk progress of the chunks [lin_begin, lin_begin + count): tiles per
+// chunk into chunk_left[lin], prog_n = 0
+void launch_progress_init(unsigned *chunk_left, uint32_t lin_begin, uint32_t count, uint32_t n_chunk_rows, uint32_t L,
+                          unsigned *prog_n, hipStream_t s);
 // zeroes the run state (staging cursor, row total, every chunk total)
 void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t n_chunks, hipStream_t s);
 // count_out (device, may be null): also receives the run's row total
@@ -145,6 +157,14 @@ void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_
 __host__ __device__ inline uint32_t chunk_linear(uint32_t n, uint32_t row, uint32_t col) {
     uint32_t rf = n - 1 - row;
     return rf * (rf + 1) / 2 + (col - row);
+}
+
+// pairs (a < b) of chunk (row, col) of an L-site set: lib.rs:636-667's loops
+__host__ __device__ inline uint64_t chunk_pairs(uint32_t L, uint32_t row, uint32_t col) {
+    const uint64_t lo_a = (uint64_t)row * kChunk, lo_b = (uint64_t)col * kChunk;
+    const uint64_t ra = lo_a >= L ? 0 : (L - lo_a < (uint64_t)kChunk ? L - lo_a : (uint64_t)kChunk);
+    const uint64_t rb = lo_b >= L ? 0 : (L - lo_b < (uint64_t)kChunk ? L - lo_b : (uint64_t)kChunk);
+    return row == col ? ra * (ra ? ra - 1 : 0) / 2 : ra * rb;
 }
 
 }  // namespace wld

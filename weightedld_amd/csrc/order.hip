@@ -158,6 +158,28 @@ __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t
     }
 }
 
+// tiles of each chunk of [lin_begin, lin_begin + count) in the pair kernels'
+// lists (b tile >= a tile, inside the set's T_used tiles)
+__global__ __launch_bounds__(256) void progress_init_kernel(unsigned *__restrict__ chunk_left, uint32_t lin_begin,
+                                                             uint32_t count, uint32_t n_chunk_rows, uint32_t T_used,
+                                                             unsigned *__restrict__ prog_n) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) *prog_n = 0;
+    if (i >= count) return;
+    uint32_t row, col;
+    chunk_of_linear(n_chunk_rows, lin_begin + i, row, col);
+    const uint32_t ra = min(T_used - min(T_used, row * kTilesPerChunk), (uint32_t)kTilesPerChunk);
+    const uint32_t rb = min(T_used - min(T_used, col * kTilesPerChunk), (uint32_t)kTilesPerChunk);
+    chunk_left[lin_begin + i] = row == col ? ra * (ra + 1) / 2 : ra * rb;
+}
+
+void launch_progress_init(unsigned *chunk_left, uint32_t lin_begin, uint32_t count, uint32_t n_chunk_rows, uint32_t L,
+                          unsigned *prog_n, hipStream_t s) {
+    const uint32_t T_used = (L + kTile - 1) / kTile;
+    hipLaunchKernelGGL(progress_init_kernel, dim3((std::max<uint32_t>(count, 1) + 255) / 256), dim3(256), 0, s,
+                       chunk_left, lin_begin, count, n_chunk_rows, T_used, prog_n);
+}
+
 void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t n_chunks, hipStream_t s) {
     const unsigned blocks = (unsigned)std::min<size_t>((std::max<size_t>(n_chunks, 4) + 255) / 256, 2048);
     hipLaunchKernelGGL(run_init_kernel, dim3(blocks), dim3(256), 0, s, counters, chunk_total, n_chunks);

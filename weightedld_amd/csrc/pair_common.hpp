@@ -183,6 +183,20 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
 }
 
+// A tile of the run is finished (one thread of its workgroup): with per-chunk
+// progress on, the workgroup that finishes its chunk's last tile appends the
+// chunk's pair count to the host log (the value lib.rs's per-chunk
+// fetch_add adds, lib.rs:670-671; the host sums the log in slot order).
+__device__ __forceinline__ void tile_done(const OrderArgs &o, uint32_t ta, uint32_t tb, uint32_t n_chunk_rows) {
+    if (!o.chunk_left) return;
+    const uint32_t row = ta / kTilesPerChunk, col = tb / kTilesPerChunk;
+    if (atomicSub(&o.chunk_left[chunk_linear(n_chunk_rows, row, col)], 1u) == 1u) {
+        const unsigned slot = atomicAdd(o.prog_n, 1u);
+        __hip_atomic_store(&o.prog_log[slot], (unsigned long long)chunk_pairs(o.L, row, col), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
     const int lane = threadIdx.x & 63;
 #pragma unroll

@@ -475,8 +475,9 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
         }
         if (__syncthreads_or(cand)) {
             if (tid == 0) sc.cand_list[atomicAdd(sc.cand_count, 1u)] = (ta << 16) | tb;
-        } else if (tid < kTile) {
-            o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
+        } else {
+            if (tid < kTile) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
+            if (tid == 0) tile_done(o, ta, tb, n_chunk_rows);  // rejected: finished here
         }
         return;
     }
@@ -515,6 +516,7 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
     // seg_cnt > 0).  One barrier decides it.
     if (!__syncthreads_or(pass != 0)) {
         if (tid < kTile) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
+        if (tid == 0) tile_done(o, ta, tb, n_chunk_rows);
         return;
     }
     if (tid < kTile) sBits[tid] = 0ull;
@@ -560,6 +562,7 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
             }
         }
     }
+    if (tid == 0) tile_done(o, ta, tb, n_chunk_rows);
 }
 
 // LDS-streaming kernel over fragment-major, selector-coded codes, one 64x64

@@ -299,6 +299,7 @@ __global__ __launch_bounds__(256, MF ? WLD_VALU_MF_WG : 2) void pair_valu_kernel
                 }
             }
         }
+        if (tid == 0) tile_done(o, ta, tb, n_chunk_rows);
     };
 
     if constexpr (!LOOP) {
