@@ -151,10 +151,14 @@ def cpu_baseline(buf, w, thr, target_s=15.0, max_s=30.0):
     n = (L + 255) // 256
     nchunks = n * (n + 1) // 2
 
+    last = {}
+
     def run(k):
         t0 = time.perf_counter()
         r = O.all_pairs(buf, w, thr, n_threads=threads, chunk_lo=0, chunk_hi=k)
-        return r["pairs"], time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        last.update(rows=r, chunks=k)
+        return r["pairs"], dt
 
     # calibrate on ~1/16 of the chunks (enough work to amortise thread start-up)
     k = min(nchunks, max(4 * threads, nchunks // 16))
@@ -173,7 +177,7 @@ def cpu_baseline(buf, w, thr, target_s=15.0, max_s=30.0):
         k2 = max(k2, 1)
         what = "the first %d of %d reference chunks (256x256, triu order) of the same workload" % (k2, nchunks)
     p, t = run(k2)
-    return {"value": p / t, "unit": "site-pairs/s", "cores": threads, "kind": "port",
+    return last["rows"], last["chunks"], {"value": p / t, "unit": "site-pairs/s", "cores": threads, "kind": "port",
             "sample": "%s = %d pairs in %.1f s; C restatement of the lib.rs simd path (8-lane f32, rayon-style "
                       "chunk scheduling), gcc -O3 -march=native" % (what, p, t)}
 
@@ -216,7 +220,14 @@ def main():
                     help="every tile with every weight-digit plane (WLD_OPT_SCREEN 0; same rows)")
     ap.add_argument("--no-prefilter", action="store_true",
                     help="every pair through the f32 epilogue (WLD_OPT_PREFILTER 0, implies --no-screen; same rows)")
+    ap.add_argument("--data", default="random", choices=["random", "ldblocks"],
+                    help="random: the seeded bench_weighted_pair_ld.rs distribution (the headline); ldblocks: the "
+                         "same size with linkage blocks of 20-200 sites (many rows, candidate tiles)")
+    ap.add_argument("--exact-sums", action="store_true",
+                    help="exact sums rounded once (WLD_OPT_REF_SUMS 0) instead of the default, lib.rs's own f32 "
+                         "summation order (rows bit-identical to lib.rs)")
     args = ap.parse_args()
+    args.ref_sums = not args.exact_sums
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,7 +255,7 @@ def main():
     if args.thr is not None and args.thr != thr:
         thr = args.thr
         desc += " (r2_threshold overridden to %g)" % thr
-    buf = synth(L, N)
+    buf = synth(L, N) if args.data == "random" else ld_blocks(L, N)
     t0 = time.perf_counter()
     ss = W.SiteSet.from_buffer(buf)
     kept = ss.filter_sites_of_interest()  # host pre-pass (lib.rs:309-338, main.rs:139)
@@ -283,6 +294,7 @@ def main():
             c.set_option("prefilter", 0)
         if args.tile_rows:
             c.set_option("tile_order", 1)
+        c.set_option("ref_sums", 0 if args.exact_sums else 1)
         c.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
         return c
 
@@ -455,9 +467,21 @@ def main():
     roof["pair_phase_ms"] = kernel_ms
     roof["pair_phase_frac"] = alg_ops / (kernel_ms * 1e-3) / 1e12 / roof["peak"]
     if screened:
+        n_cand = float(np.mean(cand))
+        cand_ms = kernel_ms - screen_ms
+        # the candidate launch: every plane of its tiles (or, --ref-sums, the
+        # f32 reference-order kernel), algorithmic work 8N per pair of its
+        # tiles (4096 pairs each, diagonal tiles counted whole)
+        cand_peak = F32_VALU_PEAK_TFLOPS if args.ref_sums else I8_MFMA_PEAK_TOPS
+        cand_ops = n_cand * 4096 * 8.0 * N
         roof["screen"] = {"kind": {3: "i8 two-plane"}.get(screen_kind, "i8"), "tiles": n_tiles,
-                          "candidate_tiles": float(np.mean(cand)),
-                          "candidate_launch_ms": kernel_ms - screen_ms, "unscreened_pair_kernel_ms": unscreened_ms,
+                          "candidate_tiles": n_cand, "candidate_fraction": n_cand / max(n_tiles, 1),
+                          "screen_ms": screen_ms, "candidate_launch_ms": cand_ms,
+                          "candidate_kernel": ("pair_valu_kernel<ref order, f32 MFMA>" if args.ref_sums else
+                                               "pair_mfma_kernel<prefilter, %d planes>" % planes),
+                          "candidate_frac": (cand_ops / (cand_ms * 1e-3) / 1e12 / cand_peak) if cand_ms > 0.02 else None,
+                          "candidate_peak": cand_peak,
+                          "unscreened_pair_kernel_ms": unscreened_ms,
                           "unscreened_frac": alg_ops / (unscreened_ms * 1e-3) / 1e12 / roof["peak"]}
     # PMC traffic (profiles/traffic.json) was measured on the default C4 line's
     # dominant kernel (the one-plane i8 screen); other lines report null
@@ -466,11 +490,21 @@ def main():
                    and not (args.rehearse_dist and args.rehearse_shard > 1))
     roof["traffic"] = tr.get("hbm_bytes_per_launch") if tr and same_kernel else None
     hbm_alg = shard_pairs * 2.0 * N / (kernel_ms * 1e-3) / 1e9  # 2N bytes per pair
-    if kern_name == "mfma":
-        dtype = ("i8 digit planes of 24-bit fixed-point weights (%d plane%s), exact i32 sums, f32 epilogue"
-                 % (planes, "s" if planes > 1 else ""))
+    # the arithmetic the timed steps executed
+    fixed = "%d-bit fixed-point weights" % (31 if planes == 4 else 23)
+    if kern_name == "mfma" and screened:
+        dtype = ("i8 MFMA screen on the top weight digit%s (i32 sums, rigorous f32/f64 r2 bound over every pair); "
+                 "candidate tiles (%.0f of %d): %s" % (
+                     "s (2 planes)" if screen_kind == 3 else " (1 plane)", float(np.mean(cand)), n_tiles,
+                     "f32 sums in lib.rs's order on f32 MFMA, f32 epilogue" if args.ref_sums else
+                     "%d i8 digit plane%s of %s, exact i32 sums, f32 epilogue" % (planes, "s" if planes > 1 else "",
+                                                                                  fixed)))
+    elif kern_name == "mfma" and not args.ref_sums:
+        dtype = "i8 MFMA, %d digit plane%s of %s, exact i32 sums, f32 epilogue" % (planes, "s" if planes > 1 else "",
+                                                                                   fixed)
     else:
-        dtype = "f32"
+        dtype = "f32 MFMA (exact products, f32 sums%s), f32 epilogue" % (
+            " in lib.rs's order" if args.ref_sums else "")
     out = {
         "metric": METRIC,
         "value": value,
@@ -483,7 +517,9 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": dtype,
-        "data": "synthetic (seeded bench_weighted_pair_ld.rs distribution, %s weights)" % (
+        "data": "synthetic (%s, %s weights)" % (
+            "seeded bench_weighted_pair_ld.rs distribution" if args.data == "random" else
+            "seeded linkage blocks of 20-200 sites (bench.ld_blocks)",
             "unit (--unweighted)" if args.unweighted else
             "Henikoff, every 10th x 2^-8 (--wide-weights)" if args.wide_weights else "Henikoff"),
         "config": {"workload": desc, "n_seqs": N, "n_sites": L, "r2_threshold": thr, "pairs": total_pairs,
@@ -505,7 +541,27 @@ def main():
                       "step_minus_kernel_rank0": float(np.median(gms))},
     }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(buf, weights, thr, args.cpu_seconds)
+        oref, ochunks, out["cpu_baseline"] = cpu_baseline(buf, weights, thr, args.cpu_seconds)
+        # the same chunks on the GPU: rows against the oracle's (lib.rs
+        # semantics).  Exact sums rounded once may put a pair whose r2 lies
+        # within 1e-5 of the threshold on the other side of the strict '>'
+        # (never more); --ref-sums must match exactly.
+        ctx.run_chunks(thr, 0, ochunks)
+        g = ctx.rows()
+        kg = set(zip(g.site_a.tolist(), g.site_b.tolist()))
+        kr = set(zip(oref["site_a"].tolist(), oref["site_b"].tolist()))
+        r2g = dict(zip(zip(g.site_a.tolist(), g.site_b.tolist()), g.r2.tolist()))
+        r2r = dict(zip(zip(oref["site_a"].tolist(), oref["site_b"].tolist()), oref["r2"].tolist()))
+        one_sided = [r2g[k] for k in kg - kr] + [r2r[k] for k in kr - kg]
+        out["rows_check"] = {"chunks": ochunks, "gpu_rows": len(kg), "oracle_rows": len(kr),
+                             "one_sided": len(one_sided),
+                             "one_sided_outside_1e-5_of_thr": sum(abs(v - thr) > 1e-5 for v in one_sided)}
+        whole = ochunks == ctx.chunks(L) and (cb, ce) == (0, ctx.chunks(L))
+        if whole:
+            out["rows_check"]["timed_rows_passing"] = rows  # the last timed step's rows: the same run
+        assert out["rows_check"]["one_sided_outside_1e-5_of_thr"] == 0, out["rows_check"]
+        assert not args.ref_sums or len(one_sided) == 0, out["rows_check"]
+        assert not whole or rows == len(kg), (rows, len(kg))
     print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()

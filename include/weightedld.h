@@ -177,21 +177,24 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *                      next load).
  *   WLD_OPT_VALU_PLAIN 0 (default): the f32 fallback multiplies on f32-input
  *                      MFMA; 1: a VALU fmaf loop (same sums, same order).
- *   WLD_OPT_REF_SUMS   0 (default): each of the four masked sums is computed
- *                      exactly (integer MFMA) or with error below the
- *                      reference's own (f32 kernel), then rounded once; 1: the
- *                      sums are formed in lib.rs's own f32 order (8 lane sums
- *                      of sequences k = j mod 8, lib.rs:416-445, their ordered
- *                      horizontal sum, packed_simd's x86 f32x8::sum(),
- *                      :447-452, then the scalar tail, :461-480) on the f32
- *                      kernel, so rows are bit-identical to lib.rs's even where
- *                      its f32 sums are inaccurate (minor alleles carried by a
- *                      few low-weight sequences).  With the MFMA kernel and a
- *                      positive threshold the i8 screen still runs first, its
- *                      bound widened by the reference's rounding, and only
- *                      candidate tiles take the f32 kernel.  The one option
- *                      that changes results (in the last bits, or more where
- *                      the reference's sums are ill-conditioned).
+ *   WLD_OPT_REF_SUMS   1 (default): the four masked sums of every pair are
+ *                      formed in lib.rs's own f32 order — 8 lane sums of the
+ *                      sequences k = j mod 8 (lib.rs:416-445), their ordered
+ *                      horizontal sum (packed_simd's x86 f32x8::sum(),
+ *                      :447-452), then the scalar tail (:461-480) — on the f32
+ *                      kernel, so d, d' and r2 are bit-identical to lib.rs's
+ *                      on every input, including pairs whose f32 sums lib.rs
+ *                      itself gets wrong (minor alleles carried by a few
+ *                      low-weight sequences).  With the MFMA kernel and a
+ *                      positive threshold the i8 screen runs first, its bound
+ *                      widened by the reference's rounding, and only candidate
+ *                      tiles take the f32 kernel.  0: exact sums (integer
+ *                      MFMA, all digit planes; the f32 kernel's two-level sums
+ *                      when the weights need it) rounded once — more accurate
+ *                      than lib.rs, faster where many tiles are candidates
+ *                      (linkage, thresholds <= 0), and different from lib.rs
+ *                      in the last bits (or more on ill-conditioned pairs).
+ *                      The one option that changes results.
  *   WLD_OPT_STAGING_ROWS   initial staging capacity in rows (default 2^25;
  *                      grown on overflow by a re-run).
  *   WLD_OPT_HOST_BATCH_PAIRS  pairs per batch of wld_run_host (default 2^31).

@@ -18,7 +18,10 @@ from conftest import CLI, FIXTURES, REPO, SYNTH
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-5
-KERNELS = ["valu", "mfma"]
+# "valu" / "mfma": the f32 kernel's two-level sums and the integer MFMA
+# kernel's exact sums (WLD_OPT_REF_SUMS 0); "ref": the default, lib.rs's own
+# f32 summation order (bit-identical to the oracle; within TOL a fortiori)
+KERNELS = ["valu", "mfma", "ref"]
 
 
 @pytest.fixture(scope="module")
@@ -29,11 +32,19 @@ def W():
 
 @pytest.fixture(scope="module")
 def ctxs(W):
-    out = {"valu": W.Context(0, W.KERNEL_VALU)}
+    out = {"valu": W.Context(0, W.KERNEL_VALU, ref_sums=False)}
     if W.lib().wld_set_kernel(out["valu"]._h, W.KERNEL_MFMA) == 0:
-        out["mfma"] = W.Context(0, W.KERNEL_MFMA)
+        out["mfma"] = W.Context(0, W.KERNEL_MFMA, ref_sums=False)
     out["valu"].set_kernel(W.KERNEL_VALU)
+    out["ref"] = W.Context(0)
     return out
+
+
+def new_ctx(W, kern, **kw):
+    """A fresh context of the same kind as ctxs[kern]."""
+    if kern == "ref":
+        return W.Context(0, **kw)
+    return W.Context(0, W.KERNEL_MFMA if kern == "mfma" else W.KERNEL_VALU, ref_sums=False, **kw)
 
 
 def _ctx(ctxs, kern):
@@ -369,7 +380,7 @@ def test_rows_vs_oracle(ctxs, kern, L, N, thr):
 def test_staging_overflow_regrows(W, ctxs, kern):
     # staging starts tiny, the run detects the overflow from the cursor and re-runs
     _ctx(ctxs, kern)
-    ctx = W.Context(0, W.KERNEL_MFMA if kern == "mfma" else W.KERNEL_VALU)  # fresh: no grown staging
+    ctx = new_ctx(W, kern)  # fresh: no grown staging
     ctx.set_option("staging_rows", 100)
     L, N = 700, 150
     buf = synth(L, N, 5)
@@ -565,14 +576,14 @@ def test_mfma_lds_pipeline_race_screen(W):
     # epilogue (no prefilter, no screen); under test: the LDS kernel behind the
     # one- and two-plane screens (at 0.001 nearly every tile is a candidate:
     # the looping candidate launch) with the prefilter
-    ref_ctx = W.Context(0, W.KERNEL_MFMA)
+    ref_ctx = W.Context(0, W.KERNEL_MFMA, ref_sums=False)
     ref_ctx.set_option("prefilter", 0)
     ref_ctx.set_option("mfma_layout", 1)
     ref_ctx.load(buf, w)
     n_ref = ref_ctx.run(0.001)
     ref = wdist.pack_rows_device(ref_ctx, n_ref, dev)
     del ref_ctx
-    ctx = W.Context(0, W.KERNEL_MFMA)
+    ctx = W.Context(0, W.KERNEL_MFMA, ref_sums=False)
     ctx.load(buf, w)
     assert n_ref > 10_000_000
     # forced: auto would send 0.001 to the full kernel after the first run

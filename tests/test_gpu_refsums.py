@@ -1,21 +1,23 @@
 """GPU tests of the reference summation order (WLD_OPT_REF_SUMS) and of how
-far the default path's rows lie from lib.rs's on ill-conditioned inputs.
+far the exact-sum path's rows lie from lib.rs's on ill-conditioned inputs.
 
 lib.rs sums each pair's four masked weights in f32 in its own order: 8 lane
 sums over sequences k = j mod 8 (lib.rs:416-445), their horizontal sum
-(:447-452), then the scalar tail (:461-480).  The default GPU path sums
-exactly (integer MFMA) and rounds once, which is more accurate but differs
-from lib.rs by lib.rs's own rounding — far beyond 1e-5 where a minor allele is
-carried by a few low-weight sequences.  With WLD_OPT_REF_SUMS the f32 kernel
+(:447-452), then the scalar tail (:461-480).  The exact-sum path
+(WLD_OPT_REF_SUMS 0) sums exactly (integer MFMA) and rounds once, which is
+more accurate but differs from lib.rs by lib.rs's own rounding — far beyond
+1e-5 where a minor allele is carried by a few low-weight sequences.  With
+WLD_OPT_REF_SUMS 1 (the default) the f32 kernel
 adds the same terms in the same order (sequences permuted into lane classes,
 the ordered horizontal sum packed_simd's x86 f32x8::sum() computes), so
 d, d' and r2 must be BIT-identical to the oracle's (oracle/wld_oracle.c, the
 C restatement of lib.rs with the same order) — on every pair, every input,
 with or without the i8 screen in front.
 
-The report tests print, per input, the default path's row-set and %.3f
-TSV-line differences against the oracle, and the reference-order path's
-against the oracle under both horizontal-sum orders (ordered, packed_simd's
+The report tests print, per input, the exact-sum path's (WLD_OPT_REF_SUMS 0)
+row-set and %.3f TSV-line differences against the oracle, and the
+reference-order path's (the default) against the oracle under both
+horizontal-sum orders (ordered, packed_simd's
 implementation; tree, its documentation): tests/conftest.py REF_REPORT.
 """
 import sys
@@ -239,10 +241,10 @@ def _report_set(W, name, buf, w, thrs):
     for order in ("ordered", "tree"):
         with O.hsum_order(order):
             refs[order] = O.all_pairs(buf, w, lo)
-    dflt = W.Context(0, W.KERNEL_AUTO)
+    dflt = W.Context(0, W.KERNEL_AUTO, ref_sums=False)  # exact sums rounded once
     dflt.load(buf, w)
-    refc = W.Context(0, W.KERNEL_AUTO)
-    refc.set_option("ref_sums", 1)
+    refc = W.Context(0, W.KERNEL_AUTO)  # the default: lib.rs's order
+    assert refc.get_option("ref_sums") == 1
     refc.load(buf, w)
     out = {}
     for thr in thrs:
@@ -253,7 +255,7 @@ def _report_set(W, name, buf, w, thrs):
         d_rows = dflt.rows()
         refc.run(thr)
         r_rows = refc.rows()
-        for mode, rows in (("default", d_rows), ("ref_sums", r_rows)):
+        for mode, rows in (("exact", d_rows), ("ref_sums", r_rows)):
             for order in ("ordered", "tree"):
                 res = row_diff(rows, sub[order], thr)
                 out[(thr, mode, order)] = res
@@ -282,10 +284,8 @@ def test_report_full_bench_workloads(W, cfg):
     lo = np.float32(0.01)
     ref = O.all_pairs(buf, w, lo)
     assert ref["pairs"] == L * (L - 1) // 2
-    for mode in ("default", "ref_sums"):
-        ctx = W.Context(0, W.KERNEL_AUTO)
-        if mode == "ref_sums":
-            ctx.set_option("ref_sums", 1)
+    for mode in ("exact", "ref_sums"):
+        ctx = W.Context(0, W.KERNEL_AUTO, ref_sums=mode == "ref_sums")
         ctx.load(buf, w)
         for t in (thr, 0.01):
             t32 = np.float32(t)

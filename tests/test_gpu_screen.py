@@ -399,7 +399,7 @@ def test_clustered_alignment_wide_range_on_integer_kernel(W):
     nz = w[w > 0]
     rng_log2 = float(np.log2(nz.min() / nz.max()))
     assert -12 < rng_log2 < -10, rng_log2
-    ctx = W.Context(0, W.KERNEL_AUTO)
+    ctx = W.Context(0, W.KERNEL_AUTO, ref_sums=False)
     ctx.load(buf, w)
     st = ctx.stats()
     assert st["kernel"] == W.KERNEL_MFMA and st["mfma_planes"] == 4, st
@@ -414,7 +414,7 @@ def test_clustered_alignment_wide_range_on_integer_kernel(W):
               "(screened %d), run %.1f ms" % (rng_log2, thr, n, ctx.stats()["pair_kernel_ms"],
                                                ctx.stats()["screened"], dt * 1e3))
     # the f32 kernel on the same input, for the record
-    v = W.Context(0, W.KERNEL_VALU)
+    v = W.Context(0, W.KERNEL_VALU, ref_sums=False)
     v.load(buf, w)
     v.run(0.0)
     print("  f32 kernel: pair phase %.3f ms" % v.stats()["pair_kernel_ms"])
@@ -454,7 +454,7 @@ def test_weights_at_mfma_range_boundary(W, N, spread, planes):
     small = rng.random(N) < 0.5
     small[0] = False
     w[small] = np.float32(spread * (1 + 2.0 ** -12))
-    ctx = W.Context(0, W.KERNEL_AUTO)
+    ctx = W.Context(0, W.KERNEL_AUTO, ref_sums=False)
     ctx.load(buf, w)
     assert ctx.stats()["kernel"] == W.KERNEL_MFMA and ctx.stats()["mfma_planes"] == planes
     dense_check(ctx, buf, w)

@@ -2,12 +2,15 @@
 # Builds an experimental variant of libweightedld.so with extra compile flags on
 # pair_mfma.hip (other objects shared with the main build):
 #   tools/build_variant.sh NAME "-DFLAG ..."   -> build/exp/NAME/libweightedld.so
+# SLP=1 builds pair_mfma.hip without -fno-slp-vectorize (packed-f32 probe).
 set -e
 cd "$(dirname "$0")/.."
 name=$1; flags=$2
 make -s build/obj/encode.o build/obj/prepass.o build/obj/pair_valu.o build/obj/order.o build/obj/capi.o build/obj/host.o
 out=build/exp/$name; mkdir -p $out
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Iinclude \
+slp=-fno-slp-vectorize
+[ "${SLP:-0}" = 1 ] && slp=
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $slp -Wall -Iinclude \
   -Iweightedld_amd/csrc $flags -c weightedld_amd/csrc/pair_mfma.hip -o $out/pair_mfma.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/libweightedld.so build/obj/encode.o build/obj/prepass.o \
   build/obj/pair_valu.o $out/pair_mfma.o build/obj/order.o build/obj/capi.o build/obj/host.o -lpthread

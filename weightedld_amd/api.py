@@ -201,9 +201,11 @@ class PairStore:
 class Context:
     """One device context (wld_ctx): HIP stream, device buffers, results."""
 
-    def __init__(self, device=0, kernel=KERNEL_AUTO, devices=None):
+    def __init__(self, device=0, kernel=KERNEL_AUTO, devices=None, ref_sums=None):
         """devices (a list of HIP ordinals, repeats allowed): a multi-device
-        context (wld_create_multi) that shards load/run_host/all-pairs calls."""
+        context (wld_create_multi) that shards load/run_host/all-pairs calls.
+        ref_sums (WLD_OPT_REF_SUMS): None keeps the library default (lib.rs's
+        own f32 summation order, bit-identical rows); False: exact sums."""
         h = ctypes.c_void_p()
         self._lib = lib()  # kept: module globals may be gone when __del__ runs at exit
         if devices is not None:
@@ -216,6 +218,8 @@ class Context:
         self.device = device
         if kernel != KERNEL_AUTO:
             self.set_kernel(kernel)
+        if ref_sums is not None:
+            self.set_option("ref_sums", int(bool(ref_sums)))
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -233,7 +237,7 @@ class Context:
     def set_option(self, name, value):
         """wld_set_option: name is a key of OPTIONS ("prefilter", "screen",
         "tile_order", "all_planes", "mfma_layout", "valu_plain", "staging_rows",
-        "host_batch_pairs"); no option changes a result."""
+        "host_batch_pairs", "ref_sums"); only "ref_sums" changes a result."""
         check(lib().wld_set_option(self._h, OPTIONS[name], int(value)), "wld_set_option")
 
     def get_option(self, name):

@@ -109,7 +109,7 @@ struct wld_ctx {
     float screen_bad_thr = -1.0f;   // auto: the largest threshold at which the screen left > half the tiles
     float screen2_bad_thr = -1.0f;  // auto: ... at which the two-plane screen left > a fifth of them
     bool opt_site_major = false, opt_valu_plain = false;
-    bool opt_ref_sums = false;  // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order
+    bool opt_ref_sums = true;  // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order (default)
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
 
     // loaded SiteSet
@@ -483,6 +483,7 @@ double ref_extra_residual(const wld_ctx *c) {
 int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *dense, bool *screened = nullptr) {
     const uint32_t n = chunk_rows_of(c->L);
     bool sc = false;
+    c->stats.ref_sums = c->opt_ref_sums ? 1 : 0;
     ValuLaunch rv{};
     if (c->opt_ref_sums) {
         WLD_TRY(ensure_ref_layout(c));
@@ -1060,7 +1061,6 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     c->stats.pair_kernel_launches = c->n_tiles ? (c->screened ? 2 : 1) : 0;
     c->stats.tiles = c->n_tiles;
     c->stats.screened = c->screened ? (c->screened2 ? 3 : 1) : 0;
-    c->stats.ref_sums = c->opt_ref_sums ? 1 : 0;
     // auto: a threshold at which even the i8 screen leaves more than half the
     // tiles is not screened from now on (nor any lower one): the screen costs a
     // third of the full three-plane kernel, the candidates as much again

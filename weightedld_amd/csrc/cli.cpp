@@ -111,6 +111,7 @@ struct Opt {
     float min_acgt = 0.8f, min_minor = 0.02f, max_minor = 0.5f, r2_threshold = 0.1f;
     bool unweighted = false;
     bool gpu_prepass = false;
+    bool exact_sums = false;  // --exact-sums: WLD_OPT_REF_SUMS 0
     int device = 0;
     std::vector<int> devices;  // --devices: a multi-device context
     int kernel = WLD_KERNEL_AUTO;
@@ -125,6 +126,8 @@ void usage(FILE *f) {
             "    -h, --help          Prints help information\n"
             "        --unweighted    Use unit weights instead of Henikoff weights\n"
             "        --gpu-prepass   Filter sites and compute Henikoff weights on the GPU (FASTA input)\n"
+            "        --exact-sums    (addition) exact masked sums rounded once, instead of lib.rs's own f32\n"
+            "                        summation order (the default: output identical to the reference)\n"
             "    -V, --version       Prints version information\n\n"
             "OPTIONS:\n"
             "        --fasta-input <fasta-input>          The source file to load\n"
@@ -206,6 +209,8 @@ Opt parse(int argc, char **argv) {
             have_pair = true;
         } else if (a == "--unweighted") {
             o.unweighted = true;
+        } else if (a == "--exact-sums") {
+            o.exact_sums = true;
         } else if (a == "--gpu-prepass") {
             o.gpu_prepass = true;
         } else if (a == "--device") {
@@ -452,6 +457,10 @@ int main(int argc, char **argv) {
         if (opt.kernel != WLD_KERNEL_AUTO) {
             int s2 = wld_set_kernel(ctx, opt.kernel);
             if (s2 != WLD_OK) die(s2, "wld_set_kernel");
+        }
+        if (opt.exact_sums) {
+            int s2 = wld_set_option(ctx, WLD_OPT_REF_SUMS, 0);
+            if (s2 != WLD_OK) die(s2, "wld_set_option");
         }
         return ctx;
     };
