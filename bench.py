@@ -437,7 +437,10 @@ def main():
     # the shard (its bound, from one digit plane of every sequence); the
     # candidate launch recomputes the few tiles it cannot reject.
     alg_ops = shard_pairs * 8.0 * N
-    if kern_name == "mfma":
+    # the f32 kernel ran every tile: the f32 fallback, or the reference order
+    # without a screen in front (thresholds <= 0, --no-screen)
+    f32_path = kern_name == "valu" or (args.ref_sums and not screened)
+    if not f32_path:
         # the dominant kernel's peak: dense i8 MFMA (no sparsity)
         peak, unit = I8_MFMA_PEAK_TOPS, "TFLOP/s"
         dom_ms = screen_ms if screened else kernel_ms
@@ -462,7 +465,8 @@ def main():
         # f32 vector peak (MI355X_MICROARCH.md, Matrix cores: F32 row)
         roof = {"bound": "mfma", "achieved": achieved, "peak": F32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / F32_VALU_PEAK_TFLOPS, "path": "f32 MFMA 16x16x4",
-                "work": "algorithmic: 8*N f32 flops per site pair", "kernel": "pair_valu_kernel",
+                "work": "algorithmic: 8*N f32 flops per site pair",
+                "kernel": "pair_valu_kernel<%s>" % ("lib.rs order" if args.ref_sums else "two-level sums"),
                 "kernel_ms": kernel_ms}
     roof["pair_phase_ms"] = kernel_ms
     roof["pair_phase_frac"] = alg_ops / (kernel_ms * 1e-3) / 1e12 / roof["peak"]
