@@ -756,7 +756,7 @@ def test_run_host_batches_concatenate(W, ctxs):
     for f in ("site_a", "site_b", "d", "d_prime", "r2"):
         assert np.array_equal(getattr(got, f).view(np.uint32), getattr(whole, f).view(np.uint32)), f
     compare_rows(got, ref, 0.01, buf=buf, w=w)
-    store = W.all_weighted_ld_pairs(W.SiteSet.from_buffer(buf), w, 0.01)
+    store = W.all_weighted_ld_pairs(W.SiteSet.from_buffer(buf), w, 0.01, ctx=ctx)
     assert np.array_equal(store.site_a, got.site_a) and np.array_equal(store.r2.view(np.uint32),
                                                                        got.r2.view(np.uint32))
     ctx.set_option("host_batch_pairs", 1 << 31)
