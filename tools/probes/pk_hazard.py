@@ -10,8 +10,8 @@ variants that differ only in how pair_mfma.hip was compiled
 (tools/build_variant.sh):
   pk_base      -fno-slp-vectorize (the shipped flags)           reference
   pk_slp       SLP on (packed f32 in the epilogue)
-  pk_slp_pad1  SLP on + -mllvm -amdgpu-snop-padding=1 (s_nop 1 before EVERY instruction)
-  pk_slp_pad4  SLP on + -mllvm -amdgpu-snop-padding=4
+  pk_slp_padK  SLP on + -mllvm -amdgpu-snop-padding=K (s_nop K, K+1 wait states,
+               before EVERY instruction), K = 1..4
 and counts, per run, the values that differ from pk_base bit for bit and the
 accumulator rows (a mod 16) they fall on.  If padding every instruction with
 wait states removes the errors, the packed code is right and a wait state is
@@ -19,6 +19,7 @@ missing (a pipeline hazard the compiler does not pad); if the errors stay,
 it is not a hazard between instructions.
 
     python tools/probes/pk_hazard.py [--reps 3]      (GPU box; prints one JSON line per run)
+    python tools/probes/pk_hazard.py --small         (640 sites: one workgroup per CU, 40 runs)
 """
 import argparse
 import json
@@ -29,22 +30,30 @@ import sys
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-VARIANTS = ["pk_base", "pk_slp", "pk_slp_pad1", "pk_slp_pad4"]
+VARIANTS = ["pk_base", "pk_slp", "pk_slp_pad1", "pk_slp_pad2", "pk_slp_pad3", "pk_slp_pad4"]
 L, N = 3000, 2000
+# --small: 640 sites = 55 tiles on 256 CUs, one workgroup per CU (no
+# co-resident waves on the SIMD), REPS dense runs in one process
+SMALL_L, SMALL_REPS = 640, 40
 
 
-def child(variant, out_npz):
+def child(variant, out_npz, small=False):
     sys.path.insert(0, REPO)
     import torch  # noqa: F401  (one HIP runtime: torch's)
     import weightedld_amd._lib as WL
     WL.LIB_PATH = os.path.join(REPO, "build", "exp", variant, "libweightedld.so")
     import bench
     import weightedld_amd as W
-    buf = bench.synth(L, N)
+    Ls = SMALL_L if small else L
+    buf = bench.synth(Ls, N)
     w = np.ones(N, dtype=np.float32)
-    ctx = W.Context(0, W.KERNEL_MFMA)
+    ctx = W.Context(0, W.KERNEL_MFMA, ref_sums=False)
     ctx.load(buf, w)
     assert ctx.stats()["mfma_planes"] == 1
+    if small:  # stack the repetitions' dense stats along a new axis
+        runs = [ctx.dense(Ls) for _ in range(SMALL_REPS)]
+        np.savez(out_npz, r2=np.stack([r[2] for r in runs]))
+        return
     d, dp, r2, valid = ctx.dense(L)
     ctx.set_option("screen", 0)  # the unscreened one-plane prefilter kernel
     ctx.run(0.001)
@@ -76,15 +85,35 @@ def compare(ref, got):
     return res
 
 
+def compare_small(ref, got):
+    bad = (ref["r2"].view(np.uint32) != got["r2"].view(np.uint32)) & ~(np.isnan(ref["r2"]) & np.isnan(got["r2"]))
+    iu = np.triu_indices(SMALL_L, 1)
+    b = bad[:, iu[0], iu[1]]
+    rows = np.zeros(16, dtype=np.int64)
+    np.add.at(rows, np.nonzero(b)[1] * 0 + iu[0][np.nonzero(b)[1]] % 16, 1)
+    return {"small_L": SMALL_L, "reps": SMALL_REPS, "r2_values": int(b.size), "r2_bad": int(b.sum()),
+            "bad_by_a_mod_16": rows.tolist()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--child", nargs=2)
+    ap.add_argument("--small", action="store_true")
     a = ap.parse_args()
     if a.child:
-        child(*a.child)
+        child(*a.child, small=a.small)
         return
     tmp = os.environ.get("TMPDIR", "/tmp")
+    if a.small:
+        ref_path = os.path.join(tmp, "pk_ref_small.npz")
+        subprocess.run([sys.executable, __file__, "--small", "--child", "pk_base", ref_path], check=True, timeout=300)
+        ref = np.load(ref_path)
+        for v in ("pk_slp", "pk_slp_pad1"):
+            p = os.path.join(tmp, "pk_small_%s.npz" % v)
+            subprocess.run([sys.executable, __file__, "--small", "--child", v, p], check=True, timeout=300)
+            print(json.dumps({"variant": v, **compare_small(ref, np.load(p))}), flush=True)
+        return
     ref_path = os.path.join(tmp, "pk_ref.npz")
     subprocess.run([sys.executable, __file__, "--child", "pk_base", ref_path], check=True, timeout=300)
     ref = np.load(ref_path)
