@@ -196,7 +196,9 @@ def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)  # the clock ramps over the first launches
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle-s", type=float, default=0.3,
+                    help="untimed back-to-back steps before the warmup while the GPU clock settles (seconds)")
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--kernel", default="auto", choices=["auto", "valu", "mfma"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -370,6 +372,24 @@ def main():
             pipe.submit(thr, cb, ce)
         return nrows(pipe.drain())
 
+    # Clock settle (untimed, before the warmup): back-to-back steps for about
+    # settle_s seconds.  The pair kernel's time falls over the first ~30
+    # launches as the clock settles (rocprofv3 trace of `--steps 20 --warmup
+    # 5`, profiles/r03c/: a C4 screen launch 1.07 -> 0.90 ms), so a short
+    # warmup would time the ramp, not the kernel.  Every rank runs the same
+    # number of steps (their collectives pair up).
+    settle_steps = 0
+    if args.settle_s > 0:
+        t1 = time.perf_counter()
+        run_steps(3)
+        torch.cuda.synchronize()
+        per = (time.perf_counter() - t1) / 3
+        settle_steps = int(np.ceil(args.settle_s / max(per, 1e-4)))
+        if dist_on:
+            t = torch.tensor([settle_steps], dtype=torch.int64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            settle_steps = int(t.item())
+        run_steps(settle_steps)
     run_steps(args.warmup)
     if dist_on:
         dist.barrier()
@@ -516,6 +536,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle_steps": settle_steps,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
         "scaling": "strong",

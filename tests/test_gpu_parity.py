@@ -481,6 +481,45 @@ def test_gpu_vcf_config3_vs_python(W, python_ref):
 
 
 
+def test_gpu_vcf_config3_unweighted_vs_python(W, python_ref):
+    """BASELINE config 3's unweighted leg: the HIP path's rows on the t7 VCF
+    with unit weights (main.rs:150-153) equal lib.rs's (the oracle, bit for
+    bit: the default summation order), and Python's own rule on top of them —
+    skip a pair when round(PA, 1) or round(PB, 1) is 1.0 over the sequences
+    major or minor at both sites (WeightedLD.py:197-237) — leaves exactly what
+    Python prints: the header alone (WeightedLD.py:176, tests/golden)."""
+    g = python_ref["t7_1000genome.vcf"]
+    ss = W.read_vcf(os.path.join(FIXTURES, "t7_1000genome.vcf"))
+    buf, sm = ss.buffer, ss.site_map
+    ones = np.ones(ss.n_seqs(), dtype=np.float32)
+    store = W.all_weighted_ld_pairs(ss, ones, float("-inf"))
+    ref = O.all_pairs(buf, ones, float("-inf"), site_map=sm)
+    assert len(store) == len(ref["site_a"]) == 10
+    assert np.array_equal(store.site_a.astype(np.uint64), ref["site_a"])
+    assert np.array_equal(store.site_b.astype(np.uint64), ref["site_b"])
+    for f in ("d", "d_prime", "r2"):
+        assert np.array_equal(getattr(store, f).view(np.uint32), ref[f].view(np.uint32)), f
+    idx = {int(p): i for i, p in enumerate(sm)}
+    printed = []
+    for a, b, d, dp, r2 in zip(store.site_a, store.site_b, store.d, store.d_prime, store.r2):
+        x, y = buf[idx[int(a)]], buf[idx[int(b)]]
+        keep = (x != 5) & (y != 5)  # WeightedLD.py:181-185: Unknown at either site dropped
+        fr = []
+        for col in (x[keep], y[keep]):
+            vals, cnt = np.unique(col, return_counts=True)
+            order = np.argsort(-cnt, kind="stable")
+            fr.append((vals[order[0]], vals[order[1]] if len(vals) > 1 else None))
+        (ma, na), (mb, nb) = fr
+        tgt = keep.copy()
+        tgt[keep] = ((x[keep] == ma) | (x[keep] == na)) & ((y[keep] == mb) | (y[keep] == nb))
+        PA = np.mean(x[tgt] == ma)
+        PB = np.mean(y[tgt] == mb)
+        if round(PA, 1) == 1.0 or round(PB, 1) == 1.0:  # WeightedLD.py:234-237
+            continue
+        printed.append((int(a), int(b), float(d), float(dp), float(r2)))
+    assert printed == g["pairs_unweighted"] == []
+
+
 # SURVEY.md App. D: expected Rust CLI output derived from lib.rs semantics
 CLI_EXPECT = {
     ("example.fasta", False): ["0\t1\t0.107\t0.345\t0.237"],
