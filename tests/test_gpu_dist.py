@@ -1,0 +1,105 @@
+"""The N>1 step path with real device contexts at world 2-3 (one GPU).
+
+Every rank is its own process owning real Contexts on device 0 and runs its
+chunk-range shard (wld_shard_chunks) through ShardStep / PipelinedShardStep —
+the bench's N>1 loop: wld_run_chunks_async on the library's stream, the
+pipelined steps queued behind each other with wld_run_after, wld_run_wait,
+the rows copied out with wld_rows_copy_device.  RCCL refuses two ranks on one
+device, so the counts and rows travel as host tensors over gloo
+(host_collectives=True); the device side is exactly the bench's.  Rank 0
+checks every step's gathered rows against the unsharded oracle, bit for bit
+(the default summation order is lib.rs's), over a threshold sequence in
+which every rank, no rank or only some ranks have rows (lib.rs:635-679 split
+over ranks and reassembled in reference order).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import REPO
+from test_dist import _free_port, ld_region_data
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_step_worker(rank, world, port, L, N, thrs, mode, q):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import torch
+    import torch.distributed as dist
+
+    import _oracle as O
+    import weightedld_amd as W
+    from weightedld_amd import dist as wdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        buf, w = ld_region_data(L, N, 5)
+        lo, hi = wdist.shard_chunks(L, world, rank)
+        depth = int(mode[0]) if mode != "step" else 1
+        ctxs = [W.Context(0) for _ in range(depth)]
+        for c in ctxs:
+            c.load(buf, w)
+        results = []
+        if mode == "step":
+            step = wdist.ShardStep(ctxs[0], rank, world, dev, host_collectives=True)
+            results = [step(t, lo, hi) for t in thrs]
+        else:
+            pipe = wdist.PipelinedShardStep(ctxs, rank, world, dev, host_collectives=True,
+                                            serialize_kernels="pair" if mode.endswith("pair") else False)
+            for t in thrs:
+                r = pipe.submit(t, lo, hi)
+                if r is not None:
+                    results.append(r)
+            results += pipe.drain_all()
+        torch.cuda.synchronize()
+        mine = [int(n) for n, _ in results]
+        counts = [None] * world
+        dist.all_gather_object(counts, mine)
+        if rank == 0:
+            ok = []
+            for i, t in enumerate(thrs):
+                ref = O.all_pairs(buf, w, np.float32(t), n_threads=4)
+                got = wdist.unpack_rows(results[i][1])
+                ok.append(len(got["site_a"]) == len(ref["site_a"]) and
+                          all(np.array_equal(got[f], ref[f].astype(got[f].dtype)) if f in ("site_a", "site_b") else
+                              np.array_equal(got[f].view(np.uint32), ref[f].view(np.uint32))
+                              for f in wdist.ROW_FIELDS))
+            q.put((ok, counts))
+        else:
+            assert all(r[1] is None for r in results)
+        for c in ctxs:
+            c.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["step", "2pair", "3pair", "2"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_shard_steps_multi_rank(world, mode):
+    L, N = 1200, 200
+    thrs = [0.0, 2.0, 0.5, 2.0, 0.0, 0.5, 0.5]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_step_worker, args=(r, world, port, L, N, thrs, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert all(c == 0 for c in codes), codes
+    ok, counts = q.get(timeout=10)
+    assert all(ok), ok
+    per_step = list(zip(*counts))
+    assert all(sum(c) == 0 for c, t in zip(per_step, thrs) if t == 2.0)
+    assert any(0 < sum(1 for x in c if x) < world for c, t in zip(per_step, thrs) if t == 0.5)

@@ -129,14 +129,21 @@ class ShardStep:
 
     ctx is anything with the Context methods the step uses
     (run_chunks_async, run_wait, rows_copy_device, stream_ptr); with a CPU
-    `device` the step runs in program order on host tensors (gloo)."""
+    `device` the step runs in program order on host tensors (gloo).
+    host_collectives=True keeps the device's kernels and the context's
+    stream but exchanges counts and rows as host tensors (gloo): several
+    ranks on one GPU, where RCCL refuses a duplicate device (the multi-rank
+    GPU test); the count then reaches the host before its all_gather."""
 
-    def __init__(self, ctx, rank, world, device, group=None):
+    def __init__(self, ctx, rank, world, device, group=None, host_collectives=False):
         import torch
 
         self.ctx = ctx
-        self.gather = RowGather(rank, world, device, group)
         device = torch.device(device)
+        self.host = host_collectives and device.type == "cuda"
+        self.gather = RowGather(rank, world, torch.device("cpu") if self.host else device, group)
+        self.cnt_dev = torch.zeros(1, dtype=torch.int64, device=device) if self.host else None
+        self.device = device
         self.stream = (torch.cuda.ExternalStream(ctx.stream_ptr(), device=device) if device.type == "cuda"
                        else _HostStream())
         self.rows_seen = False  # some rank had rows in the last finished step
@@ -150,23 +157,31 @@ class ShardStep:
 
         g = self.gather
         with _stream_scope(self.stream):
-            self.ctx.run_chunks_async(thr, chunk_begin, chunk_end, g.cnt.data_ptr())
+            self.ctx.run_chunks_async(thr, chunk_begin, chunk_end, (self.cnt_dev if self.host else g.cnt).data_ptr())
             if kernel_done is not None:
                 kernel_done.record(self.stream)
-            dist.all_gather_into_tensor(g.cnts, g.cnt, group=g.group)
+            if not self.host:
+                dist.all_gather_into_tensor(g.cnts, g.cnt, group=g.group)
 
     def finish(self):
         """Completes an enqueued step: (rows on this rank, gathered rows on rank 0 / None)."""
         import torch
+        import torch.distributed as dist
 
         g = self.gather
+        if self.host:
+            with _stream_scope(self.stream):
+                g.cnt.fill_(int(self.cnt_dev.item()))  # host wait for this step's count
+            dist.all_gather_into_tensor(g.cnts, g.cnt, group=g.group)
         with _stream_scope(self.stream):
             counts = g.cnts.tolist()  # the step's one host wait when no rank has rows
         self.rows_seen = max(counts) > 0
         n = self.ctx.run_wait()  # returns at once: the stream is idle
         if max(counts) == 0:
             return n, (g.cnt.new_zeros((5, 0), dtype=torch.int32) if g.rank == 0 else None)
-        packed = pack_rows_device(self.ctx, n, g.device)
+        packed = pack_rows_device(self.ctx, n, self.device)
+        if self.host:
+            packed = packed.cpu()
         return n, (packed if g.world == 1 else g(packed, counts))
 
     def __call__(self, thr, chunk_begin, chunk_end):
@@ -195,11 +210,11 @@ class PipelinedShardStep:
     on every rank (count all_gathers in submit order, a step's row gather when
     it completes), so the sequence is the same everywhere."""
 
-    def __init__(self, ctxs, rank, world, device, group=None, serialize_kernels=False):
+    def __init__(self, ctxs, rank, world, device, group=None, serialize_kernels=False, host_collectives=False):
         import torch
 
         assert len(ctxs) >= 2
-        self.steps = [ShardStep(c, rank, world, device, group) for c in ctxs]
+        self.steps = [ShardStep(c, rank, world, device, group, host_collectives) for c in ctxs]
         self.done = ([torch.cuda.Event() for _ in ctxs] if torch.device(device).type == "cuda"
                      else [_HostEvent() for _ in ctxs])
         self.serialize = serialize_kernels  # False: step i's kernel may start in step i-1's tail
