@@ -26,7 +26,7 @@ def child(path, config, reps, thr, unweighted=False):
     else:
         N, Ls, thr0, _ = bench.CONFIGS[config]
     thr = thr0 if thr is None else thr
-    buf = bench.synth(Ls, N)
+    buf = bench.ld_blocks(Ls, N) if os.environ.get("WLD_AB_DATA") == "ldblocks" else bench.synth(Ls, N)
     w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
     if unweighted:
         w = np.ones(N, dtype=np.float32)

@@ -489,7 +489,7 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         WLD_TRY(ensure_ref_layout(c));
         rv = ValuLaunch{ptr<uint8_t>(c->rcodes), ptr<float>(c->rw), ptr<uint8_t>(c->site_ok), ptr<uint32_t>(c->tiles),
                         c->n_tiles, nullptr, (uint32_t)c->L, (uint32_t)c->NPr, n, thr, c->safe, false, true,
-                        c->ref_cls};
+                        c->ref_cls, (uint32_t)(c->N % 8)};
     }
     // reference order without a screen in front (no positive threshold, the
     // f32 kernel, dense stats, or the auto policy's full-kernel thresholds):
@@ -544,7 +544,7 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
     } else {
         launch_pair_valu(ValuLaunch{ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), ptr<uint8_t>(c->site_ok),
                                     ptr<uint32_t>(c->tiles), c->n_tiles, nullptr, (uint32_t)c->L, (uint32_t)c->NP, n,
-                                    thr, c->safe, c->opt_valu_plain, false, 0},
+                                    thr, c->safe, c->opt_valu_plain, false, 0, 0},
                          o, dense, c->stream);
     }
     HIP_TRY(hipGetLastError());

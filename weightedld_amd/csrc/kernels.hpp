@@ -75,6 +75,7 @@ struct ValuLaunch {
     bool plain;  // WLD_OPT_VALU_PLAIN: the VALU fmaf loop instead of f32 MFMA
     bool ref;    // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order
     uint32_t ref_cls;  // REF: sequence positions per lane class (multiple of 64, 0 when N < 8)
+    uint32_t ref_tail_n;  // REF: the scalar tail's sequences (N mod 8), in the stage after the classes
 };
 void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
 // the lane-class layout of REF: cls positions per class, the tail stage, NPr

@@ -32,10 +32,10 @@
 //     chain from 0 is lane j's f32x8 sum (lib.rs:441-444: each add rounds
 //     once, adding a masked-out 0 is exact); tot += acc after block j is the
 //     ordered horizontal sum ((((0 + l0) + l1) + ...) + l7) that packed_simd's
-//     f32x8::sum() computes on x86 (lib.rs:447-452); the tail stage continues
-//     the chain on tot itself (acc = tot before it, tot = acc after it), as
-//     the scalar loop adds onto the horizontal sums (lib.rs:461-480).  With
-//     the epilogue op for op, the rows are bit-identical to lib.rs.
+//     f32x8::sum() computes on x86 (lib.rs:447-452); the <= 7 tail sequences
+//     are then added onto tot one by one on the VALU, as the scalar loop adds
+//     onto the horizontal sums (lib.rs:461-480).  With the epilogue op for
+//     op, the rows are bit-identical to lib.rs.
 // With LOOP the workgroup strides over a tile list whose length is known only
 // on the device (the candidate tiles of the i8 screen, pair_mfma.hip).
 #include "pair_common.hpp"
@@ -61,11 +61,14 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 #ifndef WLD_VALU_MF_WG
 #define WLD_VALU_MF_WG 2  // MF: 164 VGPRs would fit 3 per CU; measured equal
 #endif
+#ifndef WLD_VALU_REF_WG
+#define WLD_VALU_REF_WG 3  // MF + REF: three workgroups per CU (<= 168 VGPRs; 2 leave 208)
+#endif
 template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
-__global__ __launch_bounds__(256, MF ? WLD_VALU_MF_WG : 2) void pair_valu_kernel(
+__global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) : 2) void pair_valu_kernel(
     const uint8_t *__restrict__ codes, const float *__restrict__ w, const uint8_t *__restrict__ site_ok,
     const uint32_t *__restrict__ tiles, const unsigned *tile_count, uint32_t L, uint32_t NP, uint32_t flush,
-    uint32_t ref_cs, uint32_t n_chunk_rows, float thr, OrderArgs o, DenseArgs dn) {
+    uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, OrderArgs o, DenseArgs dn) {
     __shared__ __attribute__((aligned(16))) uint8_t sA[kTile * kStride];
     __shared__ __attribute__((aligned(16))) uint8_t sB[kTile * kStride];
     __shared__ __attribute__((aligned(16))) float sW[64];
@@ -94,11 +97,8 @@ __global__ __launch_bounds__(256, MF ? WLD_VALU_MF_WG : 2) void pair_valu_kernel
         const uint8_t *gA = codes + (size_t)(a0 + lr) * NP + part * 16;
         const uint8_t *gB = codes + (size_t)(b0 + lr) * NP + part * 16;
 
-        // REF: stages [0, 8 cs) are the eight lane classes, the stage after them the tail
-        const uint32_t class_end = 8 * ref_cs;
-        uint32_t left = 0;  // default: stages until the next flush of acc into tot
-        uint32_t st = 0;
-        for (uint32_t k0 = 0; k0 < NP; k0 += 64, ++st) {
+        // one 64-sequence stage of both panels' codes and the weights into LDS
+        auto load_stage = [&](uint32_t k0) {
             const uint4 va = *reinterpret_cast<const uint4 *>(gA + k0);
             const uint4 vb = *reinterpret_cast<const uint4 *>(gB + k0);
             const float wv = tid < 64 ? w[k0 + tid] : 0.0f;
@@ -109,23 +109,9 @@ __global__ __launch_bounds__(256, MF ? WLD_VALU_MF_WG : 2) void pair_valu_kernel
             pb[0] = vb.x; pb[1] = vb.y; pb[2] = vb.z; pb[3] = vb.w;
             if (tid < 64) sW[tid] = wv;
             __syncthreads();
-            const bool tail = REF && st >= class_end;
-            const bool blk_start = REF ? (tail || (ref_cs && st % ref_cs == 0)) : left == 0;
-            if (blk_start) {
-                left = flush;
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            // the tail continues the chain on the horizontal sums
-                            const float v = tail ? tot[i][j][q] : 0.0f;
-                            acc[i][j][q] = v;
-                            accM[j][q][i] = v;
-                        }
-            }
-
+        };
+        // the staged 64 sequences into acc (VALU) / accM (MF), in sequence order
+        auto compute_stage = [&]() {
             if constexpr (MF) {
                 const uint32_t lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
                 const uint8_t *rowA = sA + (16 * wave + r) * kStride + g;
@@ -202,18 +188,81 @@ __global__ __launch_bounds__(256, MF ? WLD_VALU_MF_WG : 2) void pair_valu_kernel
                     }
                 }
             }
-            const bool blk_end = REF ? (tail || (ref_cs && st % ref_cs == ref_cs - 1)) : (--left == 0 || k0 + 64 >= NP);
-            if (blk_end) {
-                left = 0;
+        };
+        // block start: acc = 0; block end: tot += acc
+        auto acc_zero = [&]() {
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < 4; ++j)
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const float v = MF ? accM[j][q][i] : acc[i][j][q];
-                            tot[i][j][q] = tail ? v : tot[i][j][q] + v;
+                    for (int q = 0; q < 4; ++q) {
+                        if constexpr (MF) accM[j][q][i] = 0.0f;
+                        else acc[i][j][q] = 0.0f;
+                    }
+        };
+        auto acc_fold = [&]() {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) tot[i][j][q] += MF ? accM[j][q][i] : acc[i][j][q];
+        };
+
+        if constexpr (REF) {
+            // the eight lane classes, each a chain from 0 folded into the
+            // ordered horizontal sum; then the tail stage on that sum
+            const uint32_t cls = 64 * ref_cs;
+            for (uint32_t c = 0; c < (ref_cs ? 8u : 0u); ++c) {
+                acc_zero();
+                for (uint32_t k0 = c * cls; k0 < (c + 1) * cls; k0 += 64) {
+                    load_stage(k0);
+                    compute_stage();
+                }
+                acc_fold();
+            }
+            if (ref_tail_n) {
+                // the scalar tail (lib.rs:461-480): its <= 7 sequences added
+                // onto the horizontal sums one by one, in order, on the VALU
+                // (fmaf(u, f, tot) = tot + u f rounded once: u f is exact)
+                load_stage(8 * cls);
+                for (uint32_t t = 0; t < ref_tail_n; ++t) {
+                    const float we = sW[t];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t ca = sA[arow(i) * kStride + t];
+                        const float u = (ca & kCodeIn) ? we : 0.0f;
+                        const float v = (ca & kCodeMaj) ? we : 0.0f;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const uint32_t cb = sB[(MF ? 16 * j + (tid & 15) : tx + 16 * j) * kStride + t];
+                            if constexpr (!SAFE) {
+                                const float fi = (float)(cb & 1u), fm = (float)(cb >> 1);
+                                tot[i][j][0] = __builtin_fmaf(u, fi, tot[i][j][0]);
+                                tot[i][j][1] = __builtin_fmaf(v, fi, tot[i][j][1]);
+                                tot[i][j][2] = __builtin_fmaf(u, fm, tot[i][j][2]);
+                                tot[i][j][3] = __builtin_fmaf(v, fm, tot[i][j][3]);
+                            } else {
+                                const bool bi = cb & 1u, bm = cb & 2u;
+                                tot[i][j][0] += bi ? u : 0.0f;
+                                tot[i][j][1] += bi ? v : 0.0f;
+                                tot[i][j][2] += bm ? u : 0.0f;
+                                tot[i][j][3] += bm ? v : 0.0f;
+                            }
                         }
+                    }
+                }
+            }
+        } else {
+            // blocks of `flush` stages
+            for (uint32_t k0 = 0; k0 < NP; k0 += 64 * flush) {
+                acc_zero();
+                for (uint32_t k1 = k0; k1 < min(NP, k0 + 64 * flush); k1 += 64) {
+                    load_stage(k1);
+                    compute_stage();
+                }
+                acc_fold();
             }
         }
 
@@ -361,7 +410,7 @@ template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
 void launch_v(const ValuLaunch &v, uint32_t grid, uint32_t flush, uint32_t cs, const OrderArgs &o,
               const DenseArgs &dn, hipStream_t s) {
     hipLaunchKernelGGL((pair_valu_kernel<DENSE, SAFE, MF, REF, LOOP>), dim3(grid), dim3(256), 0, s, v.codes, v.w,
-                       v.site_ok, v.tiles, v.tile_count, v.L, v.NP, flush, cs, v.n_chunk_rows, v.thr, o,
+                       v.site_ok, v.tiles, v.tile_count, v.L, v.NP, flush, cs, v.ref_tail_n, v.n_chunk_rows, v.thr, o,
                        dn);
 }
 }  // namespace
