@@ -363,8 +363,9 @@ void rows_to_linear(uint32_t n, uint32_t rb, uint32_t re, uint32_t &lb, uint32_t
 // XCDs round-robin by launch index, so position 8i + x is XCD x's i-th tile.
 // Each XCD gets whole 8x8-tile super-blocks (greedy, least-loaded first), so
 // the ~64 tiles resident on its 32 CUs read 8 A and 8 B tile columns (2 MB at
-// C4) that fit its 4 MB L2.  Short queues are padded with kNoTile entries,
-// which the pair kernels skip.
+// C4) that fit its 4 MB L2; then the queues are evened out to within one
+// tile.  Short queues are padded with kNoTile entries, which the pair kernels
+// skip.
 std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t) {
     constexpr uint32_t kX = 8, kS = 8;
     std::vector<std::vector<uint32_t>> blocks;
@@ -386,6 +387,20 @@ std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t) {
         for (size_t k = 1; k < kX; ++k)
             if (q[k].size() < q[x].size()) x = k;
         q[x].insert(q[x].end(), b.begin(), b.end());
+    }
+    // Even out the queues to within one tile: the kernel runs in rounds of
+    // (resident workgroups per XCD) and a queue a few tiles longer than the
+    // others costs a whole extra round (rank 0's 1/8 shard of C4: 7 rounds
+    // instead of 6).  Tail tiles move from the longest queue to the shortest.
+    for (;;) {
+        size_t lo = 0, hi = 0;
+        for (size_t k = 1; k < kX; ++k) {
+            if (q[k].size() < q[lo].size()) lo = k;
+            if (q[k].size() > q[hi].size()) hi = k;
+        }
+        if (q[hi].size() <= q[lo].size() + 1) break;
+        q[lo].push_back(q[hi].back());
+        q[hi].pop_back();
     }
     size_t len = 0;
     for (auto &v : q) len = std::max(len, v.size());

@@ -104,6 +104,10 @@ int mfma_weight_stats(const int8_t *wplanes, size_t LP, size_t NP, hipStream_t s
 // workgroups of the candidate launch after a screen (it strides over a tile
 // list whose length is known only on the device): 4 rounds of 2 per CU
 constexpr uint32_t kCandidateGrid = 2048;
+// ... and of the reference-order f32 kernel's candidate loop: its resident
+// workgroups (three per CU, 256 CUs); extra workgroups would only queue (and
+// cost dispatch time when there is no candidate at all)
+constexpr uint32_t kRefCandidateGrid = 768;
 
 struct MfmaLaunch {
     const uint8_t *codes;   // site-major codes (used when frag is null)

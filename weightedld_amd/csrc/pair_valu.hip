@@ -418,7 +418,8 @@ void launch_v(const ValuLaunch &v, uint32_t grid, uint32_t flush, uint32_t cs, c
 void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
     const DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
     const uint32_t flush = (uint32_t)std::max(1.0, std::floor(std::sqrt((double)v.NP) / 64.0 + 0.5));
-    const uint32_t grid = v.tile_count ? std::min<uint32_t>(v.n_tiles, kCandidateGrid) : v.n_tiles;
+    const uint32_t grid = v.tile_count ? std::min<uint32_t>(v.n_tiles, v.ref ? kRefCandidateGrid : kCandidateGrid)
+                                       : v.n_tiles;
     if (grid == 0) return;
     if (v.ref) {
         // the reference's f32 order: f32-input MFMA for finite weights, the
