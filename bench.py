@@ -402,7 +402,7 @@ def main():
     elapsed = time.perf_counter() - t0
     # per-launch HIP-event times of the same steps, sampled after the timed
     # region so that reading them adds nothing to it
-    kms, oms, sms, cand = [], [], [], []
+    kms, oms, sms, cand, cblk = [], [], [], [], []
     for _ in range(min(args.steps, 20)):
         tg = time.perf_counter()
         step()
@@ -411,6 +411,7 @@ def main():
         oms.append(st["order_ms"])
         sms.append(st["screen_ms"])
         cand.append(st["candidate_tiles"])
+        cblk.append(st["candidate_blocks"])
         gms.append((time.perf_counter() - tg) * 1e3 - st["pair_kernel_ms"])
     screen_kind = ctx.stats()["screened"]  # 0 none, 1 i8 one-plane screen, 3 two-plane screen
     screened = bool(screen_kind)
@@ -505,6 +506,11 @@ def main():
                                                "pair_mfma_kernel<prefilter, %d planes>" % planes),
                           "candidate_frac": (cand_ops / (cand_ms * 1e-3) / 1e12 / cand_peak) if cand_ms > 0.02 else None,
                           "candidate_peak": cand_peak,
+                          # --ref-sums computes only the candidate tiles' 16x16
+                          # sub-blocks holding a pair the screen could not reject
+                          "candidate_blocks": float(np.mean(cblk)),
+                          "candidate_computed_frac": ((float(np.mean(cblk)) * 256 * 8.0 * N) / (cand_ms * 1e-3) / 1e12
+                                                      / cand_peak) if cand_ms > 0.02 and args.ref_sums else None,
                           "unscreened_pair_kernel_ms": unscreened_ms,
                           "unscreened_frac": alg_ops / (unscreened_ms * 1e-3) / 1e12 / roof["peak"]}
     # PMC traffic (profiles/traffic.json) was measured on the default C4 line's

@@ -373,6 +373,9 @@ typedef struct {
     int screened;            /* 1: the last run ran the one-plane i8 screen; 3: the two-plane
                                 i8 screen; 0: none */
     int ref_sums;            /* 1: the last run summed in lib.rs's f32 order (WLD_OPT_REF_SUMS) */
+    uint64_t candidate_blocks; /* 16x16 sub-blocks of the candidate tiles holding a pair the screen
+                                  could not reject (16 x candidate_tiles unless screened); with
+                                  WLD_OPT_REF_SUMS only these are computed */
 } wld_run_stats;
 int wld_last_stats(wld_ctx *ctx, wld_run_stats *out);
 

@@ -60,6 +60,7 @@ class RunStats(ctypes.Structure):
         ("screen_ms", ctypes.c_double),
         ("screened", ctypes.c_int),
         ("ref_sums", ctypes.c_int),
+        ("candidate_blocks", ctypes.c_uint64),
     ]
 
 

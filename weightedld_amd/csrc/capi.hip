@@ -100,7 +100,7 @@ struct wld_ctx {
     hipEvent_t ev[7] = {};  // 2..3 pair phase (6: after the screen), 3..4/5 order phase
     RunPending pend;                      // the run between run_enqueue and run_complete
     bool run_dirty = true;                // run state (cursor, chunk totals) may be nonzero: re-initialise
-    unsigned long long *h_cnt = nullptr;  // mapped pinned {cursor, rows} written by chunk_scan_kernel
+    unsigned long long *h_cnt = nullptr;  // mapped pinned {cursor, rows, candidate tiles, sub-blocks} (the scan)
     unsigned long long *d_hcnt = nullptr;
     int kernel_pref = WLD_KERNEL_AUTO;
     // wld_set_option (include/weightedld.h)
@@ -431,7 +431,7 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
     if (!c->opt_tile_rows && t.size() >= 4096 && T_used < 65535) t = xcd_order(t);
     c->n_tiles = (uint32_t)t.size();
     WLD_TRY(ensure(c->tiles, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));
-    WLD_TRY(ensure(c->cand, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));  // screen candidates
+    WLD_TRY(ensure(c->cand, std::max<size_t>(t.size(), 1) * 2 * sizeof(uint32_t)));  // screen candidates + bits
     if (!t.empty())
         HIP_TRY(hipMemcpyAsync(c->tiles.p, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -495,7 +495,10 @@ double ref_extra_residual(const wld_ctx *c) {
 
 // Enqueues the pair kernel(s) of a pass; *screened tells whether the MFMA
 // screen ran (then ev[6] separates it from the candidate launch).
-int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *dense, bool *screened = nullptr) {
+// With scan given, a screen fuses the run's chunk scan into its last
+// workgroup or the candidate launch's (then the caller launches no scan).
+int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *dense, bool *screened = nullptr,
+                 const ScanArgs *scan = nullptr) {
     const uint32_t n = chunk_rows_of(c->L);
     bool sc = false;
     c->stats.ref_sums = c->opt_ref_sums ? 1 : 0;
@@ -547,6 +550,7 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
         m.cand_list = ptr<uint32_t>(c->cand);
         m.cand_count = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 2);
+        if (scan && !dense) m.scan = *scan;
         if (ref_screen) {
             m.ref_valu = &rv;
             m.r_extra_q = ref_extra_residual(c);
@@ -929,19 +933,20 @@ int enqueue_pass(wld_ctx *c) {
     }
     c->run_dirty = true;  // until run_complete has seen this pass's scan
     const OrderArgs o = order_args(c);
+    unsigned long long *cn = ptr<unsigned long long>(c->counters);  // {cursor, total, cand_count, ticket}
+    ScanArgs sa{ptr<uint32_t>(c->chunk_total), r.lin_begin, lin_count, ptr<uint32_t>(c->chunk_base), cn + 1, cn,
+                c->d_hcnt, r.count_out, reinterpret_cast<unsigned *>(cn + 2), reinterpret_cast<unsigned *>(cn + 3)};
+    c->h_cnt[0] = c->h_cnt[1] = lin_count ? ~0ull : 0ull;
+    c->h_cnt[2] = c->h_cnt[3] = 0;
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     c->screened = c->screened2 = false;
-    if (c->n_tiles) WLD_TRY(launch_pairs(c, r.thr, o, nullptr, &c->screened));
+    if (c->n_tiles) WLD_TRY(launch_pairs(c, r.thr, o, nullptr, &c->screened, lin_count ? &sa : nullptr));
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-    c->h_cnt[0] = c->h_cnt[1] = lin_count ? ~0ull : 0ull;
-    c->h_cnt[2] = 0;
-    if (lin_count) {
-        launch_chunk_scan(ptr<uint32_t>(c->chunk_total), r.lin_begin, lin_count, ptr<uint32_t>(c->chunk_base),
-                          ptr<unsigned long long>(c->counters) + 1, ptr<unsigned long long>(c->counters), c->d_hcnt,
-                          r.count_out, reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 2),
-                          c->stream);
+    if (lin_count && !c->screened) {  // after a screen the candidate launch's last workgroup ran it
+        sa.ticket = nullptr;
+        launch_chunk_scan(sa, c->stream);
         HIP_TRY(hipGetLastError());
-    } else if (r.count_out) {
+    } else if (!lin_count && r.count_out) {
         HIP_TRY(hipMemsetAsync(r.count_out, 0, sizeof(unsigned long long), c->stream));
     }
     HIP_TRY(hipEventRecord(c->ev[4], c->stream));
@@ -1032,7 +1037,7 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     const RunPending r = c->pend;
     const uint32_t n = chunk_rows_of(c->L);
     const uint32_t lin_count = r.lin_end - r.lin_begin;
-    unsigned long long h[3] = {0, 0, 0};
+    unsigned long long h[4] = {0, 0, 0, 0};
     for (int attempt = 0; attempt < 2; ++attempt) {
         if (c->prog_pass) {
             c->prog_pass = false;  // a re-run after a staging overflow does not report again
@@ -1043,6 +1048,7 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
         h[0] = __atomic_load_n(&c->h_cnt[0], __ATOMIC_ACQUIRE);
         h[1] = __atomic_load_n(&c->h_cnt[1], __ATOMIC_ACQUIRE);
         h[2] = __atomic_load_n(&c->h_cnt[2], __ATOMIC_ACQUIRE);
+        h[3] = __atomic_load_n(&c->h_cnt[3], __ATOMIC_ACQUIRE);
         if (h[0] <= c->st_capacity) break;
         if (attempt == 1) return fail(WLD_E_HIP, "internal: staging overflow after resize");
         WLD_TRY(grow_staging(c, h[0]));
@@ -1087,6 +1093,7 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     if (c->screened && c->screened2 && h[2] * 5 > c->n_tiles) c->screen2_bad_thr = std::max(c->screen2_bad_thr, r.thr);
     c->stats.screen_ms = c->screened ? event_ms(c->ev[2], c->ev[6]) : 0.0;
     c->stats.candidate_tiles = c->screened ? h[2] : c->n_tiles;
+    c->stats.candidate_blocks = c->screened ? h[3] : 16 * (uint64_t)c->n_tiles;
     if (n_rows) *n_rows = rows;
     return WLD_OK;
 }

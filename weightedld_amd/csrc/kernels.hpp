@@ -42,6 +42,24 @@ struct OrderArgs {
     uint32_t L;  // sites of the loaded set (a chunk's pair count)
 };
 
+// The run's chunk scan (order.hip): exclusive scan of the chunk totals
+// [lin_begin, lin_begin + count) into chunk_base; the row total into *total,
+// *count_out (may be null) and host_out[1], the staging cursor into
+// host_out[0], the candidate-tile count cand_count[0] into host_out[2] and
+// their computed 16x16 sub-blocks cand_count[1] into host_out[3] (host_out:
+// mapped pinned memory, may be null); cursor, the chunk totals and both
+// candidate counts are left at 0 for the next run.  With ticket set, the last
+// workgroup of the candidate launch after a screen runs it (scan_tail,
+// pair_common.hpp) instead of a launch of its own.
+struct ScanArgs {
+    uint32_t *chunk_total;
+    uint32_t lin_begin, count;
+    uint32_t *chunk_base;
+    unsigned long long *total, *cursor, *host_out, *count_out;
+    unsigned *cand_count;  // {candidate tiles, their candidate sub-blocks}
+    unsigned *ticket;  // 0 between launches; null: the scan is launched on its own
+};
+
 struct DenseArgs {
     float *d, *dp, *r2;
     uint8_t *valid;
@@ -76,6 +94,11 @@ struct ValuLaunch {
     bool ref;    // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order
     uint32_t ref_cls;  // REF: sequence positions per lane class (multiple of 64, 0 when N < 8)
     uint32_t ref_tail_n;  // REF: the scalar tail's sequences (N mod 8), in the stage after the classes
+    // tile_count launches: per list entry, the 16x16 sub-blocks (bit 4 (a/16)
+    // + b/16) whose pairs are computed; the others' pairs provably fail (the
+    // screen's per-pair bound) and are skipped.  Null: every sub-block.
+    const uint32_t *tile_bits;
+    ScanArgs scan;        // tile_count launches: the run's scan fused into the last workgroup (ticket set)
 };
 void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
 // the lane-class layout of REF: cls positions per class, the tail stage, NPr
@@ -125,7 +148,7 @@ struct MfmaLaunch {
     bool screen2;    // the screen on the top two digit planes (>= 3 active planes)
     uint64_t resid[3];
     uint64_t dsum[4];
-    uint32_t *cand_list;   // n_tiles entries
+    uint32_t *cand_list;   // 2 n_tiles entries: the candidate tiles, then their sub-block bits
     unsigned *cand_count;  // 0 before the launch (chunk_scan_kernel resets it)
     // WLD_OPT_REF_SUMS: the candidate tiles go to the reference-order f32
     // kernel (ref_valu, tiles/tile_count filled in here) and the screen's
@@ -133,6 +156,9 @@ struct MfmaLaunch {
     // reference's f32 sums can lie from the fixed-point sums, 2x2-cell L1)
     const ValuLaunch *ref_valu;
     double r_extra_q;
+    // with a screen: the run's scan, fused into the screen's or the candidate
+    // launch's last workgroup when scan.ticket is set
+    ScanArgs scan;
 };
 // Enqueues the MFMA pair kernel(s) of one pass; returns true when a screen
 // (one- or two-plane) ran (then screen_done, if given, is recorded between
@@ -147,12 +173,8 @@ void launch_progress_init(unsigned *chunk_left, uint32_t lin_begin, uint32_t cou
                           unsigned *prog_n, hipStream_t s);
 // zeroes the run state (staging cursor, row total, every chunk total)
 void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t n_chunks, hipStream_t s);
-// count_out (device, may be null): also receives the run's row total
-// host_out[2] receives the screen's candidate-tile count (cand_count, which
-// the scan resets to 0; may be null)
-void launch_chunk_scan(uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
-                       unsigned long long *total, unsigned long long *cursor, unsigned long long *host_out,
-                       unsigned long long *count_out, unsigned *cand_count, hipStream_t s);
+// the run's chunk scan as a launch of its own (ScanArgs; ticket unused)
+void launch_chunk_scan(const ScanArgs &a, hipStream_t s);
 void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,
                    uint32_t n_chunk_rows, uint32_t L, const uint32_t *site_map, uint32_t *out_a, uint32_t *out_b,
                    float *out_d, float *out_dp, float *out_r2, hipStream_t s);

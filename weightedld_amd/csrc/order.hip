@@ -25,65 +25,13 @@ __global__ __launch_bounds__(256) void run_init_kernel(unsigned long long *__res
     for (uint32_t i = i0; i < n_chunks; i += stride) chunk_total[i] = 0;
 }
 
-// host_out (mapped pinned host memory) receives {staging cursor, row total}:
-// the run's only device-to-host transfer, without a copy command.  The scan
-// also leaves the run state clean for the next run (the staging cursor and
-// the range's chunk totals back to 0), so a run needs no initialising kernel.
-__global__ __launch_bounds__(1024) void chunk_scan_kernel(uint32_t *__restrict__ chunk_total, uint32_t lin_begin,
-                                                           uint32_t count, uint32_t *__restrict__ chunk_base,
-                                                           unsigned long long *__restrict__ total,
-                                                           unsigned long long *__restrict__ cursor,
-                                                           unsigned long long *host_out,
-                                                           unsigned long long *__restrict__ count_out,
-                                                           unsigned *__restrict__ cand_count) {
-    __shared__ unsigned long long sw[16];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t per = (count + 1023) / 1024;
-    const uint32_t lo = min(count, tid * per), hi = min(count, lo + per);
-    unsigned long long s = 0;
-    for (uint32_t i = lo; i < hi; ++i) s += chunk_total[lin_begin + i];
-    // block exclusive scan of s (64-bit)
-    const int lane = tid & 63, wv = tid >> 6;
-    unsigned long long v = s;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        unsigned long long t = __shfl_up(v, off, 64);
-        if (lane >= off) v += t;
-    }
-    if (lane == 63) sw[wv] = v;
-    __syncthreads();
-    if (tid == 0) {
-        unsigned long long run = 0;
-        for (int k = 0; k < 16; ++k) {
-            unsigned long long t = sw[k];
-            sw[k] = run;
-            run += t;
-        }
-        *total = run;
-        if (count_out) *count_out = run;  // e.g. the caller's tensor for the RCCL count exchange
-        const unsigned long long cur = *cursor;
-        *cursor = 0;
-        unsigned cand = 0;
-        if (cand_count) {
-            cand = *cand_count;
-            *cand_count = 0;
-        }
-        if (host_out) {
-            host_out[0] = cur;
-            host_out[1] = run;
-            host_out[2] = cand;
-            __threadfence_system();
-        }
-    }
-    __syncthreads();
-    unsigned long long base = sw[wv] + v - s;
-    for (uint32_t i = lo; i < hi; ++i) {
-        const uint32_t t = chunk_total[lin_begin + i];
-        chunk_total[lin_begin + i] = 0;
-        chunk_base[i] = (uint32_t)base;
-        base += t;
-    }
-}
+// host_out (mapped pinned host memory) receives {staging cursor, row total,
+// candidate tiles}: the run's only device-to-host transfer, without a copy
+// command.  The scan also leaves the run state clean for the next run (the
+// staging cursor and the range's chunk totals back to 0), so a run needs no
+// initialising kernel.  After a screen it runs in the screen's or the
+// candidate launch's last workgroup instead (scan_tail).
+__global__ __launch_bounds__(1024) void chunk_scan_kernel(ScanArgs a) { chunk_scan_block(a); }
 
 // inverse of chunk_linear: exact integer version of triu_index (lib.rs:623-632)
 __device__ inline void chunk_of_linear(uint32_t n, uint32_t i, uint32_t &row, uint32_t &col) {
@@ -185,11 +133,8 @@ void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32
     hipLaunchKernelGGL(run_init_kernel, dim3(blocks), dim3(256), 0, s, counters, chunk_total, n_chunks);
 }
 
-void launch_chunk_scan(uint32_t *chunk_total, uint32_t lin_begin, uint32_t count, uint32_t *chunk_base,
-                       unsigned long long *total, unsigned long long *cursor, unsigned long long *host_out,
-                       unsigned long long *count_out, unsigned *cand_count, hipStream_t s) {
-    hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(1024), 0, s, chunk_total, lin_begin, count, chunk_base, total,
-                       cursor, host_out, count_out, cand_count);
+void launch_chunk_scan(const ScanArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(chunk_scan_kernel, dim3(1), dim3(1024), 0, s, a);
 }
 
 void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,

@@ -207,4 +207,89 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
     return v;
 }
 
+// The run's chunk scan (ScanArgs) by one workgroup of any size that is a
+// multiple of 64, up to 1024: each thread sums a contiguous run of chunk
+// totals, a wave scan and a scan of the wave totals give its base.  The
+// counters and totals it reads were last written by other workgroups'
+// agent-scope atomics in this launch (scan_tail): every load of them is an
+// agent-scope (sc1) load, served past this CU's L1.
+__device__ inline void chunk_scan_block(const ScanArgs &a) {
+    __shared__ unsigned long long sw[16];
+    auto ld32 = [](const unsigned *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    const uint32_t tid = threadIdx.x, nth = blockDim.x;
+    const uint32_t per = (a.count + nth - 1) / nth;
+    const uint32_t lo = min(a.count, tid * per), hi = min(a.count, lo + per);
+    uint32_t *ct = a.chunk_total + a.lin_begin;
+    unsigned long long s = 0;
+    for (uint32_t i = lo; i < hi; ++i) s += ld32(ct + i);
+    const int lane = tid & 63, wv = tid >> 6;
+    unsigned long long v = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned long long t = __shfl_up(v, off, 64);
+        if (lane >= off) v += t;
+    }
+    if (lane == 63) sw[wv] = v;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long run = 0;
+        for (uint32_t k = 0; k < nth / 64; ++k) {
+            const unsigned long long t = sw[k];
+            sw[k] = run;
+            run += t;
+        }
+        *a.total = run;
+        if (a.count_out) *a.count_out = run;  // e.g. the caller's tensor for the RCCL count exchange
+        const unsigned long long cur = __hip_atomic_load(a.cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *a.cursor = 0;
+        unsigned cand = 0, blocks = 0;
+        if (a.cand_count) {
+            cand = ld32(a.cand_count);
+            blocks = ld32(a.cand_count + 1);
+            a.cand_count[0] = a.cand_count[1] = 0;
+        }
+        if (a.host_out) {
+            a.host_out[0] = cur;
+            a.host_out[1] = run;
+            a.host_out[2] = cand;
+            a.host_out[3] = blocks;
+            __threadfence_system();
+        }
+    }
+    __syncthreads();
+    unsigned long long base = sw[wv] + v - s;
+    for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t t = ld32(ct + i);
+        ct[i] = 0;
+        a.chunk_base[i] = (uint32_t)base;
+        base += t;
+    }
+}
+
+// The end of every workgroup of a candidate launch (a grid-stride loop over
+// the screen's n_work candidate tiles).  With the scan fused (a.ticket set)
+// the workgroups that computed a tile take a ticket and the last one runs the
+// run's chunk scan (with no candidate, workgroup 0 alone): one launch (and
+// its dispatch gap) less per run, and no ticket traffic in the common case.
+// What the scan reads from this launch — the chunk totals and the staging
+// cursor — only wave 0 writes (lane 63's atomics in the compaction), so wave
+// 0 waits for its memory operations before lane 0 takes the ticket, and the
+// last workgroup reads them with agent-scope loads (MI355X_MICROARCH.md,
+// inter-workgroup visibility: one lane per workgroup adding to one counter,
+// the last adder told by the returned value; no per-workgroup L2 write-back).
+// The screen before the launch only appended candidates (atomics, before the
+// kernel boundary).
+__device__ inline void scan_tail(const ScanArgs &a, uint32_t n_work) {
+    if (!a.ticket) return;
+    const uint32_t p = min(gridDim.x, n_work);  // workgroups that computed a tile
+    if (blockIdx.x >= max(p, 1u)) return;
+    __shared__ unsigned s_run;
+    if (threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's atomics performed
+    if (threadIdx.x == 0) s_run = p <= 1 || atomicAdd(a.ticket, 1u) == p - 1;
+    __syncthreads();
+    if (!s_run) return;
+    if (threadIdx.x == 0 && p > 1) atomicExch(a.ticket, 0u);
+    chunk_scan_block(a);
+}
+
 }  // namespace wld

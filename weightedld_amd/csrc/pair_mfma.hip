@@ -218,6 +218,11 @@ struct Acc32 {
         return 32 * (wave & 1) + (lane & 31);
     }
 };
+// 16x16 sub-block (a_local / 16, b_local / 16) of pair i as a bit index 0..15
+template <class Acc>
+__device__ __forceinline__ uint32_t sub_block(int i, uint32_t wave, uint32_t lane) {
+    return 4 * (Acc::a_local(i, wave, lane) >> 4) + (Acc::b_local(i, wave, lane) >> 4);
+}
 // 16x16x64 shape, wave w owns a rows 16(w & 3)..+15 against NB 16x16 blocks
 // of b columns starting at block NB (w >> 2) (all 64 columns when NB = 4 with
 // four waves; 32 when NB = 2 with eight) (C/D col = lane & 15, row =
@@ -373,6 +378,8 @@ struct ScreenArgs {
     int nonneg;             // all weights >= 0 (exact 2x2 cells are >= 0)
     uint32_t *cand_list;    // kModeScreen: candidate tiles (packed ta << 16 | tb)
     unsigned *cand_count;   // kModeScreen: appended to; candidate launch: tile count
+    uint32_t *cand_bits;    // kModeScreen: per list entry, its 16x16 sub-blocks holding a candidate pair
+    ScanArgs scan;          // screen and candidate launches: the fused chunk scan (scan_tail)
 };
 
 // Reference epilogue of one pair from its exact sums (fixed-point units):
@@ -412,69 +419,70 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
     if constexpr (MODE == kModeScreen) {
         // sums in units of the screened digit plane, within R of the exact
         // sums scaled to that unit (cells: sum_c |e_c| <= R)
-        bool cand = false;
         // the f32 tests need one plane's sums (<= 128 NP); two planes
         // (Acc::kPlanes == 2, the low-threshold screen) always take r2_bound_skip
-        if (Acc::kPlanes == 1 && sc.f32 == 2) {
-            // doubled sums straight from the X/Y accumulators (raw(x, i) =
-            // {2T, 2SB} / {2SA, 2SAB}: exact integers <= 256 NP <= 2^22), the
-            // f32 bound as a violation margin, branch-free; every pair valid
-            // unless the tile touches the diagonal or a filtered/padding site
-            // E and 2^-12 Tb fixed per launch from Tg = 2 sum |top digits| >= every
-            // doubled T (screen_consts); the terms straight from X/Y
-            // (r2_screen_terms_xy); each term's f32 bits as an int: the maximum
-            // is > 0 iff some term is > 0 (finite terms: integer sums <= 2^22)
-            const float thr_c = thr * (1.0f - 0x1p-7f), R2 = 2.0f * sc.Rf;
+        const bool f32x2 = Acc::kPlanes == 1 && sc.f32 == 2, f32x1 = Acc::kPlanes == 1 && sc.f32 == 1;
+        const float thr_c = thr * (1.0f - 0x1p-7f), R2 = 2.0f * sc.Rf;
+        // f32x2: the f32 bound as a violation margin, branch-free, from the
+        // doubled sums straight from the X/Y accumulators (raw(x, i) = {2T,
+        // 2SB} / {2SA, 2SAB}: exact integers <= 256 NP <= 2^22); E and 2^-12
+        // Tb fixed per launch from Tg = 2 sum |top digits| >= every doubled T
+        // (screen_consts); the terms straight from X/Y (r2_screen_terms_xy);
+        // each term's f32 bits as an int: the maximum is > 0 iff some term is
+        // > 0 (finite terms: integer sums <= 2^22)
+        auto margin = [&](int i) {
+            const int2 p0 = acc.raw(0, i), p1 = acc.raw(1, i);  // (X, Y) of channel_a in, major
+            float t2;
+            const float t1 = r2_screen_terms_xy((float)p0.x, (float)p0.y, (float)p1.x, (float)p1.y, R2, thr_c, sc.E,
+                                                sc.mloc, t2);
+            return max(__float_as_int(t1), __float_as_int(t2));
+        };
+        auto valid_pair = [&](int i) {
+            const uint32_t a_local = Acc::a_local(i, wave, lane), b_local = Acc::b_local(i, wave, lane);
+            return ((okB >> b_local) & 1) && a0 + a_local < b0 + b_local && ((okA >> a_local) & 1);
+        };
+        // pair i may pass (valid, and the bound does not reject it)
+        auto pair_cand = [&](int i) -> bool {
+            if (!valid_pair(i)) return false;
+            if (f32x2) return margin(i) > 0;
+            // the f32 test decides almost every pair; the f64 one the rest
+            if (f32x1 && r2_screen_skip_f32((float)sum(0, 0, i), (float)sum(1, 0, i), (float)sum(0, 1, i),
+                                            (float)sum(1, 1, i), sc.Rf, thr))
+                return false;
+            return !r2_bound_skip(sum(0, 0, i), sum(1, 0, i), sum(0, 1, i), sum(1, 1, i), sc.R, thr,
+                                  f32x1 || sc.nonneg != 0);
+        };
+        bool cand = false;
+        if (f32x2 && okA == ~0ull && okB == ~0ull && ta != tb) {
+            // every pair valid (the tile touches neither the diagonal nor a
+            // filtered/padding site)
             int worst = -1;
-            const bool full = okA == ~0ull && okB == ~0ull && ta != tb;
-            if (full) {
 #pragma unroll
-                for (int i = 0; i < Acc::kPairs; ++i) {
-                    const int2 p0 = acc.raw(0, i), p1 = acc.raw(1, i);  // (X, Y) of channel_a in, major
-                    float t2;
-                    const float t1 = r2_screen_terms_xy((float)p0.x, (float)p0.y, (float)p1.x, (float)p1.y, R2, thr_c,
-                                                        sc.E, sc.mloc, t2);
-                    worst = max(worst, max(__float_as_int(t1), __float_as_int(t2)));
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < Acc::kPairs; ++i) {
-                    const int2 p0 = acc.raw(0, i), p1 = acc.raw(1, i);
-                    float t2;
-                    const float t1 = r2_screen_terms_xy((float)p0.x, (float)p0.y, (float)p1.x, (float)p1.y, R2, thr_c,
-                                                        sc.E, sc.mloc, t2);
-                    const uint32_t a_local = Acc::a_local(i, wave, lane);
-                    const uint32_t b_local = Acc::b_local(i, wave, lane);
-                    const bool valid =
-                        ((okB >> b_local) & 1) && a0 + a_local < b0 + b_local && ((okA >> a_local) & 1);
-                    if (valid) worst = max(worst, max(__float_as_int(t1), __float_as_int(t2)));
-                }
-            }
+            for (int i = 0; i < Acc::kPairs; ++i) worst = max(worst, margin(i));
             cand = worst > 0;
-        } else if (Acc::kPlanes == 1 && sc.f32) {
-#pragma unroll
-            for (int i = 0; i < Acc::kPairs; ++i) {
-                const uint32_t a_local = Acc::a_local(i, wave, lane);
-                const uint32_t b_local = Acc::b_local(i, wave, lane);
-                const bool valid = ((okB >> b_local) & 1) && a0 + a_local < b0 + b_local && ((okA >> a_local) & 1);
-                // the f32 test decides almost every pair; the f64 one the rest
-                if (valid && !r2_screen_skip_f32((float)sum(0, 0, i), (float)sum(1, 0, i), (float)sum(0, 1, i),
-                                                 (float)sum(1, 1, i), sc.Rf, thr))
-                    cand |= !r2_bound_skip(sum(0, 0, i), sum(1, 0, i), sum(0, 1, i), sum(1, 1, i), sc.R, thr, true);
-            }
         } else {
 #pragma unroll
-            for (int i = 0; i < Acc::kPairs; ++i) {
-                const uint32_t a_local = Acc::a_local(i, wave, lane);
-                const uint32_t b_local = Acc::b_local(i, wave, lane);
-                const bool valid = ((okB >> b_local) & 1) && a0 + a_local < b0 + b_local && ((okA >> a_local) & 1);
-                if (valid && !cand)
-                    cand = !r2_bound_skip(sum(0, 0, i), sum(1, 0, i), sum(0, 1, i), sum(1, 1, i), sc.R, thr,
-                                          sc.nonneg != 0);
-            }
+            for (int i = 0; i < Acc::kPairs; ++i)
+                if (!cand) cand = pair_cand(i);
         }
+        unsigned long long *sMask = sBits;  // (no compaction in this mode)
+        if (tid == 0) *sMask = 0ull;
         if (__syncthreads_or(cand)) {
-            if (tid == 0) sc.cand_list[atomicAdd(sc.cand_count, 1u)] = (ta << 16) | tb;
+            // which 16x16 sub-blocks hold a pair that may pass: the candidate
+            // launch computes only those (the others' pairs provably fail)
+            unsigned m = 0;
+#pragma unroll
+            for (int i = 0; i < Acc::kPairs; ++i)
+                if (pair_cand(i)) m |= 1u << sub_block<Acc>(i, wave, lane);
+            if (m) atomicOr(sMask, (unsigned long long)m);
+            __syncthreads();
+            if (tid == 0) {
+                const uint32_t bits = (uint32_t)*sMask;
+                const unsigned k = atomicAdd(sc.cand_count, 1u);
+                atomicAdd(sc.cand_count + 1, (unsigned)__popc(bits));  // sub-blocks to compute (stats)
+                sc.cand_list[k] = (ta << 16) | tb;
+                sc.cand_bits[k] = bits;
+            }
         } else {
             if (tid < kTile) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
             if (tid == 0) tile_done(o, ta, tb, n_chunk_rows);  // rejected: finished here
@@ -713,6 +721,7 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
             compute_tile(tiles[bi], tid);
             __syncthreads();  // the next tile's first DMA reuses buffer 0 and the compaction state
         }
+        scan_tail(sc.scan, nt);
     }
 }
 
@@ -823,6 +832,8 @@ void launch_candidates(const MfmaLaunch &m, uint32_t n, uint32_t idx, const uint
         v.tiles = m.cand_list;
         v.n_tiles = m.n_tiles;
         v.tile_count = m.cand_count;
+        v.tile_bits = sc.cand_bits;
+        v.scan = sc.scan;
         launch_pair_valu(v, o, nullptr, s);
         return;
     }
@@ -836,7 +847,7 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     const DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
     const uint64_t *ok_bits = reinterpret_cast<const uint64_t *>(m.wplanes + okbits_offset(m.NP));
     const bool prefilter = !dense && m.prefilter && m.thr > 0.0f;
-    ScreenArgs sc{0.0, 0.0f, 0.0f, 0.0f, 0, m.nonneg, m.cand_list, m.cand_count};
+    ScreenArgs sc{0.0, 0.0f, 0.0f, 0.0f, 0, m.nonneg, m.cand_list, m.cand_count, m.cand_list + m.n_tiles, ScanArgs{}};
     if (!m.frag) {  // site-major kernel (all three planes)
         const dim3 g(m.n_tiles), b(256);
         if (dense)
@@ -873,6 +884,7 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
         launch_lds_planes<kModePrefilter>(n, m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, idx, o, dn, sc, s);
         return false;
     }
+    sc.scan = m.scan;  // from here on a screen runs (and a candidate launch after it)
     // Screen: the top plane alone over every tile, the residual of the lower
     // planes bounded by R (in top-digit units: exact, a power-of-two scaling
     // of an integer below 2^53); candidate tiles then get every plane.  With

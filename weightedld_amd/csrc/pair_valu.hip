@@ -37,7 +37,8 @@
 //     onto the horizontal sums (lib.rs:461-480).  With the epilogue op for
 //     op, the rows are bit-identical to lib.rs.
 // With LOOP the workgroup strides over a tile list whose length is known only
-// on the device (the candidate tiles of the i8 screen, pair_mfma.hip).
+// on the device (the candidate tiles of the i8 screen, pair_mfma.hip), and
+// the last workgroup runs the run's chunk scan (scan_tail).
 #include "pair_common.hpp"
 
 namespace wld {
@@ -67,8 +68,9 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
 __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) : 2) void pair_valu_kernel(
     const uint8_t *__restrict__ codes, const float *__restrict__ w, const uint8_t *__restrict__ site_ok,
-    const uint32_t *__restrict__ tiles, const unsigned *tile_count, uint32_t L, uint32_t NP, uint32_t flush,
-    uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, OrderArgs o, DenseArgs dn) {
+    const uint32_t *__restrict__ tiles, const unsigned *tile_count, const uint32_t *__restrict__ tile_bits,
+    uint32_t L, uint32_t NP, uint32_t flush,
+    uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, OrderArgs o, DenseArgs dn, ScanArgs sa) {
     __shared__ __attribute__((aligned(16))) uint8_t sA[kTile * kStride];
     __shared__ __attribute__((aligned(16))) uint8_t sB[kTile * kStride];
     __shared__ __attribute__((aligned(16))) float sW[64];
@@ -77,7 +79,9 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
     __shared__ uint16_t sRowP[kTile][4];
     __shared__ uint32_t sRowBase[kTile];
 
-    auto compute_tile = [&](uint32_t tile, uint32_t tid) {
+    // bits: the 16x16 sub-blocks whose pairs are computed (MF: wave w's
+    // block n is bit 4w + n; its MFMAs are skipped when clear)
+    auto compute_tile = [&](uint32_t tile, uint32_t tid, uint32_t bits) {
         const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
         const uint32_t a0 = ta * kTile, b0 = tb * kTile;
         const uint32_t tx = tid & 15, ty = tid >> 4;
@@ -116,6 +120,7 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
                 const uint32_t lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
                 const uint8_t *rowA = sA + (16 * wave + r) * kStride + g;
                 const uint8_t *rowB = sB + r * kStride + g;
+                const uint32_t wbits = __builtin_amdgcn_readfirstlane((bits >> (4 * wave)) & 15u);
 #pragma unroll 4
                 for (int kk = 0; kk < 64; kk += 4) {
                     const float we = sW[kk + g];
@@ -124,6 +129,7 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
                     const float v = (ca & kCodeMaj) ? we : 0.0f;
 #pragma unroll
                     for (int n = 0; n < 4; ++n) {
+                        if (!((wbits >> n) & 1u)) continue;  // wave-uniform
                         const uint32_t cb = rowB[16 * n * kStride + kk];
                         const float fi = (float)(cb & 1u), fm = (float)(cb >> 1);
                         accM[n][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fi, accM[n][0], 0, 0, 0);
@@ -291,7 +297,8 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
                         dn.valid[k] = valid ? 1 : 0;
                     }
                 } else {
-                    if (valid && r2 > thr) passmask[i] |= 1u << j;  // lib.rs:660 strict '>'
+                    // lib.rs:660 strict '>' (a skipped sub-block's pairs provably fail)
+                    if (valid && r2 > thr && ((bits >> (4 * (arow(i) >> 4) + j)) & 1u)) passmask[i] |= 1u << j;
                 }
             }
         }
@@ -353,13 +360,14 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
 
     if constexpr (!LOOP) {
         const uint32_t tile = tiles[blockIdx.x];
-        if (tile != kNoTile) compute_tile(tile, threadIdx.x);  // kNoTile: padding of an XCD-ordered list
+        if (tile != kNoTile) compute_tile(tile, threadIdx.x, 0xFFFFu);  // kNoTile: padding of an XCD-ordered list
     } else {
         const uint32_t nt = *tile_count;
         for (uint32_t bi = blockIdx.x; bi < nt; bi += gridDim.x) {
-            compute_tile(tiles[bi], threadIdx.x);
+            compute_tile(tiles[bi], threadIdx.x, tile_bits ? tile_bits[bi] : 0xFFFFu);
             __syncthreads();  // the next tile's staging and compaction reuse the LDS
         }
+        scan_tail(sa, nt);
     }
 }
 
@@ -410,8 +418,8 @@ template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
 void launch_v(const ValuLaunch &v, uint32_t grid, uint32_t flush, uint32_t cs, const OrderArgs &o,
               const DenseArgs &dn, hipStream_t s) {
     hipLaunchKernelGGL((pair_valu_kernel<DENSE, SAFE, MF, REF, LOOP>), dim3(grid), dim3(256), 0, s, v.codes, v.w,
-                       v.site_ok, v.tiles, v.tile_count, v.L, v.NP, flush, cs, v.ref_tail_n, v.n_chunk_rows, v.thr, o,
-                       dn);
+                       v.site_ok, v.tiles, v.tile_count, v.tile_bits, v.L, v.NP, flush, cs, v.ref_tail_n, v.n_chunk_rows, v.thr, o,
+                       dn, v.scan);
 }
 }  // namespace
 
