@@ -211,8 +211,10 @@ def main():
                     help="at N=1: run the N>1 step path (RCCL group of one, ShardStep/pipelined steps)")
     ap.add_argument("--tile-rows", action="store_true",
                     help="plain (a-tile, b-tile) launch order instead of the XCD-aware one (WLD_OPT_TILE_ORDER 1; same rows)")
-    ap.add_argument("--pipe-depth", type=int, default=2, metavar="D",
-                    help="N>1 (or --rehearse-dist): contexts of the pipelined step loop, D - 1 steps in flight")
+    ap.add_argument("--pipe-depth", type=int, default=3, metavar="D",
+                    help="N>1 (or --rehearse-dist): contexts of the pipelined step loop, D - 1 steps in flight "
+                         "(profiles/r03i/: 3 with unserialized screens takes rank 0's 1/8 shard of C4 from "
+                         "0.142 to 0.120 ms/step)")
     ap.add_argument("--rehearse-shard", type=int, default=0, metavar="K",
                     help="with --rehearse-dist: run rank 0's shard of a K-way split (the per-rank work at "
                          "N=K; value counts that shard's pairs); a rehearsal line, never the headline")
@@ -330,11 +332,14 @@ def main():
     if dist_on and pipelined:
         pipe = wdist.PipelinedShardStep([ctx] + [new_ctx() for _ in range(max(2, args.pipe_depth) - 1)], rank, world,
                                         device,
-                                        # "pair" (default): step i's pair kernel waits on the device for
-                                        # step i-1's (wld_run_after); 0: may overlap it; 1: waits for
-                                        # step i-1's whole run (profiles/r02pc/)
+                                        # 0 (default): step i's screen may start while step i-1's runs, so
+                                        # a shard's last round of tiles overlaps the next step's first and
+                                        # no cross-queue event wait (~20 us) sits between them; "pair":
+                                        # step i's pair kernel waits on the device for step i-1's screen
+                                        # (wld_run_after); 1: for step i-1's whole run (profiles/r02pc/,
+                                        # profiles/r03i/)
                                         serialize_kernels={"0": False, "1": True}.get(
-                                            os.environ.get("WLD_PIPE_SERIALIZE", "pair"), "pair"))
+                                            os.environ.get("WLD_PIPE_SERIALIZE", "0"), "pair"))
 
     def nrows(res):
         return int(res[1].shape[1]) if res is not None and res[1] is not None else 0

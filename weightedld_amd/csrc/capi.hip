@@ -431,7 +431,8 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
     if (!c->opt_tile_rows && t.size() >= 4096 && T_used < 65535) t = xcd_order(t);
     c->n_tiles = (uint32_t)t.size();
     WLD_TRY(ensure(c->tiles, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));
-    WLD_TRY(ensure(c->cand, std::max<size_t>(t.size(), 1) * 2 * sizeof(uint32_t)));  // screen candidates + bits
+    // screen candidates: 16 weight buckets of tiles, then of their sub-block bits
+    WLD_TRY(ensure(c->cand, std::max<size_t>(t.size(), 1) * 32 * sizeof(uint32_t)));
     if (!t.empty())
         HIP_TRY(hipMemcpyAsync(c->tiles.p, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -550,6 +551,8 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
         m.cand_list = ptr<uint32_t>(c->cand);
         m.cand_count = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 2);
+        m.cand_work = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 3) + 1;  // beside the ticket
+        m.cand_buckets = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 4);
         if (scan && !dense) m.scan = *scan;
         if (ref_screen) {
             m.ref_valu = &rv;
@@ -933,9 +936,11 @@ int enqueue_pass(wld_ctx *c) {
     }
     c->run_dirty = true;  // until run_complete has seen this pass's scan
     const OrderArgs o = order_args(c);
-    unsigned long long *cn = ptr<unsigned long long>(c->counters);  // {cursor, total, cand_count, ticket}
+    // counters: {cursor, total, {candidate tiles, sub-blocks}, {ticket, work}, 16 bucket counts}
+    unsigned long long *cn = ptr<unsigned long long>(c->counters);
     ScanArgs sa{ptr<uint32_t>(c->chunk_total), r.lin_begin, lin_count, ptr<uint32_t>(c->chunk_base), cn + 1, cn,
-                c->d_hcnt, r.count_out, reinterpret_cast<unsigned *>(cn + 2), reinterpret_cast<unsigned *>(cn + 3)};
+                c->d_hcnt, r.count_out, reinterpret_cast<unsigned *>(cn + 2), reinterpret_cast<unsigned *>(cn + 4),
+                reinterpret_cast<unsigned *>(cn + 3)};
     c->h_cnt[0] = c->h_cnt[1] = lin_count ? ~0ull : 0ull;
     c->h_cnt[2] = c->h_cnt[3] = 0;
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
@@ -975,7 +980,7 @@ int run_enqueue(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uns
     const size_t ct_bytes = c->chunk_total.bytes, cn_bytes = c->counters.bytes;
     WLD_TRY(ensure(c->chunk_total, std::max<size_t>(n_chunks, 1) * sizeof(uint32_t)));
     WLD_TRY(ensure(c->chunk_base, std::max<size_t>(n_chunks, 1) * sizeof(uint32_t)));
-    WLD_TRY(ensure(c->counters, 4 * sizeof(unsigned long long)));
+    WLD_TRY(ensure(c->counters, kCounterWords * sizeof(unsigned long long)));
     if (c->chunk_total.bytes != ct_bytes || c->counters.bytes != cn_bytes) c->run_dirty = true;  // fresh memory
     c->pend = RunPending{true, thr, lin_begin, lin_end, pairs, count_out};
     c->prog_pass = false;

@@ -57,8 +57,12 @@ struct ScanArgs {
     uint32_t *chunk_base;
     unsigned long long *total, *cursor, *host_out, *count_out;
     unsigned *cand_count;  // {candidate tiles, their candidate sub-blocks}
+    unsigned *cand_buckets;  // the 16 bucket counts of the candidate list (zeroed too; may be null)
     unsigned *ticket;  // 0 between launches; null: the scan is launched on its own
 };
+
+// 64-bit words of a context's run counters (capi.hip enqueue_pass)
+constexpr uint32_t kCounterWords = 12;
 
 struct DenseArgs {
     float *d, *dp, *r2;
@@ -98,6 +102,11 @@ struct ValuLaunch {
     // + b/16) whose pairs are computed; the others' pairs provably fail (the
     // screen's per-pair bound) and are skipped.  Null: every sub-block.
     const uint32_t *tile_bits;
+    unsigned *tile_work;  // tile_count launches: the work counter (0 before the launch)
+    // tile_count launches: the list in 16 buckets of bucket_cap entries
+    // (pair_common.hpp cand_entry; null: one plain list)
+    const unsigned *tile_buckets;
+    uint32_t bucket_cap;
     ScanArgs scan;        // tile_count launches: the run's scan fused into the last workgroup (ticket set)
 };
 void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
@@ -148,8 +157,10 @@ struct MfmaLaunch {
     bool screen2;    // the screen on the top two digit planes (>= 3 active planes)
     uint64_t resid[3];
     uint64_t dsum[4];
-    uint32_t *cand_list;   // 2 n_tiles entries: the candidate tiles, then their sub-block bits
+    uint32_t *cand_list;   // 32 n_tiles entries: 16 buckets of tiles, then 16 of their sub-block bits
     unsigned *cand_count;  // 0 before the launch (chunk_scan_kernel resets it)
+    unsigned *cand_buckets;  // 16 bucket counts, 0 before the launch (chunk_scan_kernel resets them)
+    unsigned *cand_work;   // the candidate launch's work counter (the screen zeroes it)
     // WLD_OPT_REF_SUMS: the candidate tiles go to the reference-order f32
     // kernel (ref_valu, tiles/tile_count filled in here) and the screen's
     // residual bound grows by r_extra_q (fixed-point units: how far the

@@ -21,7 +21,7 @@ namespace wld {
 __global__ __launch_bounds__(256) void run_init_kernel(unsigned long long *__restrict__ counters,
                                                         uint32_t *__restrict__ chunk_total, uint32_t n_chunks) {
     const uint32_t i0 = blockIdx.x * 256 + threadIdx.x, stride = gridDim.x * 256;
-    if (i0 < 4) counters[i0] = 0;
+    if (i0 < kCounterWords) counters[i0] = 0;
     for (uint32_t i = i0; i < n_chunks; i += stride) chunk_total[i] = 0;
 }
 

@@ -248,6 +248,8 @@ __device__ inline void chunk_scan_block(const ScanArgs &a) {
             blocks = ld32(a.cand_count + 1);
             a.cand_count[0] = a.cand_count[1] = 0;
         }
+        if (a.cand_buckets)
+            for (int b = 0; b < 16; ++b) a.cand_buckets[b] = 0;
         if (a.host_out) {
             a.host_out[0] = cur;
             a.host_out[1] = run;
@@ -264,6 +266,29 @@ __device__ inline void chunk_scan_block(const ScanArgs &a) {
         a.chunk_base[i] = (uint32_t)base;
         base += t;
     }
+}
+
+// The screen's candidate list in 16 buckets of capacity cap by computed 16x16
+// sub-blocks (a tile with c of them in bucket 16 - c: the heaviest first, so
+// the workgroups dealt round-robin over the CUs each get a mix and the list's
+// light tail goes to whichever finish first); entry (b, k) at b cap + k of the
+// tile and bit arrays.  The launch maps its u-th tile through the buckets'
+// prefix sums, which cand_prefix puts in s_pre[17] (every thread calls it).
+__device__ inline void cand_prefix(const unsigned *buckets, uint32_t *s_pre) {
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int b = 0; b < 16; ++b) {
+            s_pre[b] = run;
+            run += buckets[b];
+        }
+        s_pre[16] = run;
+    }
+    __syncthreads();
+}
+__device__ inline uint32_t cand_entry(const uint32_t *s_pre, uint32_t cap, uint32_t u) {
+    uint32_t b = 0;
+    while (b < 15 && s_pre[b + 1] <= u) ++b;
+    return b * cap + (u - s_pre[b]);
 }
 
 // The end of every workgroup of a candidate launch (a grid-stride loop over

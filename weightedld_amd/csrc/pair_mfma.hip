@@ -379,6 +379,9 @@ struct ScreenArgs {
     uint32_t *cand_list;    // kModeScreen: candidate tiles (packed ta << 16 | tb)
     unsigned *cand_count;   // kModeScreen: appended to; candidate launch: tile count
     uint32_t *cand_bits;    // kModeScreen: per list entry, its 16x16 sub-blocks holding a candidate pair
+    unsigned *cand_work;    // the candidate launch's work counter (kModeScreen: workgroup 0 zeroes it)
+    unsigned *cand_buckets; // the list's 16 bucket counts (cand_entry; the list and bits: 16 cand_cap each)
+    uint32_t cand_cap;
     ScanArgs scan;          // screen and candidate launches: the fused chunk scan (scan_tail)
 };
 
@@ -477,11 +480,12 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
             if (m) atomicOr(sMask, (unsigned long long)m);
             __syncthreads();
             if (tid == 0) {
-                const uint32_t bits = (uint32_t)*sMask;
-                const unsigned k = atomicAdd(sc.cand_count, 1u);
-                atomicAdd(sc.cand_count + 1, (unsigned)__popc(bits));  // sub-blocks to compute (stats)
-                sc.cand_list[k] = (ta << 16) | tb;
-                sc.cand_bits[k] = bits;
+                const uint32_t bits = (uint32_t)*sMask, nb = (uint32_t)__popc(bits);  // nb >= 1
+                const uint32_t e = (16u - nb) * sc.cand_cap + atomicAdd(&sc.cand_buckets[16u - nb], 1u);
+                atomicAdd(sc.cand_count, 1u);
+                atomicAdd(sc.cand_count + 1, nb);  // sub-blocks to compute (stats)
+                sc.cand_list[e] = (ta << 16) | tb;
+                sc.cand_bits[e] = bits;
             }
         } else {
             if (tid < kTile) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
@@ -709,17 +713,25 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
                                             sRowBase);
     };
     if constexpr (!LOOP) {
+        if constexpr (MODE == kModeScreen)
+            if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the candidate launch
         const uint32_t tile = tiles[blockIdx.x];
         if (tile != kNoTile) compute_tile(tile, threadIdx.x);  // kNoTile: padding of an XCD-ordered list
     } else {
+        // the first tile by workgroup id, the next ones from the work counter
+        __shared__ uint32_t s_next, s_pre[17];
         const uint32_t nt = *tile_count;
-        for (uint32_t bi = blockIdx.x; bi < nt; bi += gridDim.x) {
+        cand_prefix(sc.cand_buckets, s_pre);
+        for (uint32_t bi = blockIdx.x; bi < nt;) {
             // the thread id laundered per tile: nothing lane-derived is hoisted
             // out of the loop and held live across the epilogue
             uint32_t tid = threadIdx.x;
             asm volatile("" : "+v"(tid));
-            compute_tile(tiles[bi], tid);
-            __syncthreads();  // the next tile's first DMA reuses buffer 0 and the compaction state
+            compute_tile(tiles[cand_entry(s_pre, sc.cand_cap, bi)], tid);
+            if (threadIdx.x == 0) s_next = gridDim.x + atomicAdd(sc.cand_work, 1u);
+            __syncthreads();  // (also: the next tile's first DMA reuses buffer 0 and the compaction state)
+            bi = s_next;
+            __syncthreads();
         }
         scan_tail(sc.scan, nt);
     }
@@ -833,6 +845,9 @@ void launch_candidates(const MfmaLaunch &m, uint32_t n, uint32_t idx, const uint
         v.n_tiles = m.n_tiles;
         v.tile_count = m.cand_count;
         v.tile_bits = sc.cand_bits;
+        v.tile_work = sc.cand_work;
+        v.tile_buckets = sc.cand_buckets;
+        v.bucket_cap = sc.cand_cap;
         v.scan = sc.scan;
         launch_pair_valu(v, o, nullptr, s);
         return;
@@ -847,7 +862,8 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     const DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
     const uint64_t *ok_bits = reinterpret_cast<const uint64_t *>(m.wplanes + okbits_offset(m.NP));
     const bool prefilter = !dense && m.prefilter && m.thr > 0.0f;
-    ScreenArgs sc{0.0, 0.0f, 0.0f, 0.0f, 0, m.nonneg, m.cand_list, m.cand_count, m.cand_list + m.n_tiles, ScanArgs{}};
+    ScreenArgs sc{0.0,         0.0f,         0.0f,      0.0f,        0, m.nonneg, m.cand_list, m.cand_count,
+                  m.cand_list + 16 * (size_t)m.n_tiles, m.cand_work, m.cand_buckets, m.n_tiles, ScanArgs{}};
     if (!m.frag) {  // site-major kernel (all three planes)
         const dim3 g(m.n_tiles), b(256);
         if (dense)

@@ -35,7 +35,11 @@
 //     f32x8::sum() computes on x86 (lib.rs:447-452); the <= 7 tail sequences
 //     are then added onto tot one by one on the VALU, as the scalar loop adds
 //     onto the horizontal sums (lib.rs:461-480).  With the epilogue op for
-//     op, the rows are bit-identical to lib.rs.
+//     op, the rows are bit-identical to lib.rs.  Inside a class each group of
+//     16 positions is stored transposed (position 4g + j holds element 4j + g
+//     of the group): the MFMA's lane group g takes element 4j + g at step j,
+//     so one dword read gives a lane its codes (one 16-byte read its weights)
+//     for four steps.
 // With LOOP the workgroup strides over a tile list whose length is known only
 // on the device (the candidate tiles of the i8 screen, pair_mfma.hip), and
 // the last workgroup runs the run's chunk scan (scan_tail).
@@ -69,27 +73,56 @@ template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
 __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) : 2) void pair_valu_kernel(
     const uint8_t *__restrict__ codes, const float *__restrict__ w, const uint8_t *__restrict__ site_ok,
     const uint32_t *__restrict__ tiles, const unsigned *tile_count, const uint32_t *__restrict__ tile_bits,
+    unsigned *tile_work, const unsigned *tile_buckets, uint32_t bucket_cap,
     uint32_t L, uint32_t NP, uint32_t flush,
     uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, OrderArgs o, DenseArgs dn, ScanArgs sa) {
     __shared__ __attribute__((aligned(16))) uint8_t sA[kTile * kStride];
     __shared__ __attribute__((aligned(16))) uint8_t sB[kTile * kStride];
     __shared__ __attribute__((aligned(16))) float sW[64];
-    __shared__ uint8_t sMask[kTile][16];
-    __shared__ uint16_t sRowM[kTile][4];
-    __shared__ uint16_t sRowP[kTile][4];
+    __shared__ unsigned long long sBits[kTile];  // compaction: passing b per a row
     __shared__ uint32_t sRowBase[kTile];
 
-    // bits: the 16x16 sub-blocks whose pairs are computed (MF: wave w's
-    // block n is bit 4w + n; its MFMAs are skipped when clear)
+    // bits: the 16x16 sub-blocks whose pairs are computed (bit 4 (a / 16) +
+    // b / 16); the others' pairs provably fail (the screen's bound)
     auto compute_tile = [&](uint32_t tile, uint32_t tid, uint32_t bits) {
         const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
         const uint32_t a0 = ta * kTile, b0 = tb * kTile;
         const uint32_t tx = tid & 15, ty = tid >> 4;
 
         float acc[4][4][4], tot[4][4][4];
-        v4f accM[4][4];  // MF: [b block n][sum q], element e = a row slot
-        // a row of the tile for row slot i of this thread (b = tx + 16 j either way)
-        auto arow = [&](int i) -> uint32_t { return MF ? 4 * ty + i : ty + 16 * i; };
+        v4f accM[4][4];  // MF: [slot j][sum q], element e = a row slot
+        // MF + REF: the computed sub-blocks dealt over the waves.  In
+        // column-major order (k = 4 n + i: a rows 16 i.., b columns 16 n..)
+        // the u-th computed one goes to wave u % 4, slot u / 4: the stage
+        // barriers pace a tile by its busiest wave, and a diagonal tile's 10
+        // sub-blocks then take 3 slots on it instead of 4; all 16 give wave w
+        // the a rows 16 w.. against b block j in slot j.
+        uint32_t ui[4] = {0, 0, 0, 0}, un[4] = {0, 1, 2, 3};
+        bool us[4] = {true, true, true, true};
+        if constexpr (MF && REF) {
+            const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+            uint32_t cm = 0;
+            for (uint32_t k = 0; k < 16; ++k) cm |= ((bits >> (4 * (k & 3) + (k >> 2))) & 1u) << k;
+            cm = __builtin_amdgcn_readfirstlane(cm);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t m = cm;
+                for (uint32_t t = 0; t < 4 * (uint32_t)j + wave; ++t) m &= m - 1u;  // drop the first 4j + w
+                const uint32_t k = m ? (uint32_t)__builtin_ctz(m) : 0u;
+                us[j] = m != 0;
+                ui[j] = k & 3u;
+                un[j] = k >> 2;
+            }
+        }
+        // the tile's a row / b column of this thread's pair (row slot i, slot j)
+        auto pa = [&](int i, int j) -> uint32_t {
+            if constexpr (MF && REF) return 16 * ui[j] + 4 * (ty & 3) + i;
+            else return MF ? 4 * ty + i : ty + 16 * i;
+        };
+        auto pb = [&](int i, int j) -> uint32_t {
+            if constexpr (MF && REF) return 16 * un[j] + tx;
+            else return tx + 16 * j;
+        };
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -116,11 +149,46 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
         };
         // the staged 64 sequences into acc (VALU) / accM (MF), in sequence order
         auto compute_stage = [&]() {
-            if constexpr (MF) {
+            if constexpr (MF && REF) {
+                // transposed 16-position groups: lane (r, g) reads the dword of
+                // its row at 16 grp + 4 g = elements 16 grp + 4 e + g, e = 0..3;
+                // slot j (a rows 16 ui[j].., b block un[j]) runs its 16 MFMAs of
+                // the group when the wave holds it (us[j], wave-uniform)
+                const uint32_t lane = tid & 63, r = lane & 15, g = lane >> 4;
+#pragma unroll
+                for (int grp = 0; grp < 4; ++grp) {
+                    const float4 w4 = *reinterpret_cast<const float4 *>(sW + 16 * grp + 4 * g);
+                    const float we[4] = {w4.x, w4.y, w4.z, w4.w};
+                    float u[4], v[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (!us[j]) continue;  // (slots fill in order: us[j] implies us[j - 1])
+                        if (j == 0 || ui[j] != ui[j - 1]) {  // a rows of a new row block (all 16: slot 0 only)
+                            const uint32_t a4 =
+                                *reinterpret_cast<const uint32_t *>(sA + (16 * ui[j] + r) * kStride + 4 * g + 16 * grp);
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const uint32_t ca = a4 >> (8 * e);
+                                u[e] = (ca & kCodeIn) ? we[e] : 0.0f;
+                                v[e] = (ca & kCodeMaj) ? we[e] : 0.0f;
+                            }
+                        }
+                        const uint32_t b4 =
+                            *reinterpret_cast<const uint32_t *>(sB + (16 * un[j] + r) * kStride + 4 * g + 16 * grp);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float fi = (float)((b4 >> (8 * e)) & 1u), fm = (float)((b4 >> (8 * e + 1)) & 1u);
+                            accM[j][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[e], fi, accM[j][0], 0, 0, 0);
+                            accM[j][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[e], fi, accM[j][1], 0, 0, 0);
+                            accM[j][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[e], fm, accM[j][2], 0, 0, 0);
+                            accM[j][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[e], fm, accM[j][3], 0, 0, 0);
+                        }
+                    }
+                }
+            } else if constexpr (MF) {
                 const uint32_t lane = tid & 63, wave = tid >> 6, r = lane & 15, g = lane >> 4;
                 const uint8_t *rowA = sA + (16 * wave + r) * kStride + g;
                 const uint8_t *rowB = sB + r * kStride + g;
-                const uint32_t wbits = __builtin_amdgcn_readfirstlane((bits >> (4 * wave)) & 15u);
 #pragma unroll 4
                 for (int kk = 0; kk < 64; kk += 4) {
                     const float we = sW[kk + g];
@@ -129,7 +197,6 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
                     const float v = (ca & kCodeMaj) ? we : 0.0f;
 #pragma unroll
                     for (int n = 0; n < 4; ++n) {
-                        if (!((wbits >> n) & 1u)) continue;  // wave-uniform
                         const uint32_t cb = rowB[16 * n * kStride + kk];
                         const float fi = (float)(cb & 1u), fm = (float)(cb >> 1);
                         accM[n][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fi, accM[n][0], 0, 0, 0);
@@ -142,14 +209,31 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
 #pragma unroll 2
                 for (int kk = 0; kk < 64; kk += 4) {
                     uint32_t A[4], B[4];
+                    float wk[4];
+                    if constexpr (REF) {
+                        // elements kk + e (e = 0..3) of the transposed group
+                        // sit at 16 (kk / 16) + 4 e + (kk % 16) / 4
+                        const int p0 = 16 * (kk / 16) + (kk % 16) / 4;
+                        auto gather = [&](const uint8_t *row) {
+                            return (uint32_t)row[p0] | (uint32_t)row[p0 + 4] << 8 | (uint32_t)row[p0 + 8] << 16 |
+                                   (uint32_t)row[p0 + 12] << 24;
+                        };
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        A[i] = *reinterpret_cast<const uint32_t *>(sA + (ty + 16 * i) * kStride + kk);
+                        for (int i = 0; i < 4; ++i) A[i] = gather(sA + (ty + 16 * i) * kStride);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        B[j] = *reinterpret_cast<const uint32_t *>(sB + (tx + 16 * j) * kStride + kk);
-                    const float4 w4 = *reinterpret_cast<const float4 *>(sW + kk);
-                    const float wk[4] = {w4.x, w4.y, w4.z, w4.w};
+                        for (int j = 0; j < 4; ++j) B[j] = gather(sB + (tx + 16 * j) * kStride);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) wk[e] = sW[p0 + 4 * e];
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            A[i] = *reinterpret_cast<const uint32_t *>(sA + (ty + 16 * i) * kStride + kk);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            B[j] = *reinterpret_cast<const uint32_t *>(sB + (tx + 16 * j) * kStride + kk);
+                        const float4 w4 = *reinterpret_cast<const float4 *>(sW + kk);
+                        wk[0] = w4.x; wk[1] = w4.y; wk[2] = w4.z; wk[3] = w4.w;
+                    }
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const float we = wk[e];
@@ -236,13 +320,12 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
                 for (uint32_t t = 0; t < ref_tail_n; ++t) {
                     const float we = sW[t];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const uint32_t ca = sA[arow(i) * kStride + t];
-                        const float u = (ca & kCodeIn) ? we : 0.0f;
-                        const float v = (ca & kCodeMaj) ? we : 0.0f;
+                    for (int i = 0; i < 4; ++i)
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
-                            const uint32_t cb = sB[(MF ? 16 * j + (tid & 15) : tx + 16 * j) * kStride + t];
+                            const uint32_t ca = sA[pa(i, j) * kStride + t], cb = sB[pb(i, j) * kStride + t];
+                            const float u = (ca & kCodeIn) ? we : 0.0f;
+                            const float v = (ca & kCodeMaj) ? we : 0.0f;
                             if constexpr (!SAFE) {
                                 const float fi = (float)(cb & 1u), fm = (float)(cb >> 1);
                                 tot[i][j][0] = __builtin_fmaf(u, fi, tot[i][j][0]);
@@ -257,7 +340,6 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
                                 tot[i][j][3] += bm ? v : 0.0f;
                             }
                         }
-                    }
                 }
             }
         } else {
@@ -273,21 +355,19 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
         }
 
         // ---- epilogue ------------------------------------------------------
-        uint32_t passmask[4] = {0, 0, 0, 0};  // bit j per row i
+        uint32_t passmask[4] = {0, 0, 0, 0};  // bit j per row slot i
         float res[4][4][3];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const uint32_t a = a0 + arow(i);
-            const bool oka = a < L && site_ok[a];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint32_t b = b0 + tx + 16 * j;
+                const uint32_t al = pa(i, j), bl = pb(i, j), a = a0 + al, b = b0 + bl;
                 float d, dp, r2;
                 ld_epilogue(tot[i][j][0], tot[i][j][1], tot[i][j][2], tot[i][j][3], d, dp, r2);
                 res[i][j][0] = d;
                 res[i][j][1] = dp;
                 res[i][j][2] = r2;
-                const bool valid = oka && a < b && b < L && site_ok[b];
+                const bool valid = a < b && b < L && site_ok[a] && site_ok[b];
                 if constexpr (DENSE) {
                     if (a < b && b < L) {
                         const size_t k = (size_t)a * L + b;
@@ -297,33 +377,33 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
                         dn.valid[k] = valid ? 1 : 0;
                     }
                 } else {
-                    // lib.rs:660 strict '>' (a skipped sub-block's pairs provably fail)
-                    if (valid && r2 > thr && ((bits >> (4 * (arow(i) >> 4) + j)) & 1u)) passmask[i] |= 1u << j;
+                    // lib.rs:660 strict '>' (a skipped sub-block's pairs provably fail;
+                    // an empty slot's pairs alias slot 0's sub-block)
+                    if (valid && r2 > thr && us[j] && ((bits >> (4 * (al >> 4) + (bl >> 4))) & 1u))
+                        passmask[i] |= 1u << j;
                 }
             }
         }
         if constexpr (DENSE) return;
 
-        // ---- compaction: rows of each a in b order, tile slice of the staging ----
+        // ---- compaction: a 64x64 pass-bit matrix in LDS, rows in b order ----
+        // (a tile with no passing pair writes only its 64 zero counts)
+        if (!__syncthreads_or((passmask[0] | passmask[1] | passmask[2] | passmask[3]) != 0)) {
+            if (tid < kTile) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
+            if (tid == 0) tile_done(o, ta, tb, n_chunk_rows);
+            return;
+        }
+        if (tid < kTile) sBits[tid] = 0ull;
+        __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) sMask[arow(i)][tx] = (uint8_t)passmask[i];
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (passmask[i] & (1u << j)) atomicOr(&sBits[pa(i, j)], 1ull << pb(i, j));
         __syncthreads();
         if (tid < kTile) {
             const uint32_t r = tid;
-            uint32_t M[4] = {0, 0, 0, 0};
-            for (int x = 0; x < 16; ++x) {
-                const uint32_t nib = sMask[r][x];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) M[j] |= ((nib >> j) & 1u) << x;
-            }
-            uint32_t p = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                sRowM[r][j] = (uint16_t)M[j];
-                sRowP[r][j] = (uint16_t)p;
-                p += __popc(M[j]);
-            }
-            const uint32_t cnt = p;
+            const uint32_t cnt = __popcll(sBits[r]);
             const uint32_t incl = wave_inclusive_scan(cnt);
             const uint32_t excl = incl - cnt;
             const uint32_t total = __shfl(incl, 63, 64);
@@ -341,14 +421,14 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (!passmask[i]) continue;
-            const uint32_t r = arow(i);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 if (!(passmask[i] & (1u << j))) continue;
-                const uint64_t pos = (uint64_t)sRowBase[r] + sRowP[r][j] + __popc(sRowM[r][j] & ((1u << tx) - 1u));
+                const uint32_t al = pa(i, j), bl = pb(i, j);
+                const uint64_t pos = (uint64_t)sRowBase[al] + __popcll(sBits[al] & ((1ull << bl) - 1ull));
                 if (pos < o.st_capacity) {
-                    o.st_a[pos] = a0 + r;
-                    o.st_b[pos] = b0 + tx + 16 * j;
+                    o.st_a[pos] = a0 + al;
+                    o.st_b[pos] = b0 + bl;
                     o.st_d[pos] = res[i][j][0];
                     o.st_dp[pos] = res[i][j][1];
                     o.st_r2[pos] = res[i][j][2];
@@ -362,10 +442,20 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
         const uint32_t tile = tiles[blockIdx.x];
         if (tile != kNoTile) compute_tile(tile, threadIdx.x, 0xFFFFu);  // kNoTile: padding of an XCD-ordered list
     } else {
+        // the first tile by workgroup id, the next ones from a work counter
+        // (tile_work, zeroed by the screen): the workgroups that finish first
+        // take the list's tail, not fixed ones (tiles differ in their computed
+        // sub-blocks)
+        __shared__ uint32_t s_next, s_pre[17];
         const uint32_t nt = *tile_count;
-        for (uint32_t bi = blockIdx.x; bi < nt; bi += gridDim.x) {
-            compute_tile(tiles[bi], threadIdx.x, tile_bits ? tile_bits[bi] : 0xFFFFu);
-            __syncthreads();  // the next tile's staging and compaction reuse the LDS
+        if (tile_buckets) cand_prefix(tile_buckets, s_pre);
+        for (uint32_t bi = blockIdx.x; bi < nt;) {
+            const uint32_t e = tile_buckets ? cand_entry(s_pre, bucket_cap, bi) : bi;
+            compute_tile(tiles[e], threadIdx.x, tile_bits ? tile_bits[e] : 0xFFFFu);
+            if (threadIdx.x == 0) s_next = gridDim.x + atomicAdd(tile_work, 1u);
+            __syncthreads();  // (also: the next tile's staging and compaction reuse the LDS)
+            bi = s_next;
+            __syncthreads();
         }
         scan_tail(sa, nt);
     }
@@ -373,9 +463,10 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
 
 // The reference-order layout (REF): sequence seq -> position p of the lane-
 // class order.  Block j < 8 (cls positions each, cls = 0 when N < 8) holds
-// seq = 8t + j at p = j cls + t (t < floor(N/8)); the tail seq = 8 floor(N/8)
-// + t at p = 8 cls + t; every other position is padding (code 0, weight 0).
-// One thread per (site, position).
+// seq = 8t + j at p = j cls + t' (t < floor(N/8)), t' = t with each group of
+// 16 transposed (t = 16q + 4j + g at t' = 16q + 4g + j); the tail seq = 8
+// floor(N/8) + t at p = 8 cls + t; every other position is padding (code 0,
+// weight 0).  One thread per (site, position).
 __global__ __launch_bounds__(256) void ref_layout_kernel(const uint8_t *__restrict__ codes, const float *__restrict__ w,
                                                          uint32_t LP, uint32_t NP, uint32_t N, uint32_t NPr,
                                                          uint32_t cls, uint8_t *__restrict__ rcodes,
@@ -386,7 +477,8 @@ __global__ __launch_bounds__(256) void ref_layout_kernel(const uint8_t *__restri
     const uint32_t n8 = N / 8;
     uint32_t seq = 0xFFFFFFFFu;
     if (p < 8 * cls) {
-        const uint32_t blk = p / cls, t = p % cls;
+        const uint32_t blk = p / cls, tp = p % cls;
+        const uint32_t t = (tp & ~15u) | (tp & 3u) << 2 | (tp >> 2 & 3u);  // transposed 16-groups
         if (t < n8) seq = 8 * t + blk;
     } else if (p - 8 * cls < N - 8 * n8) {
         seq = 8 * n8 + (p - 8 * cls);
@@ -418,7 +510,7 @@ template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
 void launch_v(const ValuLaunch &v, uint32_t grid, uint32_t flush, uint32_t cs, const OrderArgs &o,
               const DenseArgs &dn, hipStream_t s) {
     hipLaunchKernelGGL((pair_valu_kernel<DENSE, SAFE, MF, REF, LOOP>), dim3(grid), dim3(256), 0, s, v.codes, v.w,
-                       v.site_ok, v.tiles, v.tile_count, v.tile_bits, v.L, v.NP, flush, cs, v.ref_tail_n, v.n_chunk_rows, v.thr, o,
+                       v.site_ok, v.tiles, v.tile_count, v.tile_bits, v.tile_work, v.tile_buckets, v.bucket_cap, v.L, v.NP, flush, cs, v.ref_tail_n, v.n_chunk_rows, v.thr, o,
                        dn, v.scan);
 }
 }  // namespace
