@@ -15,6 +15,7 @@ restatement of the lib.rs simd path (oracle/wld_oracle.c, "port"), threaded
 like rayon over 256x256 chunks, timed on a bounded sample of the same workload.
 """
 import argparse
+import collections
 import json
 import os
 import sys
@@ -326,9 +327,10 @@ def main():
     LP, NP = -(-L // 256) * 256, -(-N // 64) * 64
     pipelined = not args.no_pipeline and 2 * LP * NP <= 128 << 20
     pipe = None
-    ctx1b = None  # N=1: the second context of the pipelined loop
+    ctxs1 = None  # N=1: the contexts of the pipelined loop
     if not dist_on and pipelined:
-        ctx1b = new_ctx()
+        ctxs1 = [ctx] + [new_ctx() for _ in range(max(2, args.pipe_depth) - 1)]
+    serialize = os.environ.get("WLD_PIPE_SERIALIZE", "0")
     if dist_on and pipelined:
         pipe = wdist.PipelinedShardStep([ctx] + [new_ctx() for _ in range(max(2, args.pipe_depth) - 1)], rank, world,
                                         device,
@@ -351,23 +353,27 @@ def main():
         return int(rows.shape[1]) if rows is not None else 0
 
     def run_steps(k):
-        if ctx1b is not None:
-            # N=1 pipelined: step i on context i % 2 (double-buffered rows), the
-            # host completes step i-1 (wld_run_wait) while step i's kernel runs
-            # (after a step with rows, one at a time: its row assembly then does
-            # not compete with the next kernel)
-            cs, r, prev = (ctx, ctx1b), 0, None
+        if ctxs1 is not None:
+            # N=1 pipelined: step i on context i % D (D-buffered rows), up to
+            # D - 1 steps in flight; the host completes the oldest step
+            # (wld_run_wait) while the newer ones run.  Step i's screen may
+            # start while step i-1's runs (WLD_PIPE_SERIALIZE=pair: queued
+            # behind it with wld_run_after); after a step with rows the
+            # pipeline drains first, so row assembly does not compete with
+            # the next kernels.
+            pend, r = collections.deque(), 0
             for i in range(k):
-                c = cs[i & 1]
-                if prev is not None and r > 0:
-                    r, prev = prev.run_wait(), None
-                if prev is not None:
-                    c.run_after(prev)  # this pair kernel queued behind the previous one (device wait)
+                c = ctxs1[i % len(ctxs1)]
+                if len(pend) == len(ctxs1) or (r > 0 and pend):
+                    while pend and (len(pend) == len(ctxs1) or r > 0):
+                        r = pend.popleft().run_wait()
+                if pend and serialize == "pair":
+                    c.run_after(pend[-1])  # this pair kernel queued behind the previous one (device wait)
                 c.run_chunks_async(thr, cb, ce)
-                if prev is not None:
-                    r = prev.run_wait()
-                prev = c
-            return prev.run_wait() if prev is not None else r
+                pend.append(c)
+            while pend:
+                r = pend.popleft().run_wait()
+            return r
         if pipe is None:
             r = 0
             for _ in range(k):
@@ -562,7 +568,7 @@ def main():
                    "rows_passing": rows, "kernel": kern_name, "mfma_planes": planes,
                    "parallelism": "chunk-range shard x%d%s%s" % (
                        world, (" + RCCL gather" if dist_on else ""),
-                       ", pipelined steps" if (pipe is not None or ctx1b is not None) else "")},
+                       ", pipelined steps" if (pipe is not None or ctxs1 is not None) else "")},
         "roofline": roof,
         # SURVEY 8(d)'s no-reuse byte MODEL (2N bytes per pair as if every pair
         # re-read both site columns from HBM) — not a roofline: the kernel

@@ -301,3 +301,28 @@ def test_report_full_bench_workloads(W, cfg):
                 assert res["one_sided_outside_band"] == 0, res
                 assert res["beyond_tol_d"] == 0 and res["beyond_tol_r2"] == 0, res
         ctx.close()
+
+
+def test_ref_screen_policy(W):
+    # In lib.rs's order the candidates cost ~30 screen tiles each, so the auto
+    # policy keeps the one-plane screen until nine tenths of the tiles are
+    # candidates (then the two-plane screen, then the full f32 kernel); rows
+    # bit-identical to the oracle at every step of the policy.
+    ctx = W.Context(0, W.KERNEL_AUTO)
+    buf = synth(2000, 2000, 23)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ctx.load(buf, w)
+    seen = []
+    for thr in (0.002, 0.002, 0.002, 0.003, 0.05):
+        ctx.run(thr)
+        st = ctx.stats()
+        seen.append((thr, st["screened"], st["candidate_tiles"], st["tiles"]))
+        assert_rows_bit_exact(ctx.rows(), O.all_pairs(buf, w, np.float32(thr)))
+    assert seen[0][1] == 1, seen
+    for prev, cur in zip(seen[:2], seen[1:3]):
+        bad = prev[2] * 10 > prev[3] * 9
+        if prev[1] == 1:
+            assert cur[1] == (3 if bad else 1), seen
+        elif prev[1] == 3:
+            assert cur[1] == (0 if bad else 3), seen
+    assert seen[-1][1] == 1, seen

@@ -106,8 +106,11 @@ struct wld_ctx {
     // wld_set_option (include/weightedld.h)
     bool opt_prefilter = true, opt_tile_rows = false, opt_all_planes = false;
     int opt_screen = 1;             // WLD_OPT_SCREEN: 0 never, 1 auto (default), 2 always, 3 always two-plane
-    float screen_bad_thr = -1.0f;   // auto: the largest threshold at which the screen left > half the tiles
-    float screen2_bad_thr = -1.0f;  // auto: ... at which the two-plane screen left > a fifth of them
+    // auto: the largest threshold at which the screen left > half the tiles (in
+    // lib.rs's order: > nine tenths), and at which the two-plane screen left > a
+    // fifth (nine tenths)
+    float screen_bad_thr = -1.0f;
+    float screen2_bad_thr = -1.0f;
     bool opt_site_major = false, opt_valu_plain = false;
     bool opt_ref_sums = true;  // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order (default)
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
@@ -675,7 +678,10 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
             break;
         case WLD_OPT_MFMA_LAYOUT: c->opt_site_major = value != 0; break;
         case WLD_OPT_VALU_PLAIN: c->opt_valu_plain = value != 0; break;
-        case WLD_OPT_REF_SUMS: c->opt_ref_sums = value != 0; break;
+        case WLD_OPT_REF_SUMS:
+            c->opt_ref_sums = value != 0;
+            c->screen_bad_thr = c->screen2_bad_thr = -1.0f;  // the policy's break-even differs
+            break;
         case WLD_OPT_STAGING_ROWS:
             if (value < 1) return fail(WLD_E_ARG, "WLD_OPT_STAGING_ROWS must be >= 1");
             c->opt_staging_rows = (uint64_t)value;
@@ -1090,12 +1096,17 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     // auto: a threshold at which even the i8 screen leaves more than half the
     // tiles is not screened from now on (nor any lower one): the screen costs a
     // third of the full three-plane kernel, the candidates as much again
-    if (c->screened && !c->screened2 && h[2] * 2 > c->n_tiles)
-        c->screen_bad_thr = std::max(c->screen_bad_thr, r.thr);
     // ... and one at which the two-plane screen (0.8 of the full kernel's
     // time at BASELINE config 4, profiles/r02s2/) leaves more than a fifth
-    // goes to the full kernel
-    if (c->screened && c->screened2 && h[2] * 5 > c->n_tiles) c->screen2_bad_thr = std::max(c->screen2_bad_thr, r.thr);
+    // goes to the full kernel.  In lib.rs's order the candidates run on the
+    // f32 kernel, about 30 times a screen tile's cost (C4: 27.8 ms for every
+    // tile against a 0.9 ms screen), so either screen pays until nine tenths
+    // of the tiles are candidates.
+    const bool ref_cand = c->opt_ref_sums != 0;
+    if (c->screened && !c->screened2 && h[2] * (ref_cand ? 10 : 2) > c->n_tiles * (ref_cand ? 9 : 1))
+        c->screen_bad_thr = std::max(c->screen_bad_thr, r.thr);
+    if (c->screened && c->screened2 && h[2] * (ref_cand ? 10 : 5) > c->n_tiles * (ref_cand ? 9 : 1))
+        c->screen2_bad_thr = std::max(c->screen2_bad_thr, r.thr);
     c->stats.screen_ms = c->screened ? event_ms(c->ev[2], c->ev[6]) : 0.0;
     c->stats.candidate_tiles = c->screened ? h[2] : c->n_tiles;
     c->stats.candidate_blocks = c->screened ? h[3] : 16 * (uint64_t)c->n_tiles;
