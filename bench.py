@@ -212,10 +212,10 @@ def main():
                     help="at N=1: run the N>1 step path (RCCL group of one, ShardStep/pipelined steps)")
     ap.add_argument("--tile-rows", action="store_true",
                     help="plain (a-tile, b-tile) launch order instead of the XCD-aware one (WLD_OPT_TILE_ORDER 1; same rows)")
-    ap.add_argument("--pipe-depth", type=int, default=3, metavar="D",
-                    help="N>1 (or --rehearse-dist): contexts of the pipelined step loop, D - 1 steps in flight "
-                         "(profiles/r03i/: 3 with unserialized screens takes rank 0's 1/8 shard of C4 from "
-                         "0.142 to 0.120 ms/step)")
+    ap.add_argument("--pipe-depth", type=int, default=0, metavar="D",
+                    help="contexts of the pipelined step loop, D - 1 steps in flight (default: 3 for the N>1 "
+                         "step path, where unserialized screens take rank 0's 1/8 shard of C4 from 0.142 to "
+                         "0.118 ms/step, profiles/r03j/; 2 at N=1, where three measured equal, profiles/r03q/)")
     ap.add_argument("--rehearse-shard", type=int, default=0, metavar="K",
                     help="with --rehearse-dist: run rank 0's shard of a K-way split (the per-rank work at "
                          "N=K; value counts that shard's pairs); a rehearsal line, never the headline")
@@ -327,12 +327,16 @@ def main():
     LP, NP = -(-L // 256) * 256, -(-N // 64) * 64
     pipelined = not args.no_pipeline and 2 * LP * NP <= 128 << 20
     pipe = None
+    # N>1: three contexts, step i's screen may overlap step i-1's; N=1: two,
+    # queued back to back with wld_run_after (WLD_PIPE_SERIALIZE / --pipe-depth
+    # select the others)
+    depth = args.pipe_depth or (3 if dist_on else 2)
+    serialize = os.environ.get("WLD_PIPE_SERIALIZE", "0" if dist_on else "pair")
     ctxs1 = None  # N=1: the contexts of the pipelined loop
     if not dist_on and pipelined:
-        ctxs1 = [ctx] + [new_ctx() for _ in range(max(2, args.pipe_depth) - 1)]
-    serialize = os.environ.get("WLD_PIPE_SERIALIZE", "0")
+        ctxs1 = [ctx] + [new_ctx() for _ in range(max(2, depth) - 1)]
     if dist_on and pipelined:
-        pipe = wdist.PipelinedShardStep([ctx] + [new_ctx() for _ in range(max(2, args.pipe_depth) - 1)], rank, world,
+        pipe = wdist.PipelinedShardStep([ctx] + [new_ctx() for _ in range(max(2, depth) - 1)], rank, world,
                                         device,
                                         # 0 (default): step i's screen may start while step i-1's runs, so
                                         # a shard's last round of tiles overlaps the next step's first and
@@ -340,8 +344,7 @@ def main():
                                         # step i's pair kernel waits on the device for step i-1's screen
                                         # (wld_run_after); 1: for step i-1's whole run (profiles/r02pc/,
                                         # profiles/r03i/)
-                                        serialize_kernels={"0": False, "1": True}.get(
-                                            os.environ.get("WLD_PIPE_SERIALIZE", "0"), "pair"))
+                                        serialize_kernels={"0": False, "1": True}.get(serialize, "pair"))
 
     def nrows(res):
         return int(res[1].shape[1]) if res is not None and res[1] is not None else 0
@@ -568,7 +571,10 @@ def main():
                    "rows_passing": rows, "kernel": kern_name, "mfma_planes": planes,
                    "parallelism": "chunk-range shard x%d%s%s" % (
                        world, (" + RCCL gather" if dist_on else ""),
-                       ", pipelined steps" if (pipe is not None or ctxs1 is not None) else "")},
+                       (", pipelined steps (%d contexts, %s)" % (
+                           depth, {"0": "screens may overlap", "1": "serialized on the whole step"}.get(
+                               serialize, "pair kernels queued back to back"))
+                        if (pipe is not None or ctxs1 is not None) else ""))},
         "roofline": roof,
         # SURVEY 8(d)'s no-reuse byte MODEL (2N bytes per pair as if every pair
         # re-read both site columns from HBM) — not a roofline: the kernel
