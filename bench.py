@@ -335,6 +335,9 @@ def main():
     ctxs1 = None  # N=1: the contexts of the pipelined loop
     if not dist_on and pipelined:
         ctxs1 = [ctx] + [new_ctx() for _ in range(max(2, depth) - 1)]
+        if serialize == "stream":  # every context on the first one's stream (wld_set_stream)
+            for c in ctxs1[1:]:
+                c.set_stream(ctx)
     if dist_on and pipelined:
         pipe = wdist.PipelinedShardStep([ctx] + [new_ctx() for _ in range(max(2, depth) - 1)], rank, world,
                                         device,
@@ -370,7 +373,7 @@ def main():
                 if len(pend) == len(ctxs1) or (r > 0 and pend):
                     while pend and (len(pend) == len(ctxs1) or r > 0):
                         r = pend.popleft().run_wait()
-                if pend and serialize == "pair":
+                if pend and serialize in ("pair", "stream"):
                     c.run_after(pend[-1])  # this pair kernel queued behind the previous one (device wait)
                 c.run_chunks_async(thr, cb, ce)
                 pend.append(c)
@@ -572,7 +575,8 @@ def main():
                    "parallelism": "chunk-range shard x%d%s%s" % (
                        world, (" + RCCL gather" if dist_on else ""),
                        (", pipelined steps (%d contexts, %s)" % (
-                           depth, {"0": "screens may overlap", "1": "serialized on the whole step"}.get(
+                           depth, {"0": "screens may overlap", "1": "serialized on the whole step",
+                                   "stream": "one stream"}.get(
                                serialize, "pair kernels queued back to back"))
                         if (pipe is not None or ctxs1 is not None) else ""))},
         "roofline": roof,

@@ -333,6 +333,14 @@ int wld_run_wait(wld_ctx *ctx, uint64_t *n_rows);
 int wld_run_after(wld_ctx *ctx, wld_ctx *prev);
 /* The context's HIP stream (hipStream_t), for ordering caller work after a run. */
 void *wld_stream(wld_ctx *ctx);
+/* Runs the context's device work on the caller's HIP stream from now on
+ * (a hipStream_t of the context's device; NULL: back to the context's own
+ * stream).  Contexts given one stream run one after another in enqueue order
+ * with nothing between their kernels (the N=1 pipelined loop: the next run
+ * queued behind the previous one without a cross-queue event, cf.
+ * wld_run_after, which then returns at once).  WLD_E_STATE during a run,
+ * WLD_E_ARG for device groups. */
+int wld_set_stream(wld_ctx *ctx, void *stream);
 /* All pairs of the loaded set, any size, rows to host: runs the reference's
  * chunk sequence in batches of at most 2^31 pairs (one wld_run_chunks each),
  * appending each batch's rows to library-allocated host arrays in reference

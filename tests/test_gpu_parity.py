@@ -699,6 +699,54 @@ def test_run_chunks_async_matches_sync(W, ctxs):
         ctx.run_wait()  # nothing in flight
 
 
+def test_contexts_on_one_stream(W):
+    # wld_set_stream: three contexts on the first one's stream, runs enqueued
+    # back to back (no event between them; wld_run_after a no-op), each
+    # context's rows bit-identical to the oracle's in lib.rs's order; back on
+    # its own stream afterwards; refused during a run.
+    L, N = 600, 300
+    buf = synth(L, N, 91)
+    w = np.random.default_rng(9).random(N).astype(np.float32) + 0.05
+    cs = [W.Context(0) for _ in range(3)]
+    for c in cs:
+        c.load(buf, w)
+    for c in cs[1:]:
+        c.set_stream(cs[0])
+        assert c.stream_ptr() == cs[0].stream_ptr()
+    thrs = [0.0, 0.02, 0.3, 0.02, 0.0, 0.3]
+    refs = {t: O.all_pairs(buf, w, np.float32(t)) for t in set(thrs)}
+    pend = []
+    for i, t in enumerate(thrs):
+        c = cs[i % 3]
+        if pend and pend[0][0] is c:
+            pc, pt = pend.pop(0)
+            assert pc.run_wait() == len(refs[pt]["site_a"])
+            _bit_equal_rows(pc.rows(), refs[pt])
+        if pend:
+            c.run_after(pend[-1][0])
+        c.run_chunks_async(t, 0, 0)
+        pend.append((c, t))
+        if i == 2:
+            with pytest.raises(W.WldError):
+                c.set_stream(None)  # during its run
+    for pc, pt in pend:
+        assert pc.run_wait() == len(refs[pt]["site_a"])
+        _bit_equal_rows(pc.rows(), refs[pt])
+    cs[1].set_stream(None)
+    assert cs[1].stream_ptr() not in (0, cs[0].stream_ptr())
+    assert cs[1].run(0.02) == len(refs[0.02]["site_a"])
+    _bit_equal_rows(cs[1].rows(), refs[0.02])
+
+
+def _bit_equal_rows(store, ref):
+    assert np.array_equal(store.site_a.astype(np.uint64), ref["site_a"])
+    assert np.array_equal(store.site_b.astype(np.uint64), ref["site_b"])
+    for f in ("d", "d_prime", "r2"):
+        g, r = getattr(store, f), np.asarray(ref[f], dtype=np.float32)
+        assert np.array_equal(g.view(np.uint32), r.view(np.uint32)) or \
+            np.all((g.view(np.uint32) == r.view(np.uint32)) | (np.isnan(g) & np.isnan(r))), f
+
+
 def test_shard_step_world1_rccl(W, ctxs):
     # ShardStep (the bench's N>1 step) through a real world-1 RCCL group: the
     # count all_gather ordered on the library's stream, then the rows.

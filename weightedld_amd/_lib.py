@@ -124,6 +124,7 @@ SIGNATURES = {
     "wld_run_wait": (_int, [_vp, _u64p]),
     "wld_run_after": (_int, [_vp, _vp]),
     "wld_stream": (_vp, [_vp]),
+    "wld_set_stream": (_int, [_vp, _vp]),
     "wld_run_host": (_int, [_vp, ctypes.c_float, PROGRESS_FN, _vp, ctypes.POINTER(Pairs)]),
     "wld_rows_device": (_int, [_vp, ctypes.POINTER(Pairs)]),
     "wld_rows_copy": (_int, [_vp, _u32p, _u32p, _f32p, _f32p, _f32p]),

@@ -338,6 +338,12 @@ class Context:
         """The context's hipStream_t as an int (torch.cuda.ExternalStream)."""
         return int(lib().wld_stream(self._h) or 0)
 
+    def set_stream(self, stream):
+        """wld_set_stream: run on another context's stream (a Context), a
+        hipStream_t given as an int, or None for the context's own."""
+        ptr = stream.stream_ptr() if isinstance(stream, Context) else (stream or 0)
+        check(lib().wld_set_stream(self._h, ctypes.c_void_p(ptr) if ptr else None), "wld_set_stream")
+
     def rows(self):
         v = Pairs()
         check(lib().wld_rows_device(self._h, ctypes.byref(v)), "wld_rows_device")

@@ -96,7 +96,8 @@ struct wld_ctx {
     // a device group (wld_create_multi): one member context per device; the
     // group itself owns no stream or buffers
     std::vector<wld_ctx *> members;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // where the context's work goes (own_stream or the caller's)
+    hipStream_t own_stream = nullptr;  // created with the context
     hipEvent_t ev[7] = {};  // 2..3 pair phase (6: after the screen), 3..4/5 order phase
     RunPending pend;                      // the run between run_enqueue and run_complete
     bool run_dirty = true;                // run state (cursor, chunk totals) may be nonzero: re-initialise
@@ -168,7 +169,7 @@ struct wld_ctx {
             if (e) (void)hipEventDestroy(e);
         if (h_cnt) (void)hipHostFree(h_cnt);
         if (h_plog) (void)hipHostFree(h_plog);
-        if (stream) (void)hipStreamDestroy(stream);
+        if (own_stream) (void)hipStreamDestroy(own_stream);
     }
 };
 
@@ -601,7 +602,8 @@ int wld_create(int device, wld_ctx **out) {
     HIP_TRY(hipSetDevice(device));
     auto *c = new wld_ctx;
     c->device = device;
-    hipError_t es = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    hipError_t es = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    c->stream = c->own_stream;
     if (es != hipSuccess) {
         delete c;
         return fail(WLD_E_HIP, "hipStreamCreate: %s", hipGetErrorString(es));
@@ -1162,7 +1164,18 @@ int wld_run_after(wld_ctx *c, wld_ctx *prev) {
     WLD_TRY(set_dev(c));
     // ev[6] separates a screened pass's screen from its candidate launch;
     // ev[3] follows the pair kernel(s) (enqueue_pass)
+    if (c->stream == prev->stream) return WLD_OK;  // one stream: already in order
     HIP_TRY(hipStreamWaitEvent(c->stream, prev->screened ? prev->ev[6] : prev->ev[3], 0));
+    return WLD_OK;
+}
+
+int wld_set_stream(wld_ctx *c, void *stream) {
+    if (!c) return fail(WLD_E_ARG, "null context");
+    if (!c->members.empty()) return fail(WLD_E_ARG, "wld_set_stream on a device group");
+    if (c->pend.active) return fail(WLD_E_STATE, "wld_set_stream during a run");
+    WLD_TRY(set_dev(c));
+    HIP_TRY(hipStreamSynchronize(c->stream));  // work already queued completes first
+    c->stream = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
     return WLD_OK;
 }
 
