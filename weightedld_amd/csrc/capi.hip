@@ -1029,7 +1029,7 @@ int drain_progress(wld_ctx *c, uint32_t n_chunks) {
         }
     };
     for (;;) {
-        const hipError_t q = hipStreamQuery(c->stream);
+        const hipError_t q = hipEventQuery(c->ev[4]);  // the pass's end (the stream may hold later work)
         drain();
         if (q == hipSuccess) break;
         if (q != hipErrorNotReady) HIP_TRY(q);
@@ -1056,7 +1056,9 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
             c->prog_pass = false;  // a re-run after a staging overflow does not report again
             WLD_TRY(drain_progress(c, lin_count));
         }
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        // the pass's end, not the stream's: on a shared stream (wld_set_stream)
+        // the next context's run may already be queued behind it
+        HIP_TRY(hipEventSynchronize(c->ev[4]));
         c->run_dirty = false;  // the pass completed: its scan cleaned the run state
         h[0] = __atomic_load_n(&c->h_cnt[0], __ATOMIC_ACQUIRE);
         h[1] = __atomic_load_n(&c->h_cnt[1], __ATOMIC_ACQUIRE);
@@ -1082,7 +1084,7 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
                       c->stream);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ev[5], c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipEventSynchronize(c->ev[5]));
         order_end = 5;
     }
     c->rows = rows;
