@@ -419,7 +419,7 @@ def main():
     elapsed = time.perf_counter() - t0
     # per-launch HIP-event times of the same steps, sampled after the timed
     # region so that reading them adds nothing to it
-    kms, oms, sms, cand, cblk = [], [], [], [], []
+    kms, oms, sms, cand, cblk, cpairs = [], [], [], [], [], []
     for _ in range(min(args.steps, 20)):
         tg = time.perf_counter()
         step()
@@ -429,8 +429,10 @@ def main():
         sms.append(st["screen_ms"])
         cand.append(st["candidate_tiles"])
         cblk.append(st["candidate_blocks"])
+        cpairs.append(st["candidate_pairs"])
         gms.append((time.perf_counter() - tg) * 1e3 - st["pair_kernel_ms"])
-    screen_kind = ctx.stats()["screened"]  # 0 none, 1 i8 one-plane screen, 3 two-plane screen
+    # 0 none, 1 i8 one-plane screen, 3 two-plane screen, 4 exact candidate pairs
+    screen_kind = ctx.stats()["screened"]
     screened = bool(screen_kind)
     n_tiles = ctx.stats()["tiles"]
     # the same steps without the screen (every tile, every plane; same rows),
@@ -483,7 +485,9 @@ def main():
         peak, unit = I8_MFMA_PEAK_TOPS, "TFLOP/s"
         dom_ms = screen_ms if screened else kernel_ms
         achieved = alg_ops / (dom_ms * 1e-3) / 1e12
-        if screened:
+        if screen_kind == 4:
+            kname = "pair_mfma_kernel<exact candidate pairs, %d planes>" % planes
+        elif screened:
             kname = "pair_mfma_kernel<screen,%d plane%s>" % ((2, "s") if screen_kind == 3 else (1, ""))
         else:
             kname = "pair_mfma_kernel<%d planes>" % planes
@@ -492,7 +496,7 @@ def main():
                 "kernel": kname, "kernel_ms": dom_ms}
         # what the matrix cores executed: P digit planes x 8 N per pair (one
         # or two i8 planes when screened)
-        ex_planes = (2 if screen_kind == 3 else 1) if screened else planes
+        ex_planes = (2 if screen_kind == 3 else 1) if screened and screen_kind != 4 else planes
         roof["executed_frac"] = shard_pairs * 8.0 * ex_planes * N / (dom_ms * 1e-3) / 1e12 / peak
         roof["executed_work"] = "%d i8 digit plane(s) x 8*N ops per pair" % ex_planes
         # against the i8 peak as well (the integer kernels' roofline)
@@ -516,11 +520,16 @@ def main():
         # tiles (4096 pairs each, diagonal tiles counted whole)
         cand_peak = F32_VALU_PEAK_TFLOPS if args.ref_sums else I8_MFMA_PEAK_TOPS
         cand_ops = n_cand * 4096 * 8.0 * N
-        roof["screen"] = {"kind": {3: "i8 two-plane"}.get(screen_kind, "i8"), "tiles": n_tiles,
+        if screen_kind == 4:  # the per-pair kernel's algorithmic work: 8N per candidate pair
+            cand_ops = float(np.mean(cpairs)) * 8.0 * N
+        roof["screen"] = {"kind": {3: "i8 two-plane", 4: "exact candidate pairs (i8, every plane)"}.get(screen_kind, "i8"),
+                          "tiles": n_tiles,
                           "candidate_tiles": n_cand, "candidate_fraction": n_cand / max(n_tiles, 1),
                           "screen_ms": screen_ms, "candidate_launch_ms": cand_ms,
-                          "candidate_kernel": ("pair_valu_kernel<ref order, f32 MFMA>" if args.ref_sums else
+                          "candidate_kernel": ("ref_rows_kernel<lib.rs order, one pair per thread>" if screen_kind == 4
+                                               else "pair_valu_kernel<ref order, f32 MFMA>" if args.ref_sums else
                                                "pair_mfma_kernel<prefilter, %d planes>" % planes),
+                          "candidate_pairs": float(np.mean(cpairs)) if screen_kind == 4 else None,
                           "candidate_frac": (cand_ops / (cand_ms * 1e-3) / 1e12 / cand_peak) if cand_ms > 0.02 else None,
                           "candidate_peak": cand_peak,
                           # --ref-sums computes only the candidate tiles' 16x16
@@ -539,7 +548,10 @@ def main():
     hbm_alg = shard_pairs * 2.0 * N / (kernel_ms * 1e-3) / 1e9  # 2N bytes per pair
     # the arithmetic the timed steps executed
     fixed = "%d-bit fixed-point weights" % (31 if planes == 4 else 23)
-    if kern_name == "mfma" and screened:
+    if kern_name == "mfma" and screen_kind == 4:
+        dtype = ("i8 MFMA, %d digit planes of %s, exact i32 sums, rigorous r2 bound with lib.rs's rounding; the "
+                 "%.0f candidate pairs: f32 sums in lib.rs's order, f32 epilogue" % (planes, fixed, float(np.mean(cpairs))))
+    elif kern_name == "mfma" and screened:
         dtype = ("i8 MFMA screen on the top weight digit%s (i32 sums, rigorous f32/f64 r2 bound over every pair); "
                  "candidate tiles (%.0f of %d): %s" % (
                      "s (2 planes)" if screen_kind == 3 else " (1 plane)", float(np.mean(cand)), n_tiles,

@@ -167,7 +167,15 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *                      tile goes to the full kernel directly); 2: always the
  *                      one-plane screen; 3: always the two-plane screen (the
  *                      one-plane one with fewer than three active planes);
- *                      0: every tile, every plane.
+ *                      0: every tile, every plane.  In lib.rs's order
+ *                      (WLD_OPT_REF_SUMS 1) auto replaces the two-plane tier:
+ *                      where the one-plane screen does not pay, every tile runs
+ *                      once on all planes, staging the pairs the bound cannot
+ *                      reject (the reference's rounding as residual), and only
+ *                      those are summed in lib.rs's order, one by one — unless
+ *                      at this or a higher threshold they were more than a
+ *                      tenth of all pairs (then the full f32 kernel); 4: always
+ *                      that path (lib.rs's order; otherwise as 0).
  *   WLD_OPT_TILE_ORDER 0 (default): L2/XCD-aware tile launch order; 1: plain
  *                      (a-tile, b-tile) order.
  *   WLD_OPT_ALL_PLANES 0 (default): all-zero digit planes are skipped; 1: the
@@ -379,11 +387,14 @@ typedef struct {
     uint64_t candidate_tiles;/* tiles computed with every plane (= tiles unless screened) */
     double screen_ms;        /* HIP-event time of the screen launch (0 if none)    */
     int screened;            /* 1: the last run ran the one-plane i8 screen; 3: the two-plane
-                                i8 screen; 0: none */
+                                i8 screen; 4: (lib.rs's order) the exact i8 pass staging the
+                                pairs its bound cannot reject, each then summed alone in
+                                lib.rs's order; 0: none */
     int ref_sums;            /* 1: the last run summed in lib.rs's f32 order (WLD_OPT_REF_SUMS) */
     uint64_t candidate_blocks; /* 16x16 sub-blocks of the candidate tiles holding a pair the screen
                                   could not reject (16 x candidate_tiles unless screened); with
                                   WLD_OPT_REF_SUMS only these are computed */
+    uint64_t candidate_pairs; /* screened == 4: the pairs summed one by one in lib.rs's order */
 } wld_run_stats;
 int wld_last_stats(wld_ctx *ctx, wld_run_stats *out);
 

@@ -304,25 +304,75 @@ def test_report_full_bench_workloads(W, cfg):
 
 
 def test_ref_screen_policy(W):
-    # In lib.rs's order the candidates cost ~30 screen tiles each, so the auto
-    # policy keeps the one-plane screen until nine tenths of the tiles are
-    # candidates (then the two-plane screen, then the full f32 kernel); rows
-    # bit-identical to the oracle at every step of the policy.
+    # lib.rs's order, auto policy: the one-plane screen until it leaves more
+    # than half the tiles as candidates; then the exact candidate pairs, each
+    # summed alone (screened 4), until those are more than a tenth of all
+    # pairs; then the full f32 kernel.  Rows bit-identical to the oracle at
+    # every step of the policy.
     ctx = W.Context(0, W.KERNEL_AUTO)
     buf = synth(2000, 2000, 23)
     w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
     ctx.load(buf, w)
     seen = []
-    for thr in (0.002, 0.002, 0.002, 0.003, 0.05):
-        ctx.run(thr)
+    for thr in (0.002, 0.002, 0.002, 0.003, 0.0005, 0.0005, 0.05):
+        n = ctx.run(thr)
         st = ctx.stats()
-        seen.append((thr, st["screened"], st["candidate_tiles"], st["tiles"]))
+        seen.append((thr, st["screened"], st["candidate_tiles"], st["tiles"], st["candidate_pairs"], st["pairs"]))
+        assert n == len(ctx.rows())
         assert_rows_bit_exact(ctx.rows(), O.all_pairs(buf, w, np.float32(thr)))
     assert seen[0][1] == 1, seen
-    for prev, cur in zip(seen[:2], seen[1:3]):
-        bad = prev[2] * 10 > prev[3] * 9
+    for prev, cur in zip(seen[:5], seen[1:6]):
+        if cur[0] > prev[0]:
+            continue  # a higher threshold may screen again
         if prev[1] == 1:
-            assert cur[1] == (3 if bad else 1), seen
-        elif prev[1] == 3:
-            assert cur[1] == (0 if bad else 3), seen
+            assert cur[1] == (4 if prev[2] * 2 > prev[3] else 1), seen
+        elif prev[1] == 4:
+            assert cur[1] == (0 if prev[4] * 10 > prev[5] else 4), seen
+            assert prev[4] >= n  # the candidates include every row
     assert seen[-1][1] == 1, seen
+
+
+@pytest.mark.parametrize("case", ["random", "ldblocks", "rare", "mixed_sign"])
+@pytest.mark.parametrize("thr", [0.002, 0.01, 0.05])
+def test_ref_pairs_rows_bit_exact(W, case, thr):
+    # WLD_OPT_SCREEN 4: every tile on all i8 planes, the pairs the bound cannot
+    # reject (the reference's rounding as residual) summed one by one in
+    # lib.rs's order: the rows (order, indices, d, d', r2) are the oracle's bit
+    # for bit, and every row was a candidate.
+    rng = np.random.default_rng(7)
+    w = None
+    if case == "random":
+        buf = synth(700, 300, 17)
+    elif case == "ldblocks":
+        buf = ld_blocks(900, 257, 3)
+    elif case == "rare":
+        buf, w = rare_carriers(600, 301, 5)
+    else:
+        buf = synth(500, 203, 19)
+    if w is None:
+        w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    if case == "mixed_sign":
+        w = (rng.random(buf.shape[1]) - 0.3).astype(np.float32)
+    ctx = W.Context(0, W.KERNEL_AUTO)
+    ctx.set_option("screen", 4)
+    ctx.load(buf, w)
+    n = ctx.run(thr)
+    st = ctx.stats()
+    ref = O.all_pairs(buf, w, np.float32(thr))
+    if st["kernel"] == W.KERNEL_MFMA:
+        assert st["screened"] == 4 and st["candidate_pairs"] >= n, st
+    assert_rows_bit_exact(ctx.rows(), ref)
+
+
+def test_ref_pairs_staging_regrow(W):
+    # a staging overflow of the candidate rows re-runs the pass with enough
+    # staging: the same rows
+    buf = synth(800, 300, 29)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ctx = W.Context(0, W.KERNEL_AUTO)
+    ctx.set_option("screen", 4)
+    ctx.set_option("staging_rows", 64)
+    ctx.load(buf, w)
+    n = ctx.run(0.003)
+    assert ctx.stats()["screened"] == 4 and n > 64
+    assert_rows_bit_exact(ctx.rows(), O.all_pairs(buf, w, np.float32(0.003)))

@@ -61,6 +61,7 @@ class RunStats(ctypes.Structure):
         ("screened", ctypes.c_int),
         ("ref_sums", ctypes.c_int),
         ("candidate_blocks", ctypes.c_uint64),
+        ("candidate_pairs", ctypes.c_uint64),
     ]
 
 

@@ -106,12 +106,15 @@ struct wld_ctx {
     int kernel_pref = WLD_KERNEL_AUTO;
     // wld_set_option (include/weightedld.h)
     bool opt_prefilter = true, opt_tile_rows = false, opt_all_planes = false;
-    int opt_screen = 1;             // WLD_OPT_SCREEN: 0 never, 1 auto (default), 2 always, 3 always two-plane
-    // auto: the largest threshold at which the screen left > half the tiles (in
-    // lib.rs's order: > nine tenths), and at which the two-plane screen left > a
-    // fifth (nine tenths)
+    int opt_screen = 1;  // WLD_OPT_SCREEN: 0 never, 1 auto (default), 2 always, 3 two-plane, 4 exact candidate pairs
+    // auto: the largest threshold at which the screen left > half the tiles,
+    // and at which the two-plane screen left > a fifth
     float screen_bad_thr = -1.0f;
     float screen2_bad_thr = -1.0f;
+    // auto, lib.rs's order: the largest threshold at which the exact candidate
+    // pairs were more than a tenth of all pairs (then the full f32 kernel)
+    float ref_pairs_bad_thr = -1.0f;
+    bool ref_pairs_pass = false;  // the pass staged exact candidate pairs (ref_rows_kernel)
     bool opt_site_major = false, opt_valu_plain = false;
     bool opt_ref_sums = true;  // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order (default)
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
@@ -213,7 +216,7 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     const size_t L = c->L, N = c->N;
     // a new data set: the auto screen policy (thresholds learned on the last
     // one) starts over; the reference-order layout is rebuilt when needed
-    c->screen_bad_thr = c->screen2_bad_thr = -1.0f;
+    c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = -1.0f;
     c->have_ref = false;
     c->LP = round_up(std::max<size_t>(L, 1), kChunk);
     c->NP = round_up(std::max<size_t>(N, 1), kSeqPad);
@@ -507,6 +510,7 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
     const uint32_t n = chunk_rows_of(c->L);
     bool sc = false;
     c->stats.ref_sums = c->opt_ref_sums ? 1 : 0;
+    c->ref_pairs_pass = false;
     ValuLaunch rv{};
     if (c->opt_ref_sums) {
         WLD_TRY(ensure_ref_layout(c));
@@ -541,14 +545,17 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         m.prefilter = c->opt_prefilter && thr > 0.0f;
         // auto: below a threshold at which the screen left more than half the
         // tiles as candidates, every tile goes straight to the full kernel
-        m.screen = m.prefilter && (c->opt_screen >= 2 || (c->opt_screen == 1 && thr > c->screen_bad_thr));
+        m.screen = m.prefilter && (c->opt_screen == 2 || c->opt_screen == 3 ||
+                                   (c->opt_screen == 1 && thr > c->screen_bad_thr));
         // ... where the one-plane screen proved ineffective, the two-plane one
-        // (>= 3 active planes), unless it proved ineffective too
-        if (m.prefilter && !m.screen && c->opt_screen == 1 && thr > c->screen2_bad_thr) m.screen = m.screen2 = true;
+        // (>= 3 active planes), unless it proved ineffective too; in lib.rs's
+        // order the exact candidate pairs instead (below)
+        if (m.prefilter && !m.screen && c->opt_screen == 1 && !ref_screen && thr > c->screen2_bad_thr)
+            m.screen = m.screen2 = true;
         if (c->opt_screen == 3) m.screen2 = true;
         if (m.screen2 && __builtin_popcount(c->plane_mask & 15) < 3) {
             m.screen2 = false;  // one or two active planes: the one-plane screen or the full kernel
-            m.screen = c->opt_screen >= 2;
+            m.screen = c->opt_screen == 2 || c->opt_screen == 3;
         }
         c->screened2 = m.screen && m.screen2;
         for (int t = 0; t < 3; ++t) m.resid[t] = c->wst.resid[t];
@@ -558,11 +565,21 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         m.cand_work = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 3) + 1;  // beside the ticket
         m.cand_buckets = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 4);
         if (scan && !dense) m.scan = *scan;
+        RefRowsLaunch rr{};
         if (ref_screen) {
             m.ref_valu = &rv;
             m.r_extra_q = ref_extra_residual(c);
+            // where the screen does not pay: every tile on all planes, the
+            // pairs the bound cannot reject summed one by one in lib.rs's
+            // order, unless that proved to be most pairs (then the full kernel)
+            if (!m.screen && ((c->opt_screen == 1 && thr > c->ref_pairs_bad_thr) || c->opt_screen == 4)) {
+                rr = RefRowsLaunch{ptr<uint8_t>(c->rcodes), ptr<float>(c->rw), (uint32_t)c->NPr, c->ref_cls,
+                                   (uint32_t)(c->N % 8), n, thr, nullptr, nullptr, nullptr, ScanArgs{}};
+                m.ref_rows = &rr;
+                c->ref_pairs_pass = true;
+            }
         }
-        if (ref_screen && !m.screen) {
+        if (ref_screen && !m.screen && !m.ref_rows) {
             launch_pair_valu(rv, o, nullptr, c->stream);  // the policy sends this threshold to the full kernel
         } else {
             sc = launch_pair_mfma(m, o, dense, c->stream, c->ev[6]);
@@ -664,9 +681,9 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
     switch (option) {
         case WLD_OPT_PREFILTER: c->opt_prefilter = value != 0; break;
         case WLD_OPT_SCREEN:
-            if (value < 0 || value > 3) return fail(WLD_E_ARG, "WLD_OPT_SCREEN takes 0, 1, 2 or 3");
+            if (value < 0 || value > 4) return fail(WLD_E_ARG, "WLD_OPT_SCREEN takes 0 to 4");
             c->opt_screen = (int)value;
-            c->screen_bad_thr = c->screen2_bad_thr = -1.0f;
+            c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = -1.0f;
             break;
         case WLD_OPT_TILE_ORDER:
             c->opt_tile_rows = value != 0;
@@ -682,7 +699,7 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
         case WLD_OPT_VALU_PLAIN: c->opt_valu_plain = value != 0; break;
         case WLD_OPT_REF_SUMS:
             c->opt_ref_sums = value != 0;
-            c->screen_bad_thr = c->screen2_bad_thr = -1.0f;  // the policy's break-even differs
+            c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = -1.0f;  // the policy's break-even differs
             break;
         case WLD_OPT_STAGING_ROWS:
             if (value < 1) return fail(WLD_E_ARG, "WLD_OPT_STAGING_ROWS must be >= 1");
@@ -1070,7 +1087,10 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
         WLD_TRY(enqueue_pass(c));
     }
     const uint64_t rows = h[1];
-    if (h[0] != h[1]) return fail(WLD_E_HIP, "internal: staging cursor %llu != chunk total %llu", h[0], h[1]);
+    // (exact candidate pairs: the cursor counts the candidates staged, the
+    // chunk totals the rows kept)
+    if (c->ref_pairs_pass ? h[0] < h[1] : h[0] != h[1])
+        return fail(WLD_E_HIP, "internal: staging cursor %llu vs chunk total %llu", h[0], h[1]);
     WLD_TRY(ensure(c->out_a, std::max<uint64_t>(rows, 1) * 4));
     WLD_TRY(ensure(c->out_b, std::max<uint64_t>(rows, 1) * 4));
     WLD_TRY(ensure(c->out_d, std::max<uint64_t>(rows, 1) * 4));
@@ -1096,24 +1116,29 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     c->stats.order_ms = event_ms(c->ev[3], c->ev[order_end]);
     c->stats.pair_kernel_launches = c->n_tiles ? (c->screened ? 2 : 1) : 0;
     c->stats.tiles = c->n_tiles;
-    c->stats.screened = c->screened ? (c->screened2 ? 3 : 1) : 0;
+    c->stats.screened = c->ref_pairs_pass ? 4 : c->screened ? (c->screened2 ? 3 : 1) : 0;
+    c->stats.candidate_pairs = c->ref_pairs_pass ? h[0] : 0;
     // auto: a threshold at which even the i8 screen leaves more than half the
     // tiles is not screened from now on (nor any lower one): the screen costs a
-    // third of the full three-plane kernel, the candidates as much again
+    // third of the full three-plane kernel, the candidates as much again; in
+    // lib.rs's order the exact candidate pairs take over there (a screened
+    // tile with one uncertain 16x16 sub-block costs ~0.12 us on the f32
+    // kernel: half the C4 tiles ~3 ms over the 0.9 ms screen, about the exact
+    // candidate pairs' cost)
     // ... and one at which the two-plane screen (0.8 of the full kernel's
     // time at BASELINE config 4, profiles/r02s2/) leaves more than a fifth
-    // goes to the full kernel.  In lib.rs's order the candidates run on the
-    // f32 kernel, about 30 times a screen tile's cost (C4: 27.8 ms for every
-    // tile against a 0.9 ms screen), so either screen pays until nine tenths
-    // of the tiles are candidates.
-    const bool ref_cand = c->opt_ref_sums != 0;
-    if (c->screened && !c->screened2 && h[2] * (ref_cand ? 10 : 2) > c->n_tiles * (ref_cand ? 9 : 1))
+    // goes to the full kernel (the exact mode; lib.rs's order takes the two-
+    // plane screen only when asked, WLD_OPT_SCREEN 3)
+    if (c->screened && !c->ref_pairs_pass && !c->screened2 && h[2] * 2 > c->n_tiles)
         c->screen_bad_thr = std::max(c->screen_bad_thr, r.thr);
-    if (c->screened && c->screened2 && h[2] * (ref_cand ? 10 : 5) > c->n_tiles * (ref_cand ? 9 : 1))
-        c->screen2_bad_thr = std::max(c->screen2_bad_thr, r.thr);
+    if (c->screened && c->screened2 && h[2] * 5 > c->n_tiles) c->screen2_bad_thr = std::max(c->screen2_bad_thr, r.thr);
+    // exact candidate pairs, each summed alone in lib.rs's order (~1 ms per
+    // million at C4 size): past a tenth of all pairs the full f32 kernel
+    // (27.8 ms for every tile at C4) is cheaper
+    if (c->ref_pairs_pass && h[0] * 10 > r.pairs) c->ref_pairs_bad_thr = std::max(c->ref_pairs_bad_thr, r.thr);
     c->stats.screen_ms = c->screened ? event_ms(c->ev[2], c->ev[6]) : 0.0;
     c->stats.candidate_tiles = c->screened ? h[2] : c->n_tiles;
-    c->stats.candidate_blocks = c->screened ? h[3] : 16 * (uint64_t)c->n_tiles;
+    c->stats.candidate_blocks = c->screened && !c->ref_pairs_pass ? h[3] : 16 * (uint64_t)c->n_tiles;
     if (n_rows) *n_rows = rows;
     return WLD_OK;
 }

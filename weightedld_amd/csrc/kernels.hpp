@@ -110,6 +110,22 @@ struct ValuLaunch {
     ScanArgs scan;        // tile_count launches: the run's scan fused into the last workgroup (ticket set)
 };
 void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
+// The candidate pairs a kModeRefPairs launch (pair_mfma.hip) staged, summed in
+// lib.rs's order one pair per thread from the lane-class layout; the passing
+// rows are kept in place (in order), their segment counts/offsets and chunk
+// totals corrected, the rest dropped.  The run's chunk scan runs in the last
+// workgroup (scan.ticket).
+struct RefRowsLaunch {
+    const uint8_t *rcodes;  // the lane-class layout (NPr bytes per site)
+    const float *rw;
+    uint32_t NPr, ref_cls, ref_tail_n, n_chunk_rows;
+    float thr;
+    const uint32_t *slices;  // per tile with candidates: {staging base, rows, ta << 16 | tb}
+    const unsigned *slice_count;
+    unsigned *work;  // work counter, 0 before the launch
+    ScanArgs scan;
+};
+void launch_ref_rows(const RefRowsLaunch &r, const OrderArgs &o, hipStream_t s);
 // the lane-class layout of REF: cls positions per class, the tail stage, NPr
 void ref_layout_dims(size_t N, uint32_t *cls, uint32_t *tail, size_t *NPr);
 void launch_ref_layout(const uint8_t *codes, const float *w_pad, size_t LP, size_t NP, size_t N, uint8_t *rcodes,
@@ -140,6 +156,8 @@ constexpr uint32_t kCandidateGrid = 2048;
 // workgroups (three per CU, 256 CUs); extra workgroups would only queue (and
 // cost dispatch time when there is no candidate at all)
 constexpr uint32_t kRefCandidateGrid = 768;
+// ... and of ref_rows_kernel (low-register, latency-bound: eight per CU)
+constexpr uint32_t kRefRowsGrid = 2048;
 
 struct MfmaLaunch {
     const uint8_t *codes;   // site-major codes (used when frag is null)
@@ -167,6 +185,11 @@ struct MfmaLaunch {
     // reference's f32 sums can lie from the fixed-point sums, 2x2-cell L1)
     const ValuLaunch *ref_valu;
     double r_extra_q;
+    // WLD_OPT_REF_SUMS without a screen: every tile on all planes, the pairs
+    // the bound cannot reject (residual r_extra_q) staged as candidates, then
+    // summed one by one in lib.rs's order (launch_ref_rows; ref_rows filled in
+    // here but for the slices, count and work counter)
+    const RefRowsLaunch *ref_rows;
     // with a screen: the run's scan, fused into the screen's or the candidate
     // launch's last workgroup when scan.ticket is set
     ScanArgs scan;

@@ -364,7 +364,13 @@ __device__ __forceinline__ void zero_acc(Acc16<NPL, NB> &acc) {
 //                  tile with any pair the bound cannot reject is appended to
 //                  the candidate list (recomputed with every plane by the
 //                  kModePrefilter launch), the others write their zero counts
-enum : int { kModeDense = 0, kModeAll = 1, kModePrefilter = 2, kModeScreen = 3 };
+//   kModeRefPairs  exact sums, then every valid pair r2_bound_skip cannot
+//                  reject with the reference's rounding as residual (sc.R) is
+//                  staged as a candidate row, and each tile's slice of them
+//                  recorded (sc.cand_list, sc.cand_count): ref_rows_kernel
+//                  (pair_valu.hip) then sums those pairs in lib.rs's order and
+//                  keeps the ones that pass
+enum : int { kModeDense = 0, kModeAll = 1, kModePrefilter = 2, kModeScreen = 3, kModeRefPairs = 4 };
 
 // the one-plane screen's doubled sums |2S| <= 256 NP stay exact in f32 up to here
 constexpr uint32_t kScrF32MaxNP = 16384;
@@ -391,12 +397,19 @@ struct ScreenArgs {
 // f32 epilogue ran (always for kModeDense).
 template <int MODE>
 __device__ __forceinline__ bool pair_eval(double T, double SA, double SB, double SAB, bool valid, float thr,
-                                          double scale, bool nonneg, float &d, float &dp, float &r2) {
+                                          double scale, bool nonneg, double R, float &d, float &dp, float &r2) {
     if constexpr (MODE != kModeDense) {
         if (!valid) return false;
         // the f32 epilogue below provably gives r2 <= thr (pair_common.hpp)
         if constexpr (MODE == kModePrefilter)
             if (r2_bound_skip(T, SA, SB, SAB, 0.0, thr, nonneg)) return false;
+        // ... or, with the reference's rounding as the sums' residual R, the
+        // reference's own f32 sums cannot give r2 > thr either; the others are
+        // candidates (their values come from ref_rows_kernel)
+        if constexpr (MODE == kModeRefPairs) {
+            d = dp = r2 = 0.0f;
+            return !r2_bound_skip(T, SA, SB, SAB, R, thr, nonneg);
+        }
     }
     ld_epilogue((float)(T * scale), (float)(SA * scale), (float)(SB * scale), (float)(SAB * scale), d, dp, r2);
     return valid && r2 > thr;
@@ -504,7 +517,7 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
         float d = 0.f, dp = 0.f, r2 = 0.f;
         const bool ok =
             pair_eval<MODE>(sum(0, 0, i), sum(1, 0, i), sum(0, 1, i), sum(1, 1, i), valid, thr, scale, sc.nonneg != 0,
-                            d, dp, r2);
+                            sc.R, d, dp, r2);
         res[i][0] = d;
         res[i][1] = dp;
         res[i][2] = r2;
@@ -547,7 +560,15 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
         const uint32_t excl = incl - cnt;
         const uint32_t total = __shfl(incl, 63, 64);
         unsigned long long base = 0;
-        if (rr == 63 && total) base = atomicAdd(o.cursor, (unsigned long long)total);
+        if (rr == 63 && total) {
+            base = atomicAdd(o.cursor, (unsigned long long)total);
+            if constexpr (MODE == kModeRefPairs) {  // the tile's slice of candidate rows
+                const unsigned k = atomicAdd(sc.cand_count, 1u);
+                sc.cand_list[3 * k] = (uint32_t)base;
+                sc.cand_list[3 * k + 1] = total;
+                sc.cand_list[3 * k + 2] = (ta << 16) | tb;
+            }
+        }
         base = __shfl(base, 63, 64);
         sRowBase[rr] = (uint32_t)base + excl;
         const uint32_t a = a0 + rr;
@@ -713,8 +734,8 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
                                             sRowBase);
     };
     if constexpr (!LOOP) {
-        if constexpr (MODE == kModeScreen)
-            if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the candidate launch
+        if constexpr (MODE == kModeScreen || MODE == kModeRefPairs)
+            if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
         const uint32_t tile = tiles[blockIdx.x];
         if (tile != kNoTile) compute_tile(tile, threadIdx.x);  // kNoTile: padding of an XCD-ordered list
     } else {
@@ -895,6 +916,21 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     if (!prefilter) {
         launch_lds_planes<kModeAll>(n, m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, idx, o, dn, sc, s);
         return false;
+    }
+    if (m.ref_rows) {
+        // exact candidate pairs (every plane, residual = the reference's
+        // rounding), then each summed alone in lib.rs's order; screen_done
+        // separates the two launches, and the second runs the chunk scan
+        sc.R = m.r_extra_q;
+        launch_lds_planes<kModeRefPairs>(n, m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, idx, o, dn, sc, s);
+        if (screen_done) (void)hipEventRecord(screen_done, s);
+        RefRowsLaunch rr = *m.ref_rows;
+        rr.slices = m.cand_list;
+        rr.slice_count = m.cand_count;
+        rr.work = m.cand_work;
+        rr.scan = m.scan;
+        launch_ref_rows(rr, o, s);
+        return true;
     }
     if (!m.screen) {
         launch_lds_planes<kModePrefilter>(n, m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, idx, o, dn, sc, s);

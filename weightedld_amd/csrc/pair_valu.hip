@@ -487,6 +487,135 @@ __global__ __launch_bounds__(256) void ref_layout_kernel(const uint8_t *__restri
     if (s == 0) rw[p] = seq < N ? w[seq] : 0.0f;
 }
 
+// lib.rs's four sums (lib.rs:416-480) of one pair from the lane-class layout,
+// on 8 lanes as in lib.rs's f32x8 loop: lane c runs class c's chain over its
+// elements in order (adds of selected weights, lib.rs's select + add), then
+// the first lane folds the 8 chains into the ordered horizontal sum and adds
+// the scalar tail onto it.  A 16-position group holds element 4j + g at
+// position 4g + j, so a 16-byte read gives 16 elements, taken in element
+// order from its dwords.  Returns the sums on the pair's first lane.
+__device__ inline void ref_pair_sums8(const RefRowsLaunch &r, uint32_t a, uint32_t b, uint32_t c,
+                                      float (&tot)[4]) {
+    const uint8_t *ra = r.rcodes + (size_t)a * r.NPr, *rb = r.rcodes + (size_t)b * r.NPr;
+    const uint32_t cls = r.ref_cls;
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (uint32_t q0 = c * cls; q0 < (c + 1) * cls; q0 += 16) {
+        const uint4 va = *reinterpret_cast<const uint4 *>(ra + q0);
+        const uint4 vb = *reinterpret_cast<const uint4 *>(rb + q0);
+        const float4 w0 = *reinterpret_cast<const float4 *>(r.rw + q0);
+        const float4 w1 = *reinterpret_cast<const float4 *>(r.rw + q0 + 4);
+        const float4 w2 = *reinterpret_cast<const float4 *>(r.rw + q0 + 8);
+        const float4 w3 = *reinterpret_cast<const float4 *>(r.rw + q0 + 12);
+        const uint32_t A[4] = {va.x, va.y, va.z, va.w}, B[4] = {vb.x, vb.y, vb.z, vb.w};
+        const float W[16] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w,
+                             w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int g = e & 3, j = e >> 2;  // element 4j + g at position 4g + j
+            const uint32_t xa = A[g] >> (8 * j), xb = B[g] >> (8 * j);
+            const float we = W[4 * g + j];
+            const float u = (xa & kCodeIn) ? we : 0.0f, v = (xa & kCodeMaj) ? we : 0.0f;
+            acc[0] += (xb & kCodeIn) ? u : 0.0f;
+            acc[1] += (xb & kCodeIn) ? v : 0.0f;
+            acc[2] += (xb & kCodeMaj) ? u : 0.0f;
+            acc[3] += (xb & kCodeMaj) ? v : 0.0f;
+        }
+    }
+    const int first = (threadIdx.x & 63) & ~7;  // the pair's lane 0
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        float t = 0.0f;
+        for (int k = 0; k < 8; ++k) t += __shfl(acc[q], first + k, 64);  // ((0 + l0) + l1) + ... + l7
+        tot[q] = cls ? t : 0.0f;
+    }
+    if (c != 0) return;
+    for (uint32_t t = 0; t < r.ref_tail_n; ++t) {
+        const uint32_t p = 8 * cls + t;
+        const uint32_t xa = ra[p], xb = rb[p];
+        const float we = r.rw[p];
+        const float u = (xa & kCodeIn) ? we : 0.0f, v = (xa & kCodeMaj) ? we : 0.0f;
+        tot[0] += (xb & kCodeIn) ? u : 0.0f;
+        tot[1] += (xb & kCodeIn) ? v : 0.0f;
+        tot[2] += (xb & kCodeMaj) ? u : 0.0f;
+        tot[3] += (xb & kCodeMaj) ? v : 0.0f;
+    }
+}
+
+// One workgroup per tile slice (the first by id, the next from the work
+// counter), 32 candidate rows at a time, 8 lanes each: lib.rs's sums and
+// epilogue; the passing rows move down in place (a row's new position never
+// exceeds its old one, and every row of a chunk is read before the chunk's
+// writes), so the slice keeps its (a, b) order; then the tile's 64 segment
+// counts/offsets are rewritten and the dropped rows leave its chunk total.
+__global__ __launch_bounds__(256) void ref_rows_kernel(RefRowsLaunch r, OrderArgs o) {
+    __shared__ uint32_t sCnt[kTile], sWave[4], s_next;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, slot = tid >> 3, cl = tid & 7;
+    const uint32_t ns = *r.slice_count;
+    for (uint32_t si = blockIdx.x; si < ns;) {
+        const uint32_t base = r.slices[3 * si], total = r.slices[3 * si + 1], tile = r.slices[3 * si + 2];
+        const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu, a0 = ta * kTile;
+        // a slice past the staging capacity was not stored: the pass re-runs
+        // with more staging (run_complete)
+        const bool stored = (uint64_t)base + total <= o.st_capacity;
+        if (tid < kTile) sCnt[tid] = 0;
+        __syncthreads();
+        uint32_t kept = 0;
+        for (uint32_t c0 = 0; stored && c0 < total; c0 += 32) {
+            const uint32_t i = c0 + slot;
+            bool pass = false;
+            uint32_t a = 0, b = 0;
+            float d = 0.0f, dp = 0.0f, r2 = 0.0f;
+            if (i < total) {  // (uniform over the pair's 8 lanes)
+                a = o.st_a[base + i];
+                b = o.st_b[base + i];
+                float t4[4];
+                ref_pair_sums8(r, a, b, cl, t4);
+                if (cl == 0) {
+                    ld_epilogue(t4[0], t4[1], t4[2], t4[3], d, dp, r2);
+                    pass = r2 > r.thr;  // lib.rs:660 strict '>' (every staged pair is valid)
+                }
+            }
+            const uint64_t bal = __ballot(pass);
+            if (lane == 0) sWave[wv] = (uint32_t)__popcll(bal);
+            __syncthreads();  // (also: this chunk's rows have all been read)
+            uint32_t off = 0, ctot = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                off += k < wv ? sWave[k] : 0u;
+                ctot += sWave[k];
+            }
+            if (pass) {
+                const uint32_t pos = base + kept + off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+                o.st_a[pos] = a;
+                o.st_b[pos] = b;
+                o.st_d[pos] = d;
+                o.st_dp[pos] = dp;
+                o.st_r2[pos] = r2;
+                atomicAdd(&sCnt[a - a0], 1u);
+            }
+            kept += ctot;
+            __syncthreads();
+        }
+        if (stored && tid < kTile) {  // the slice is in (a, b) order: a's rows follow the smaller a's
+            const uint32_t cnt = sCnt[tid], incl = wave_inclusive_scan(cnt);
+            o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = (uint8_t)cnt;
+            o.seg_off[(size_t)(a0 + tid) * o.T + tb] = base + incl - cnt;
+        }
+        if (tid == 0 && stored && kept < total)
+            atomicSub(&o.chunk_total[chunk_linear(r.n_chunk_rows, ta / kTilesPerChunk, tb / kTilesPerChunk)],
+                      total - kept);
+        if (tid == 0) s_next = gridDim.x + atomicAdd(r.work, 1u);
+        __syncthreads();
+        si = s_next;
+        __syncthreads();
+    }
+    scan_tail(r.scan, ns);
+}
+
+void launch_ref_rows(const RefRowsLaunch &r, const OrderArgs &o, hipStream_t s) {
+    hipLaunchKernelGGL(ref_rows_kernel, dim3(kRefRowsGrid), dim3(256), 0, s, r, o);
+}
+
 void ref_layout_dims(size_t N, uint32_t *cls, uint32_t *tail, size_t *NPr) {
     const size_t stages = (N / 8 + 63) / 64;  // 64-sequence stages per lane class (0 when N < 8)
     *cls = (uint32_t)(stages * 64);
