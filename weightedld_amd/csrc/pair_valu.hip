@@ -488,47 +488,57 @@ __global__ __launch_bounds__(256) void ref_layout_kernel(const uint8_t *__restri
 }
 
 // lib.rs's four sums (lib.rs:416-480) of one pair from the lane-class layout,
-// on 8 lanes as in lib.rs's f32x8 loop: lane c runs class c's chain over its
+// on L = 8 lanes as in lib.rs's f32x8 loop (small slices: 8x shorter chains),
+// or all on one lane (L = 1, large slices: no exchange).  Lane c runs class
+// c's chain over its
 // elements in order (adds of selected weights, lib.rs's select + add), then
 // the first lane folds the 8 chains into the ordered horizontal sum and adds
 // the scalar tail onto it.  A 16-position group holds element 4j + g at
 // position 4g + j, so a 16-byte read gives 16 elements, taken in element
 // order from its dwords.  Returns the sums on the pair's first lane.
-__device__ inline void ref_pair_sums8(const RefRowsLaunch &r, uint32_t a, uint32_t b, uint32_t c,
-                                      float (&tot)[4]) {
+template <int LANES>
+__device__ inline void ref_pair_sums(const RefRowsLaunch &r, uint32_t a, uint32_t b, uint32_t c, float (&tot)[4]) {
     const uint8_t *ra = r.rcodes + (size_t)a * r.NPr, *rb = r.rcodes + (size_t)b * r.NPr;
     const uint32_t cls = r.ref_cls;
-    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    for (uint32_t q0 = c * cls; q0 < (c + 1) * cls; q0 += 16) {
-        const uint4 va = *reinterpret_cast<const uint4 *>(ra + q0);
-        const uint4 vb = *reinterpret_cast<const uint4 *>(rb + q0);
-        const float4 w0 = *reinterpret_cast<const float4 *>(r.rw + q0);
-        const float4 w1 = *reinterpret_cast<const float4 *>(r.rw + q0 + 4);
-        const float4 w2 = *reinterpret_cast<const float4 *>(r.rw + q0 + 8);
-        const float4 w3 = *reinterpret_cast<const float4 *>(r.rw + q0 + 12);
-        const uint32_t A[4] = {va.x, va.y, va.z, va.w}, B[4] = {vb.x, vb.y, vb.z, vb.w};
-        const float W[16] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w,
-                             w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
+    tot[0] = tot[1] = tot[2] = tot[3] = 0.0f;
+    for (uint32_t k = (LANES == 8 ? c : 0); k < (LANES == 8 ? c + 1 : (cls ? 8u : 0u)); ++k) {
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (uint32_t q0 = k * cls; q0 < (k + 1) * cls; q0 += 16) {
+            const uint4 va = *reinterpret_cast<const uint4 *>(ra + q0);
+            const uint4 vb = *reinterpret_cast<const uint4 *>(rb + q0);
+            const float4 w0 = *reinterpret_cast<const float4 *>(r.rw + q0);
+            const float4 w1 = *reinterpret_cast<const float4 *>(r.rw + q0 + 4);
+            const float4 w2 = *reinterpret_cast<const float4 *>(r.rw + q0 + 8);
+            const float4 w3 = *reinterpret_cast<const float4 *>(r.rw + q0 + 12);
+            const uint32_t A[4] = {va.x, va.y, va.z, va.w}, B[4] = {vb.x, vb.y, vb.z, vb.w};
+            const float W[16] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w,
+                                 w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int g = e & 3, j = e >> 2;  // element 4j + g at position 4g + j
-            const uint32_t xa = A[g] >> (8 * j), xb = B[g] >> (8 * j);
-            const float we = W[4 * g + j];
-            const float u = (xa & kCodeIn) ? we : 0.0f, v = (xa & kCodeMaj) ? we : 0.0f;
-            acc[0] += (xb & kCodeIn) ? u : 0.0f;
-            acc[1] += (xb & kCodeIn) ? v : 0.0f;
-            acc[2] += (xb & kCodeMaj) ? u : 0.0f;
-            acc[3] += (xb & kCodeMaj) ? v : 0.0f;
+            for (int e = 0; e < 16; ++e) {
+                const int g = e & 3, j = e >> 2;  // element 4j + g at position 4g + j
+                const uint32_t xa = A[g] >> (8 * j), xb = B[g] >> (8 * j);
+                const float we = W[4 * g + j];
+                const float u = (xa & kCodeIn) ? we : 0.0f, v = (xa & kCodeMaj) ? we : 0.0f;
+                acc[0] += (xb & kCodeIn) ? u : 0.0f;
+                acc[1] += (xb & kCodeIn) ? v : 0.0f;
+                acc[2] += (xb & kCodeMaj) ? u : 0.0f;
+                acc[3] += (xb & kCodeMaj) ? v : 0.0f;
+            }
+        }
+        if constexpr (LANES == 8) {
+            const int first = (threadIdx.x & 63) & ~7;  // the pair's lane 0
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float t = 0.0f;
+                for (int j = 0; j < 8; ++j) t += __shfl(acc[q], first + j, 64);  // ((0 + l0) + l1) + ... + l7
+                tot[q] = cls ? t : 0.0f;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) tot[q] += acc[q];  // the same ordered fold, class by class
         }
     }
-    const int first = (threadIdx.x & 63) & ~7;  // the pair's lane 0
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        float t = 0.0f;
-        for (int k = 0; k < 8; ++k) t += __shfl(acc[q], first + k, 64);  // ((0 + l0) + l1) + ... + l7
-        tot[q] = cls ? t : 0.0f;
-    }
-    if (c != 0) return;
+    if (LANES == 8 && c != 0) return;
     for (uint32_t t = 0; t < r.ref_tail_n; ++t) {
         const uint32_t p = 8 * cls + t;
         const uint32_t xa = ra[p], xb = rb[p];
@@ -542,7 +552,8 @@ __device__ inline void ref_pair_sums8(const RefRowsLaunch &r, uint32_t a, uint32
 }
 
 // One workgroup per tile slice (the first by id, the next from the work
-// counter), 32 candidate rows at a time, 8 lanes each: lib.rs's sums and
+// counter), 32 candidate rows at a time on 8 lanes each, or (slices of 128
+// rows or more) 256 at a time on one lane each: lib.rs's sums and
 // epilogue; the passing rows move down in place (a row's new position never
 // exceeds its old one, and every row of a chunk is read before the chunk's
 // writes), so the slice keeps its (a, b) order; then the tile's 64 segment
@@ -560,17 +571,22 @@ __global__ __launch_bounds__(256) void ref_rows_kernel(RefRowsLaunch r, OrderArg
         if (tid < kTile) sCnt[tid] = 0;
         __syncthreads();
         uint32_t kept = 0;
-        for (uint32_t c0 = 0; stored && c0 < total; c0 += 32) {
-            const uint32_t i = c0 + slot;
+        const bool wide = total >= 128;  // uniform
+        const uint32_t per = wide ? 256u : 32u;
+        for (uint32_t c0 = 0; stored && c0 < total; c0 += per) {
+            const uint32_t i = c0 + (wide ? tid : slot);
             bool pass = false;
             uint32_t a = 0, b = 0;
             float d = 0.0f, dp = 0.0f, r2 = 0.0f;
-            if (i < total) {  // (uniform over the pair's 8 lanes)
+            if (i < total) {  // (uniform over a pair's 8 lanes)
                 a = o.st_a[base + i];
                 b = o.st_b[base + i];
                 float t4[4];
-                ref_pair_sums8(r, a, b, cl, t4);
-                if (cl == 0) {
+                if (wide)
+                    ref_pair_sums<1>(r, a, b, 0, t4);
+                else
+                    ref_pair_sums<8>(r, a, b, cl, t4);
+                if (wide || cl == 0) {
                     ld_epilogue(t4[0], t4[1], t4[2], t4[3], d, dp, r2);
                     pass = r2 > r.thr;  // lib.rs:660 strict '>' (every staged pair is valid)
                 }
