@@ -486,7 +486,7 @@ def main():
         dom_ms = screen_ms if screened else kernel_ms
         achieved = alg_ops / (dom_ms * 1e-3) / 1e12
         if screen_kind == 4:
-            kname = "pair_mfma_kernel<exact candidate pairs, %d planes>" % planes
+            kname = "pair_mfma_kernel<candidate pairs, %d planes>" % min(planes, 2)
         elif screened:
             kname = "pair_mfma_kernel<screen,%d plane%s>" % ((2, "s") if screen_kind == 3 else (1, ""))
         else:
@@ -496,7 +496,8 @@ def main():
                 "kernel": kname, "kernel_ms": dom_ms}
         # what the matrix cores executed: P digit planes x 8 N per pair (one
         # or two i8 planes when screened)
-        ex_planes = (2 if screen_kind == 3 else 1) if screened and screen_kind != 4 else planes
+        ex_planes = (2 if screen_kind == 3 else 1) if screened and screen_kind != 4 else \
+            min(planes, 2) if screen_kind == 4 else planes
         roof["executed_frac"] = shard_pairs * 8.0 * ex_planes * N / (dom_ms * 1e-3) / 1e12 / peak
         roof["executed_work"] = "%d i8 digit plane(s) x 8*N ops per pair" % ex_planes
         # against the i8 peak as well (the integer kernels' roofline)
@@ -522,7 +523,7 @@ def main():
         cand_ops = n_cand * 4096 * 8.0 * N
         if screen_kind == 4:  # the per-pair kernel's algorithmic work: 8N per candidate pair
             cand_ops = float(np.mean(cpairs)) * 8.0 * N
-        roof["screen"] = {"kind": {3: "i8 two-plane", 4: "exact candidate pairs (i8, every plane)"}.get(screen_kind, "i8"),
+        roof["screen"] = {"kind": {3: "i8 two-plane", 4: "candidate pairs (i8 pass on the top two digit planes, rigorous bound)"}.get(screen_kind, "i8"),
                           "tiles": n_tiles,
                           "candidate_tiles": n_cand, "candidate_fraction": n_cand / max(n_tiles, 1),
                           "screen_ms": screen_ms, "candidate_launch_ms": cand_ms,
@@ -549,8 +550,9 @@ def main():
     # the arithmetic the timed steps executed
     fixed = "%d-bit fixed-point weights" % (31 if planes == 4 else 23)
     if kern_name == "mfma" and screen_kind == 4:
-        dtype = ("i8 MFMA, %d digit planes of %s, exact i32 sums, rigorous r2 bound with lib.rs's rounding; the "
-                 "%.0f candidate pairs: f32 sums in lib.rs's order, f32 epilogue" % (planes, fixed, float(np.mean(cpairs))))
+        dtype = ("i8 MFMA on the top %d digit plane(s) of %s (i32 sums), rigorous r2 bound with lib.rs's rounding; "
+                 "the %.0f candidate pairs: f32 sums in lib.rs's order, f32 epilogue" % (
+                     min(planes, 2), fixed, float(np.mean(cpairs))))
     elif kern_name == "mfma" and screened:
         dtype = ("i8 MFMA screen on the top weight digit%s (i32 sums, rigorous f32/f64 r2 bound over every pair); "
                  "candidate tiles (%.0f of %d): %s" % (

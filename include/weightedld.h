@@ -170,7 +170,7 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *                      0: every tile, every plane.  In lib.rs's order
  *                      (WLD_OPT_REF_SUMS 1) auto replaces the two-plane tier:
  *                      where the one-plane screen does not pay, every tile runs
- *                      once on all planes, staging the pairs the bound cannot
+ *                      once on the top two digit planes, staging the pairs the bound cannot
  *                      reject (the reference's rounding as residual), and only
  *                      those are summed in lib.rs's order, one by one — unless
  *                      at this or a higher threshold they were more than a
@@ -387,9 +387,9 @@ typedef struct {
     uint64_t candidate_tiles;/* tiles computed with every plane (= tiles unless screened) */
     double screen_ms;        /* HIP-event time of the screen launch (0 if none)    */
     int screened;            /* 1: the last run ran the one-plane i8 screen; 3: the two-plane
-                                i8 screen; 4: (lib.rs's order) the exact i8 pass staging the
-                                pairs its bound cannot reject, each then summed alone in
-                                lib.rs's order; 0: none */
+                                i8 screen; 4: (lib.rs's order) an i8 pass (the top two digit
+                                planes) staging the pairs its bound cannot reject, each then
+                                summed alone in lib.rs's order; 0: none */
     int ref_sums;            /* 1: the last run summed in lib.rs's f32 order (WLD_OPT_REF_SUMS) */
     uint64_t candidate_blocks; /* 16x16 sub-blocks of the candidate tiles holding a pair the screen
                                   could not reject (16 x candidate_tiles unless screened); with

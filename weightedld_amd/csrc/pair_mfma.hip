@@ -364,8 +364,8 @@ __device__ __forceinline__ void zero_acc(Acc16<NPL, NB> &acc) {
 //                  tile with any pair the bound cannot reject is appended to
 //                  the candidate list (recomputed with every plane by the
 //                  kModePrefilter launch), the others write their zero counts
-//   kModeRefPairs  exact sums, then every valid pair r2_bound_skip cannot
-//                  reject with the reference's rounding as residual (sc.R) is
+//   kModeRefPairs  every valid pair r2_bound_skip cannot reject with the
+//                  reference's rounding (plus any omitted planes) as residual (sc.R) is
 //                  staged as a candidate row, and each tile's slice of them
 //                  recorded (sc.cand_list, sc.cand_count): ref_rows_kernel
 //                  (pair_valu.hip) then sums those pairs in lib.rs's order and
@@ -918,11 +918,24 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
         return false;
     }
     if (m.ref_rows) {
-        // exact candidate pairs (every plane, residual = the reference's
-        // rounding), then each summed alone in lib.rs's order; screen_done
-        // separates the two launches, and the second runs the chunk scan
-        sc.R = m.r_extra_q;
-        launch_lds_planes<kModeRefPairs>(n, m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, idx, o, dn, sc, s);
+        // candidate pairs, then each summed alone in lib.rs's order;
+        // screen_done separates the two launches, and the second runs the
+        // chunk scan.  The bound's residual is the reference's rounding
+        // (r_extra_q), which at these thresholds dwarfs what the lowest digit
+        // plane adds (2^-16 of the weights against ~1e-4 at N = 2000): with
+        // three or more active planes the top two suffice (2/3 of the MFMA
+        // work), the planes below bounded by resid as in the two-plane screen;
+        // sums in fixed-point units either way
+        if (n >= 3) {
+            const uint32_t lo = top - 1;
+            sc.R = (double)m.resid[lo - 1] + m.r_extra_q;
+            launch_lds<kModeRefPairs, 2>(m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, lo | (top << 2), o, dn,
+                                          sc, s);
+        } else {
+            sc.R = m.r_extra_q;
+            launch_lds_planes<kModeRefPairs>(n, m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, idx, o, dn, sc,
+                                             s);
+        }
         if (screen_done) (void)hipEventRecord(screen_done, s);
         RefRowsLaunch rr = *m.ref_rows;
         rr.slices = m.cand_list;
