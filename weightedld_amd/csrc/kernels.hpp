@@ -110,11 +110,12 @@ struct ValuLaunch {
     ScanArgs scan;        // tile_count launches: the run's scan fused into the last workgroup (ticket set)
 };
 void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
-// The candidate pairs a kModeRefPairs launch (pair_mfma.hip) staged, summed in
-// lib.rs's order one pair per thread from the lane-class layout; the passing
-// rows are kept in place (in order), their segment counts/offsets and chunk
-// totals corrected, the rest dropped.  The run's chunk scan runs in the last
-// workgroup (scan.ticket).
+// The candidate pairs a kModeRefPairs launch (pair_mfma.hip) staged: summed in
+// lib.rs's order one pair per thread from the lane-class layout
+// (ref_sums_kernel), then per tile slice the passing rows kept in place (in
+// order), its segment counts/offsets and chunk total corrected, the rest
+// dropped (ref_compact_kernel, whose last workgroup runs the run's chunk scan:
+// scan.ticket).
 struct RefRowsLaunch {
     const uint8_t *rcodes;  // the lane-class layout (NPr bytes per site)
     const float *rw;
@@ -156,7 +157,7 @@ constexpr uint32_t kCandidateGrid = 2048;
 // workgroups (three per CU, 256 CUs); extra workgroups would only queue (and
 // cost dispatch time when there is no candidate at all)
 constexpr uint32_t kRefCandidateGrid = 768;
-// ... and of ref_rows_kernel (low-register, latency-bound: eight per CU)
+// ... and of ref_sums_kernel / ref_compact_kernel (low-register: eight per CU)
 constexpr uint32_t kRefRowsGrid = 2048;
 
 struct MfmaLaunch {

@@ -304,12 +304,16 @@ __device__ inline uint32_t cand_entry(const uint32_t *s_pre, uint32_t cap, uint3
 // the last adder told by the returned value; no per-workgroup L2 write-back).
 // The screen before the launch only appended candidates (atomics, before the
 // kernel boundary).
-__device__ inline void scan_tail(const ScanArgs &a, uint32_t n_work) {
+// (all_waves: every wave wrote what the scan reads, and drains before the ticket)
+__device__ inline void scan_tail(const ScanArgs &a, uint32_t n_work, bool all_waves = false) {
     if (!a.ticket) return;
     const uint32_t p = min(gridDim.x, n_work);  // workgroups that computed a tile
     if (blockIdx.x >= max(p, 1u)) return;
     __shared__ unsigned s_run;
-    if (threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's atomics performed
+    if (all_waves || threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // atomics performed
+    // every wave has drained (waves that work independently may still be
+    // writing when wave 0 arrives) before the workgroup takes its ticket
+    if (all_waves) __syncthreads();
     if (threadIdx.x == 0) s_run = p <= 1 || atomicAdd(a.ticket, 1u) == p - 1;
     __syncthreads();
     if (!s_run) return;

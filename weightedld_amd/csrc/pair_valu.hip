@@ -487,60 +487,48 @@ __global__ __launch_bounds__(256) void ref_layout_kernel(const uint8_t *__restri
     if (s == 0) rw[p] = seq < N ? w[seq] : 0.0f;
 }
 
-// lib.rs's four sums (lib.rs:416-480) of one pair from the lane-class layout,
-// on L = 8 lanes as in lib.rs's f32x8 loop (small slices: 8x shorter chains),
-// or all on one lane (L = 1, large slices: no exchange).  Lane c runs class
-// c's chain over its
-// elements in order (adds of selected weights, lib.rs's select + add), then
-// the first lane folds the 8 chains into the ordered horizontal sum and adds
-// the scalar tail onto it.  A 16-position group holds element 4j + g at
-// position 4g + j, so a 16-byte read gives 16 elements, taken in element
-// order from its dwords.  Returns the sums on the pair's first lane.
-template <int LANES>
-__device__ inline void ref_pair_sums(const RefRowsLaunch &r, uint32_t a, uint32_t b, uint32_t c, float (&tot)[4]) {
-    const uint8_t *ra = r.rcodes + (size_t)a * r.NPr, *rb = r.rcodes + (size_t)b * r.NPr;
-    const uint32_t cls = r.ref_cls;
-    tot[0] = tot[1] = tot[2] = tot[3] = 0.0f;
-    for (uint32_t k = (LANES == 8 ? c : 0); k < (LANES == 8 ? c + 1 : (cls ? 8u : 0u)); ++k) {
-        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        for (uint32_t q0 = k * cls; q0 < (k + 1) * cls; q0 += 16) {
-            const uint4 va = *reinterpret_cast<const uint4 *>(ra + q0);
-            const uint4 vb = *reinterpret_cast<const uint4 *>(rb + q0);
-            const float4 w0 = *reinterpret_cast<const float4 *>(r.rw + q0);
-            const float4 w1 = *reinterpret_cast<const float4 *>(r.rw + q0 + 4);
-            const float4 w2 = *reinterpret_cast<const float4 *>(r.rw + q0 + 8);
-            const float4 w3 = *reinterpret_cast<const float4 *>(r.rw + q0 + 12);
-            const uint32_t A[4] = {va.x, va.y, va.z, va.w}, B[4] = {vb.x, vb.y, vb.z, vb.w};
-            const float W[16] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w,
-                                 w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int g = e & 3, j = e >> 2;  // element 4j + g at position 4g + j
-                const uint32_t xa = A[g] >> (8 * j), xb = B[g] >> (8 * j);
-                const float we = W[4 * g + j];
-                const float u = (xa & kCodeIn) ? we : 0.0f, v = (xa & kCodeMaj) ? we : 0.0f;
-                acc[0] += (xb & kCodeIn) ? u : 0.0f;
-                acc[1] += (xb & kCodeIn) ? v : 0.0f;
-                acc[2] += (xb & kCodeMaj) ? u : 0.0f;
-                acc[3] += (xb & kCodeMaj) ? v : 0.0f;
-            }
+// One class chain of lib.rs's four sums (lib.rs:416-480) over positions
+// [q0, q1) of the lane-class layout, in element order: adds of selected
+// weights, lib.rs's select + add.  A 16-position group holds element 4j + g at
+// position 4g + j, so a 16-byte read gives 16 elements, taken in element order
+// from its dwords.  The next group's loads are issued before this group's
+// adds (a chain walks ~2,000 sequences of two random site rows).
+__device__ inline void ref_chain(const uint8_t *ra, const uint8_t *rb, const float *rw, uint32_t q0, uint32_t q1,
+                                 float (&acc)[4]) {
+    if (q0 >= q1) return;
+    uint4 va = *reinterpret_cast<const uint4 *>(ra + q0), vb = *reinterpret_cast<const uint4 *>(rb + q0);
+    float4 w0 = *reinterpret_cast<const float4 *>(rw + q0), w1 = *reinterpret_cast<const float4 *>(rw + q0 + 4);
+    float4 w2 = *reinterpret_cast<const float4 *>(rw + q0 + 8), w3 = *reinterpret_cast<const float4 *>(rw + q0 + 12);
+    for (uint32_t q = q0; q < q1; q += 16) {
+        const uint32_t A[4] = {va.x, va.y, va.z, va.w}, B[4] = {vb.x, vb.y, vb.z, vb.w};
+        const float W[16] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w,
+                             w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
+        if (q + 16 < q1) {
+            va = *reinterpret_cast<const uint4 *>(ra + q + 16);
+            vb = *reinterpret_cast<const uint4 *>(rb + q + 16);
+            w0 = *reinterpret_cast<const float4 *>(rw + q + 16);
+            w1 = *reinterpret_cast<const float4 *>(rw + q + 20);
+            w2 = *reinterpret_cast<const float4 *>(rw + q + 24);
+            w3 = *reinterpret_cast<const float4 *>(rw + q + 28);
         }
-        if constexpr (LANES == 8) {
-            const int first = (threadIdx.x & 63) & ~7;  // the pair's lane 0
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                float t = 0.0f;
-                for (int j = 0; j < 8; ++j) t += __shfl(acc[q], first + j, 64);  // ((0 + l0) + l1) + ... + l7
-                tot[q] = cls ? t : 0.0f;
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) tot[q] += acc[q];  // the same ordered fold, class by class
+        for (int e = 0; e < 16; ++e) {
+            const int g = e & 3, j = e >> 2;  // element 4j + g at position 4g + j
+            const uint32_t xa = A[g] >> (8 * j), xb = B[g] >> (8 * j);
+            const float we = W[4 * g + j];
+            const float u = (xa & kCodeIn) ? we : 0.0f, v = (xa & kCodeMaj) ? we : 0.0f;
+            acc[0] += (xb & kCodeIn) ? u : 0.0f;
+            acc[1] += (xb & kCodeIn) ? v : 0.0f;
+            acc[2] += (xb & kCodeMaj) ? u : 0.0f;
+            acc[3] += (xb & kCodeMaj) ? v : 0.0f;
         }
     }
-    if (LANES == 8 && c != 0) return;
+}
+
+// ... the scalar tail (lib.rs:461-480), added onto the horizontal sums
+__device__ inline void ref_tail(const RefRowsLaunch &r, const uint8_t *ra, const uint8_t *rb, float (&tot)[4]) {
     for (uint32_t t = 0; t < r.ref_tail_n; ++t) {
-        const uint32_t p = 8 * cls + t;
+        const uint32_t p = 8 * r.ref_cls + t;
         const uint32_t xa = ra[p], xb = rb[p];
         const float we = r.rw[p];
         const float u = (xa & kCodeIn) ? we : 0.0f, v = (xa & kCodeMaj) ? we : 0.0f;
@@ -551,85 +539,113 @@ __device__ inline void ref_pair_sums(const RefRowsLaunch &r, uint32_t a, uint32_
     }
 }
 
-// One workgroup per tile slice (the first by id, the next from the work
-// counter), 32 candidate rows at a time on 8 lanes each, or (slices of 128
-// rows or more) 256 at a time on one lane each: lib.rs's sums and
-// epilogue; the passing rows move down in place (a row's new position never
-// exceeds its old one, and every row of a chunk is read before the chunk's
-// writes), so the slice keeps its (a, b) order; then the tile's 64 segment
-// counts/offsets are rewritten and the dropped rows leave its chunk total.
-__global__ __launch_bounds__(256) void ref_rows_kernel(RefRowsLaunch r, OrderArgs o) {
-    __shared__ uint32_t sCnt[kTile], sWave[4], s_next;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, slot = tid >> 3, cl = tid & 7;
+// Every staged candidate row (the staging cursor the candidate pass left):
+// lib.rs's sums and epilogue, the values written back into the row's staging
+// slot; whether it passes (r2 > thr) is read back from that r2 by
+// ref_compact_kernel.  Up to an eighth of the grid's threads in rows, each
+// row on 8 lanes, one class chain each, folded in order ((((0 + l0) + l1) +
+// ...) + l7) with shuffles (8x shorter chains); more rows, one lane per row
+// walking the 8 chains (no exchange), grid-stride.
+__global__ __launch_bounds__(256) void ref_sums_kernel(RefRowsLaunch r, OrderArgs o) {
+    const uint64_t n = min((uint64_t)*o.cursor, o.st_capacity);  // (an overflowing pass re-runs)
+    const uint64_t threads = (uint64_t)gridDim.x * 256, gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t cls = r.ref_cls;
+    if (n * 8 <= threads) {
+        const uint64_t i = gid >> 3;
+        if (i >= n) return;  // (a row's 8 lanes leave together)
+        const uint32_t c = (uint32_t)(gid & 7);
+        const uint8_t *ra = r.rcodes + (size_t)o.st_a[i] * r.NPr, *rb = r.rcodes + (size_t)o.st_b[i] * r.NPr;
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f}, tot[4];
+        ref_chain(ra, rb, r.rw, c * cls, (c + 1) * cls, acc);
+        const int first = (int)(threadIdx.x & 63) & ~7;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float t = 0.0f;
+            for (int k = 0; k < 8; ++k) t += __shfl(acc[q], first + k, 64);
+            tot[q] = cls ? t : 0.0f;
+        }
+        if (c != 0) return;
+        ref_tail(r, ra, rb, tot);
+        float d, dp, r2;
+        ld_epilogue(tot[0], tot[1], tot[2], tot[3], d, dp, r2);
+        o.st_d[i] = d;
+        o.st_dp[i] = dp;
+        o.st_r2[i] = r2;
+        return;
+    }
+    for (uint64_t i = gid; i < n; i += threads) {
+        const uint8_t *ra = r.rcodes + (size_t)o.st_a[i] * r.NPr, *rb = r.rcodes + (size_t)o.st_b[i] * r.NPr;
+        float tot[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (uint32_t k = 0; k < (cls ? 8u : 0u); ++k) {
+            float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            ref_chain(ra, rb, r.rw, k * cls, (k + 1) * cls, acc);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) tot[q] += acc[q];
+        }
+        ref_tail(r, ra, rb, tot);
+        float d, dp, r2;
+        ld_epilogue(tot[0], tot[1], tot[2], tot[3], d, dp, r2);
+        o.st_d[i] = d;
+        o.st_dp[i] = dp;
+        o.st_r2[i] = r2;
+    }
+}
+
+// One wave per tile slice (the first by workgroup and wave id, the next from
+// the work counter): the rows with r2 > thr (lib.rs:660, strict; every staged
+// pair is valid) move down in place, 64 at a time — a row's new position
+// never exceeds its old one and a batch is read before it is written — so
+// the slice keeps its (a, b) order; then the tile's 64 segment counts/offsets
+// are rewritten and the dropped rows leave its chunk total.  The run's chunk
+// scan runs in the last workgroup.
+__global__ __launch_bounds__(256) void ref_compact_kernel(RefRowsLaunch r, OrderArgs o) {
+    __shared__ uint32_t sCnt[4][kTile];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t *cnt = sCnt[wv];
     const uint32_t ns = *r.slice_count;
-    for (uint32_t si = blockIdx.x; si < ns;) {
+    for (uint32_t si = 4 * blockIdx.x + wv; si < ns;) {
         const uint32_t base = r.slices[3 * si], total = r.slices[3 * si + 1], tile = r.slices[3 * si + 2];
         const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu, a0 = ta * kTile;
-        // a slice past the staging capacity was not stored: the pass re-runs
-        // with more staging (run_complete)
-        const bool stored = (uint64_t)base + total <= o.st_capacity;
-        if (tid < kTile) sCnt[tid] = 0;
-        __syncthreads();
-        uint32_t kept = 0;
-        const bool wide = total >= 128;  // uniform
-        const uint32_t per = wide ? 256u : 32u;
-        for (uint32_t c0 = 0; stored && c0 < total; c0 += per) {
-            const uint32_t i = c0 + (wide ? tid : slot);
-            bool pass = false;
-            uint32_t a = 0, b = 0;
-            float d = 0.0f, dp = 0.0f, r2 = 0.0f;
-            if (i < total) {  // (uniform over a pair's 8 lanes)
-                a = o.st_a[base + i];
-                b = o.st_b[base + i];
-                float t4[4];
-                if (wide)
-                    ref_pair_sums<1>(r, a, b, 0, t4);
-                else
-                    ref_pair_sums<8>(r, a, b, cl, t4);
-                if (wide || cl == 0) {
-                    ld_epilogue(t4[0], t4[1], t4[2], t4[3], d, dp, r2);
-                    pass = r2 > r.thr;  // lib.rs:660 strict '>' (every staged pair is valid)
+        if ((uint64_t)base + total <= o.st_capacity) {  // else not stored: the pass re-runs
+            cnt[lane] = 0;
+            uint32_t kept = 0;
+            for (uint32_t c0 = 0; c0 < total; c0 += 64) {
+                const uint32_t i = base + c0 + lane;
+                const bool in = c0 + lane < total;
+                const uint32_t a = in ? o.st_a[i] : 0u, b = in ? o.st_b[i] : 0u;
+                const float d = in ? o.st_d[i] : 0.0f, dp = in ? o.st_dp[i] : 0.0f, r2 = in ? o.st_r2[i] : 0.0f;
+                const bool pass = in && r2 > r.thr;
+                const uint64_t bal = __ballot(pass);
+                if (pass) {
+                    const uint32_t pos = base + kept + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+                    o.st_a[pos] = a;
+                    o.st_b[pos] = b;
+                    o.st_d[pos] = d;
+                    o.st_dp[pos] = dp;
+                    o.st_r2[pos] = r2;
+                    atomicAdd(&cnt[a - a0], 1u);
                 }
+                kept += (uint32_t)__popcll(bal);
             }
-            const uint64_t bal = __ballot(pass);
-            if (lane == 0) sWave[wv] = (uint32_t)__popcll(bal);
-            __syncthreads();  // (also: this chunk's rows have all been read)
-            uint32_t off = 0, ctot = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                off += k < wv ? sWave[k] : 0u;
-                ctot += sWave[k];
-            }
-            if (pass) {
-                const uint32_t pos = base + kept + off + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-                o.st_a[pos] = a;
-                o.st_b[pos] = b;
-                o.st_d[pos] = d;
-                o.st_dp[pos] = dp;
-                o.st_r2[pos] = r2;
-                atomicAdd(&sCnt[a - a0], 1u);
-            }
-            kept += ctot;
-            __syncthreads();
+            // the slice is in (a, b) order: a's rows follow the smaller a's
+            const uint32_t c = cnt[lane], incl = wave_inclusive_scan(c);
+            o.seg_cnt[(size_t)(a0 + lane) * o.T + tb] = (uint8_t)c;
+            o.seg_off[(size_t)(a0 + lane) * o.T + tb] = base + incl - c;
+            if (lane == 0 && kept < total)
+                atomicSub(&o.chunk_total[chunk_linear(r.n_chunk_rows, ta / kTilesPerChunk, tb / kTilesPerChunk)],
+                          total - kept);
         }
-        if (stored && tid < kTile) {  // the slice is in (a, b) order: a's rows follow the smaller a's
-            const uint32_t cnt = sCnt[tid], incl = wave_inclusive_scan(cnt);
-            o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = (uint8_t)cnt;
-            o.seg_off[(size_t)(a0 + tid) * o.T + tb] = base + incl - cnt;
-        }
-        if (tid == 0 && stored && kept < total)
-            atomicSub(&o.chunk_total[chunk_linear(r.n_chunk_rows, ta / kTilesPerChunk, tb / kTilesPerChunk)],
-                      total - kept);
-        if (tid == 0) s_next = gridDim.x + atomicAdd(r.work, 1u);
-        __syncthreads();
-        si = s_next;
-        __syncthreads();
+        uint32_t next = 0;
+        if (lane == 0) next = 4 * gridDim.x + atomicAdd(r.work, 1u);
+        si = __shfl(next, 0, 64);
     }
-    scan_tail(r.scan, ns);
+    // every wave's atomics (chunk totals) are drained before the ticket
+    scan_tail(r.scan, (ns + 3) / 4, true);
 }
 
 void launch_ref_rows(const RefRowsLaunch &r, const OrderArgs &o, hipStream_t s) {
-    hipLaunchKernelGGL(ref_rows_kernel, dim3(kRefRowsGrid), dim3(256), 0, s, r, o);
+    hipLaunchKernelGGL(ref_sums_kernel, dim3(kRefRowsGrid), dim3(256), 0, s, r, o);
+    hipLaunchKernelGGL(ref_compact_kernel, dim3(kRefRowsGrid), dim3(256), 0, s, r, o);
 }
 
 void ref_layout_dims(size_t N, uint32_t *cls, uint32_t *tail, size_t *NPr) {
