@@ -511,16 +511,29 @@ __device__ inline void ref_chain(const uint8_t *ra, const uint8_t *rb, const flo
             w2 = *reinterpret_cast<const float4 *>(rw + q + 24);
             w3 = *reinterpret_cast<const float4 *>(rw + q + 28);
         }
+        // per dword: the "in" and "major" bits of its 4 bytes as 0/1 bytes,
+        // each turned into 0.0/1.0 by a byte convert; u = in_a w, v = maj_a w
+        // (exact), then fmaf(u, f_b, acc) = acc + u f_b rounded once, as
+        // lib.rs's select + add (finite weights: this path follows the i8
+        // pass, which needs them)
+        uint32_t ai[4], am[4], bi[4], bm[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            ai[g] = A[g] & 0x01010101u;
+            am[g] = (A[g] >> 1) & 0x01010101u;
+            bi[g] = B[g] & 0x01010101u;
+            bm[g] = (B[g] >> 1) & 0x01010101u;
+        }
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const int g = e & 3, j = e >> 2;  // element 4j + g at position 4g + j
-            const uint32_t xa = A[g] >> (8 * j), xb = B[g] >> (8 * j);
             const float we = W[4 * g + j];
-            const float u = (xa & kCodeIn) ? we : 0.0f, v = (xa & kCodeMaj) ? we : 0.0f;
-            acc[0] += (xb & kCodeIn) ? u : 0.0f;
-            acc[1] += (xb & kCodeIn) ? v : 0.0f;
-            acc[2] += (xb & kCodeMaj) ? u : 0.0f;
-            acc[3] += (xb & kCodeMaj) ? v : 0.0f;
+            const float u = (float)((ai[g] >> (8 * j)) & 0xFFu) * we, v = (float)((am[g] >> (8 * j)) & 0xFFu) * we;
+            const float fi = (float)((bi[g] >> (8 * j)) & 0xFFu), fm = (float)((bm[g] >> (8 * j)) & 0xFFu);
+            acc[0] = __builtin_fmaf(u, fi, acc[0]);
+            acc[1] = __builtin_fmaf(v, fi, acc[1]);
+            acc[2] = __builtin_fmaf(u, fm, acc[2]);
+            acc[3] = __builtin_fmaf(v, fm, acc[3]);
         }
     }
 }
@@ -591,10 +604,10 @@ __global__ __launch_bounds__(256) void ref_sums_kernel(RefRowsLaunch r, OrderArg
     }
 }
 
-// One wave per tile slice (the first by workgroup and wave id, the next from
-// the work counter): the rows with r2 > thr (lib.rs:660, strict; every staged
-// pair is valid) move down in place, 64 at a time — a row's new position
-// never exceeds its old one and a batch is read before it is written — so
+// One wave per tile slice (wave-strided over the slices): the rows with r2 >
+// thr (lib.rs:660, strict; every staged pair is valid) move down in place,
+// 64 at a time — a row's new position never exceeds its old one and a batch
+// is read before it is written — so
 // the slice keeps its (a, b) order; then the tile's 64 segment counts/offsets
 // are rewritten and the dropped rows leave its chunk total.  The run's chunk
 // scan runs in the last workgroup.
@@ -635,9 +648,7 @@ __global__ __launch_bounds__(256) void ref_compact_kernel(RefRowsLaunch r, Order
                 atomicSub(&o.chunk_total[chunk_linear(r.n_chunk_rows, ta / kTilesPerChunk, tb / kTilesPerChunk)],
                           total - kept);
         }
-        uint32_t next = 0;
-        if (lane == 0) next = 4 * gridDim.x + atomicAdd(r.work, 1u);
-        si = __shfl(next, 0, 64);
+        si += 4 * gridDim.x;  // (static: tens of thousands of small slices would queue on one work counter)
     }
     // every wave's atomics (chunk totals) are drained before the ticket
     scan_tail(r.scan, (ns + 3) / 4, true);
