@@ -376,3 +376,28 @@ def test_ref_pairs_staging_regrow(W):
     n = ctx.run(0.003)
     assert ctx.stats()["screened"] == 4 and n > 64
     assert_rows_bit_exact(ctx.rows(), O.all_pairs(buf, w, np.float32(0.003)))
+
+
+def test_modes_and_tiers_on_one_context(W):
+    # One context switched between lib.rs's order and the exact mode and across
+    # every tier (screen + candidate tiles, candidate pairs, full kernel, the
+    # two-plane screen of the exact mode): lib.rs-order rows bit-identical to
+    # the oracle each time, exact-mode rows the same set with values within
+    # 1e-5 (or closer to the f64 truth), no state leaking between runs.
+    from test_gpu_parity import compare_rows
+    buf = ld_blocks(1200, 301, 11)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ctx = W.Context(0, W.KERNEL_AUTO)
+    ctx.load(buf, w)
+    plan = [(1, 1, 0.05), (1, 4, 0.003), (0, 1, 0.003), (1, 1, 0.003), (0, 3, 0.01), (1, 0, 0.05),
+            (1, 2, 0.02), (0, 1, 0.05), (1, 1, 0.0), (1, 4, 0.05)]
+    for ref_sums, screen, thr in plan:
+        ctx.set_option("ref_sums", ref_sums)
+        ctx.set_option("screen", screen)
+        n = ctx.run(thr)
+        ref = O.all_pairs(buf, w, np.float32(thr))
+        if ref_sums:
+            assert_rows_bit_exact(ctx.rows(), ref)
+        else:
+            compare_rows(ctx.rows(), ref, np.float32(thr), buf=buf, w=w)
+        assert n == len(ctx.rows())
