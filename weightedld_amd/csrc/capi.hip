@@ -970,9 +970,13 @@ int enqueue_pass(wld_ctx *c) {
     c->h_cnt[2] = c->h_cnt[3] = 0;
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     c->screened = c->screened2 = false;
-    if (c->n_tiles) WLD_TRY(launch_pairs(c, r.thr, o, nullptr, &c->screened, lin_count ? &sa : nullptr));
+    // the scan is fused into the launch after a screen for ranges up to 4096
+    // chunks (C4: 3,160, ~10 us in one 256-thread workgroup); a larger range
+    // (C5: 19,306 chunks, ~70 us fused) gets the 1024-thread scan kernel
+    const bool fuse_scan = lin_count && lin_count <= 4096;
+    if (c->n_tiles) WLD_TRY(launch_pairs(c, r.thr, o, nullptr, &c->screened, fuse_scan ? &sa : nullptr));
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-    if (lin_count && !c->screened) {  // after a screen the candidate launch's last workgroup ran it
+    if (lin_count && !(c->screened && fuse_scan)) {  // else the candidate launch's last workgroup ran it
         sa.ticket = nullptr;
         launch_chunk_scan(sa, c->stream);
         HIP_TRY(hipGetLastError());
