@@ -1,0 +1,74 @@
+"""bench.py's contract: the synthetic inputs (CPU) and the one JSON line a
+short default run prints (GPU, run as a child process exactly as the driver
+runs it)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+
+def test_synth_distribution_and_seed():
+    """bench_weighted_pair_ld.rs:8-28's distribution: '-' 0.10, major 0.60,
+    minor 0.30, per site a major != minor from ACGT; seeded."""
+    a = bench.synth(300, 2000)
+    assert a.shape == (300, 2000) and a.dtype == np.uint8
+    assert np.array_equal(a, bench.synth(300, 2000))
+    gap = (a == 4).mean()
+    assert abs(gap - 0.10) < 0.005
+    for s in range(0, 300, 37):
+        row = a[s][a[s] != 4]
+        vals, cnt = np.unique(row, return_counts=True)
+        assert len(vals) == 2 and vals.max() < 4
+        assert abs(cnt.max() / len(row) - 2 / 3) < 0.05  # major 0.6 of 0.9
+
+
+def test_ld_blocks_and_vcf_like_shapes():
+    b = bench.ld_blocks(500, 300)
+    assert b.shape == (500, 300) and np.array_equal(b, bench.ld_blocks(500, 300))
+    assert set(np.unique(b)) <= {0, 1, 2, 3, 4}
+    v = bench.vcf_like(200, n_hap=64)
+    assert v.shape == (200, 64) and set(np.unique(v)) <= {0, 1, 4}
+
+
+def test_pairs_in_rows_partition():
+    """Row-block pair counts add up to L(L-1)/2 (the shard balance uses them)."""
+    L = 20000
+    blocks = (L + 255) // 256
+    total = sum(bench.pairs_in_rows(L, r, r + 1) for r in range(blocks))
+    assert total == L * (L - 1) // 2
+    assert bench.pairs_in_rows(L, 0, blocks) == total
+
+
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+            "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
+
+
+@pytest.mark.gpu
+def test_bench_json_line():
+    """A short default-config run: one JSON line with the driver's keys, the
+    roofline object, rows equal to the oracle's (bench asserts it)."""
+    env = dict(os.environ)
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "5", "--warmup", "2", "--cpu-seconds", "2"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert REQUIRED <= set(out), sorted(REQUIRED - set(out))
+    assert out["metric"] == bench.METRIC and out["n_gpus"] == 1 and out["steps"] == 5 and out["warmup"] == 2
+    assert out["higher_is_better"] is True and out["value"] > 0 and out["ms_per_step"] > 0
+    n_pairs = 20000 * 19999 // 2
+    assert abs(out["value"] * out["ms_per_step"] / 1e3 / n_pairs - 1) < 0.01
+    rf = out["roofline"]
+    assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(rf)
+    assert 0 < rf["frac"] < 1 and abs(rf["achieved"] / rf["peak"] - rf["frac"]) < 1e-3
+    cb = out["cpu_baseline"]
+    assert cb["kind"] in ("port", "reference") and cb["value"] > 0 and cb["cores"] >= 1
+    assert out["config"]["workload"]
