@@ -758,141 +758,6 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
     }
 }
 
-// One-plane screen with two waves per 64x64 tile, each 32 a rows x 64 b
-// columns (RB = 2 row blocks x NB = 4 column blocks of 16x16): per 64
-// sequences a wave issues 32 MFMAs against 16 v_perm (A side, two row
-// blocks) and 16 v_and (B side, shared by both row blocks), 1.0 vector
-// instruction per MFMA instead of 1.5 with 16-row waves, at 2 waves per SIMD
-// (128 accumulators).  Same fragments, stages, DMA protocol and epilogue as
-// pair_mfma_kernel<kModeScreen, 1>.
-template <int RB, int NB>
-struct AccW {
-    static constexpr int kPlanes = 1;
-    static constexpr int kPairs = 4 * NB * RB;
-    v4i v[RB][NB][2][2];  // [row block][column block][channel_a][X, Y]
-    __device__ __forceinline__ int get(int x, int, int y, int i) const {
-        const int X = v[i / (4 * NB)][(i >> 2) % NB][x][0][i & 3], Y = v[i / (4 * NB)][(i >> 2) % NB][x][1][i & 3];
-        return (y ? X - Y : X + Y) >> 1;
-    }
-    __device__ __forceinline__ int2 raw(int x, int i) const {
-        return make_int2(v[i / (4 * NB)][(i >> 2) % NB][x][0][i & 3], v[i / (4 * NB)][(i >> 2) % NB][x][1][i & 3]);
-    }
-    static __device__ __forceinline__ uint32_t a_local(int i, uint32_t wave, uint32_t lane) {
-        return 16 * (RB * wave + i / (4 * NB)) + 4 * (lane >> 4) + (i & 3);
-    }
-    static __device__ __forceinline__ uint32_t b_local(int i, uint32_t, uint32_t lane) {
-        return 16 * ((i >> 2) % NB) + (lane & 15);
-    }
-};
-
-#ifndef WLD_SCRW_STAGES
-#define WLD_SCRW_STAGES 4
-#endif
-#ifndef WLD_SCRW_WPE
-#define WLD_SCRW_WPE 2  // waves per SIMD
-#endif
-constexpr int kScrWStages = WLD_SCRW_STAGES;  // 32-sequence stages per LDS group (even)
-constexpr int kScrWBytes = kScrWStages * kStageCodes + kDigGroup;
-
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WLD_SCRW_WPE, WLD_SCRW_WPE))) void pair_screen_wide_kernel(
-    const uint8_t *__restrict__ frag, const uint8_t *__restrict__ frag_b, const int8_t *__restrict__ planes,
-    const uint64_t *__restrict__ ok_bits, const uint32_t *__restrict__ tiles, uint32_t L, uint32_t NP,
-    uint32_t n_chunk_rows, float thr, int shift, uint32_t top, OrderArgs o, ScreenArgs sc) {
-    constexpr int KG = kScrWStages, KGB = kScrWBytes, RB = 2, NB = 4;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * KGB];
-    __shared__ unsigned long long sBits[kTile];
-    __shared__ uint32_t sRowBase[kTile];
-    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the candidate launch
-    const uint32_t tile = tiles[blockIdx.x];
-    if (tile == kNoTile) return;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const uint32_t NKB = NP / 32;
-    const uint32_t n_groups = (NKB + KG - 1) / KG;
-    const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
-    // wave w copies code blocks A_w (selector copy, a sites 32w..) and B_w
-    // (0/1/2 copy, b sites 32w..) of every stage; wave 0 also the digits
-    const uint8_t *srcA = frag + (size_t)(2 * ta + wave) * NKB * 1024;
-    const uint8_t *srcB = frag_b + (size_t)(2 * tb + wave) * NKB * 1024;
-    const int8_t *digf = planes + digf_offset(NP);
-    const uint32_t smem_lds = lds_addr(smem);
-    auto issue = [&](uint32_t grp, uint32_t buf) {
-        const uint32_t gb = smem_lds + buf * KGB;
-        const uint32_t kb0 = grp * KG;
-        const uint32_t lane16 = lane * 16;
-#pragma unroll
-        for (int st = 0; st < KG; ++st)
-            if (kb0 + st < NKB) {
-                glds16_s(srcA + (size_t)(kb0 + st) * 1024, lane16, gb + st * kStageCodes + wave * 1024);
-                glds16_s(srcB + (size_t)(kb0 + st) * 1024, lane16, gb + st * kStageCodes + (2 + wave) * 1024);
-            }
-        if (wave == 0) glds16_s(digf + digf_stage(kb0), lane16, gb + KG * kStageCodes);
-    };
-    issue(0, 0);
-    const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
-    const uint32_t g4 = lane >> 4, so = g4 >> 1, hh = g4 & 1;
-    const uint32_t lrow = so * kStageCodes + (32 * hh + (lane & 15)) * 16;
-    const uint32_t offA = lrow + wave * 1024;  // + r * 256: row block r of the wave's 32 a sites
-    const uint32_t offB = lrow + 2048;         // + (n >> 1) * 1024 + (n & 1) * 256
-    const uint32_t offP = KG * kStageCodes + so * kDigStage + hh * 16 + 32 * top;
-
-    AccW<RB, NB> acc;
-#pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-        for (int n = 0; n < NB; ++n)
-#pragma unroll
-            for (int x = 0; x < 2; ++x)
-#pragma unroll
-                for (int y = 0; y < 2; ++y) acc.v[r][n][x][y] = v4i{0, 0, 0, 0};
-    constexpr unsigned kOnes = 0x01010101u;
-    uint32_t buf = 0;
-    for (uint32_t grp = 0; grp < n_groups; ++grp) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (grp + 1 < n_groups) issue(grp + 1, buf ^ 1);
-        const uint8_t *gb = smem + buf * KGB;
-        const uint32_t n_st = min((uint32_t)KG, NKB - grp * KG);
-        for (uint32_t st = 0; st < n_st; st += 2) {
-            const uint8_t *sc_ = gb + st * kStageCodes;
-            // A operands of both row blocks first (16 v_perm), then per
-            // column block its raw bytes, minor bits (4 v_and) and 8 MFMAs
-            const v4i dp = *reinterpret_cast<const v4i *>(gb + st * kDigStage + offP);
-            v4i ai[RB], am[RB];
-#pragma unroll
-            for (int r = 0; r < RB; ++r) {
-                const v4i ca = *reinterpret_cast<const v4i *>(sc_ + offA + r * 256);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    ai[r][e] = (int)__builtin_amdgcn_perm((unsigned)dp[e], (unsigned)dp[e], (unsigned)ca[e]);
-                    am[r][e] = (int)__builtin_amdgcn_perm((unsigned)dp[e], 0u, (unsigned)ca[e]);
-                }
-            }
-#pragma unroll
-            for (int n = 0; n < NB; ++n) {
-                const v4i cb = *reinterpret_cast<const v4i *>(sc_ + offB + (n >> 1) * 1024 + (n & 1) * 256);
-                v4i bm;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) bm[e] = cb[e] & (int)kOnes;
-#pragma unroll
-                for (int r = 0; r < RB; ++r) {
-                    acc.v[r][n][0][0] = mfma_i8_16(ai[r], cb, acc.v[r][n][0][0]);
-                    acc.v[r][n][0][1] = mfma_i8_16(ai[r], bm, acc.v[r][n][0][1]);
-                    acc.v[r][n][1][0] = mfma_i8_16(am[r], cb, acc.v[r][n][1][0]);
-                    acc.v[r][n][1][1] = mfma_i8_16(am[r], bm, acc.v[r][n][1][1]);
-                }
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        buf ^= 1;
-    }
-    auto sum = [&](int x, int y, int i) { return acc.get(x, 0, y, i); };
-    const DenseArgs dn{nullptr, nullptr, nullptr, nullptr};
-    tile_epilogue<kModeScreen, AccW<RB, NB>>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, shift, o, dn, sc,
-                                             sBits, sRowBase);
-}
-
 // Site-major variant (one tile per workgroup, codes read straight into
 // registers, all three digit planes): the reference for the LDS path's race
 // screen (WLD_OPT_MFMA_LAYOUT).
@@ -1116,12 +981,7 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     sc.f32 = m.nonneg ? (m.NP <= kScrF32MaxNP ? 2 : m.NP <= kScreenF32MaxNP ? 1 : 0) : 0;
     // every doubled one-plane T <= 2 sum_k |d_top,k| <= 256 NP <= 2^22 (exact in f32)
     if (sc.f32 == 2) screen_consts((float)(2 * m.dsum[top]), 2.0f * sc.Rf, sc.E, sc.mloc);
-#ifdef WLD_SCR_WIDE
-    hipLaunchKernelGGL(pair_screen_wide_kernel, dim3(m.n_tiles), dim3(128), 0, s, m.frag, m.frag_b, m.wplanes, ok_bits,
-                       m.tiles, m.L, m.NP, m.n_chunk_rows, m.thr, m.shift, top, o, sc);
-#else
     launch_lds<kModeScreen, 1>(m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, top, o, dn, sc, s);
-#endif
     if (screen_done) (void)hipEventRecord(screen_done, s);
     launch_candidates(m, n, idx, ok_bits, o, dn, sc, s);
     return true;
