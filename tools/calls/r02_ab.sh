@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of experimental builds at C4 (Henikoff and unit weights) + the screen tests on the variant.
-#   tools/r02_ab.sh TAG VARIANT...   (build/exp/VARIANT/libweightedld.so)
+#   tools/calls/r02_ab.sh TAG VARIANT...   (build/exp/VARIANT/libweightedld.so)
 tag=$1; shift
 out=gpurun_out/$tag; mkdir -p $out
 builds="base=weightedld_amd/libweightedld.so"

@@ -2,7 +2,7 @@
 # One GPU call for the round-2 measurements of the committed tree:
 # GPU tests, bench lines (C4 pipelined + not, C2, C5, unweighted, wide weights,
 # f32 fallback) and the rocprofv3 kernel trace/stats of the non-pipelined C4 bench.
-#   tools/r02_measure.sh TAG   -> gpurun_out/TAG/...
+#   tools/calls/r02_measure.sh TAG   -> gpurun_out/TAG/...
 out=gpurun_out/${1:-r02m}
 mkdir -p $out
 export TMPDIR=/tmp

@@ -1,6 +1,6 @@
 #!/bin/bash
 # The -m gpu suite (or the given test files) on the GPU box, one call.
-#   tools/r03_tests.sh TAG [pytest args...]   -> gpurun_out/TAG/gpu_tests.txt
+#   tools/calls/r03_tests.sh TAG [pytest args...]   -> gpurun_out/TAG/gpu_tests.txt
 tag=${1:-r03t}; shift
 out=gpurun_out/$tag
 mkdir -p $out
