@@ -220,8 +220,21 @@ __device__ inline void chunk_scan_block(const ScanArgs &a) {
     const uint32_t per = (a.count + nth - 1) / nth;
     const uint32_t lo = min(a.count, tid * per), hi = min(a.count, lo + per);
     uint32_t *ct = a.chunk_total + a.lin_begin;
+    // up to kScanRegs totals per thread (every run up to 16 x 256 chunks on a
+    // 256-thread workgroup) are loaded at once, all in flight together, and
+    // kept in registers for the second pass; longer runs loop
+    constexpr uint32_t kScanRegs = 16;
+    const bool in_regs = per <= kScanRegs;
+    uint32_t vals[kScanRegs];
     unsigned long long s = 0;
-    for (uint32_t i = lo; i < hi; ++i) s += ld32(ct + i);
+    if (in_regs) {
+#pragma unroll
+        for (uint32_t j = 0; j < kScanRegs; ++j) vals[j] = lo + j < hi ? ld32(ct + lo + j) : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < kScanRegs; ++j) s += vals[j];
+    } else {
+        for (uint32_t i = lo; i < hi; ++i) s += ld32(ct + i);
+    }
     const int lane = tid & 63, wv = tid >> 6;
     unsigned long long v = s;
 #pragma unroll
@@ -260,6 +273,16 @@ __device__ inline void chunk_scan_block(const ScanArgs &a) {
     }
     __syncthreads();
     unsigned long long base = sw[wv] + v - s;
+    if (in_regs) {
+#pragma unroll
+        for (uint32_t j = 0; j < kScanRegs; ++j)
+            if (lo + j < hi) {
+                ct[lo + j] = 0;
+                a.chunk_base[lo + j] = (uint32_t)base;
+                base += vals[j];
+            }
+        return;
+    }
     for (uint32_t i = lo; i < hi; ++i) {
         const uint32_t t = ld32(ct + i);
         ct[i] = 0;

@@ -742,7 +742,7 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
         // the first tile by workgroup id, the next ones from the work counter
         __shared__ uint32_t s_next, s_pre[17];
         const uint32_t nt = *tile_count;
-        cand_prefix(sc.cand_buckets, s_pre);
+        if (blockIdx.x < nt) cand_prefix(sc.cand_buckets, s_pre);  // (a workgroup without a tile skips it)
         for (uint32_t bi = blockIdx.x; bi < nt;) {
             // the thread id laundered per tile: nothing lane-derived is hoisted
             // out of the loop and held live across the epilogue

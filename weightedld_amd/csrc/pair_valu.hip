@@ -448,7 +448,7 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
         // sub-blocks)
         __shared__ uint32_t s_next, s_pre[17];
         const uint32_t nt = *tile_count;
-        if (tile_buckets) cand_prefix(tile_buckets, s_pre);
+        if (tile_buckets && blockIdx.x < nt) cand_prefix(tile_buckets, s_pre);  // (a workgroup without a tile skips it)
         for (uint32_t bi = blockIdx.x; bi < nt;) {
             const uint32_t e = tile_buckets ? cand_entry(s_pre, bucket_cap, bi) : bi;
             compute_tile(tiles[e], threadIdx.x, tile_bits ? tile_bits[e] : 0xFFFFu);
