@@ -448,8 +448,21 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
         // sub-blocks)
         __shared__ uint32_t s_next, s_pre[17];
         const uint32_t nt = *tile_count;
-        if (tile_buckets && blockIdx.x < nt) cand_prefix(tile_buckets, s_pre);  // (a workgroup without a tile skips it)
-        for (uint32_t bi = blockIdx.x; bi < nt;) {
+#ifndef WLD_CAND_MIX
+#define WLD_CAND_MIX 1
+#endif
+        // first tiles: the list is heaviest first and the dispatcher deals
+        // workgroups i, i + m, i + 2m (m = grid / 3) to one CU, so that CU
+        // would start three of the heaviest tiles at once (one wave of each on
+        // every SIMD): deal it ranks j, 2m - 1 - j and 2m + j instead, a heavy,
+        // a light and a middle one (a permutation of [0, grid))
+        uint32_t first = blockIdx.x;
+        if (WLD_CAND_MIX && tile_buckets) {
+            const uint32_t m = gridDim.x / 3, k = m ? blockIdx.x / m : 3u, j = blockIdx.x - (k < 3 ? k * m : 0u);
+            if (k < 3) first = k == 0 ? j : k == 1 ? 2 * m - 1 - j : 2 * m + j;
+        }
+        if (tile_buckets && first < nt) cand_prefix(tile_buckets, s_pre);  // (a workgroup without a tile skips it)
+        for (uint32_t bi = first; bi < nt;) {
             const uint32_t e = tile_buckets ? cand_entry(s_pre, bucket_cap, bi) : bi;
             compute_tile(tiles[e], threadIdx.x, tile_bits ? tile_bits[e] : 0xFFFFu);
             if (threadIdx.x == 0) s_next = gridDim.x + atomicAdd(tile_work, 1u);
