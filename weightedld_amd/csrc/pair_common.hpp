@@ -328,10 +328,13 @@ __device__ inline uint32_t cand_entry(const uint32_t *s_pre, uint32_t cap, uint3
 // The screen before the launch only appended candidates (atomics, before the
 // kernel boundary).
 // (all_waves: every wave wrote what the scan reads, and drains before the ticket)
-__device__ inline void scan_tail(const ScanArgs &a, uint32_t n_work, bool all_waves = false) {
+// first: the workgroup's first work item (a permutation of the grid's ids:
+// the workgroups that computed anything are exactly those with first < p).
+__device__ inline void scan_tail(const ScanArgs &a, uint32_t n_work, bool all_waves = false,
+                                 uint32_t first = blockIdx.x) {
     if (!a.ticket) return;
     const uint32_t p = min(gridDim.x, n_work);  // workgroups that computed a tile
-    if (blockIdx.x >= max(p, 1u)) return;
+    if (first >= max(p, 1u)) return;
     __shared__ unsigned s_run;
     if (all_waves || threadIdx.x < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // atomics performed
     // every wave has drained (waves that work independently may still be

@@ -470,7 +470,7 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
             bi = s_next;
             __syncthreads();
         }
-        scan_tail(sa, nt);
+        scan_tail(sa, nt, false, first);
     }
 }
 
