@@ -368,17 +368,21 @@ void rows_to_linear(uint32_t n, uint32_t rb, uint32_t re, uint32_t &lb, uint32_t
 // L2-aware launch order (default; WLD_TILE_ORDER=rows keeps plain (ta, tb)
 // order): workgroups are dealt to the 8
 // XCDs round-robin by launch index, so position 8i + x is XCD x's i-th tile.
-// Each XCD gets whole 8x8-tile super-blocks (greedy, least-loaded first), so
-// the ~64 tiles resident on its 32 CUs read 8 A and 8 B tile columns (2 MB at
-// C4) that fit its 4 MB L2; then the queues are evened out to within one
-// tile.  Short queues are padded with kNoTile entries, which the pair kernels
-// skip.
-std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t) {
-    constexpr uint32_t kX = 8, kS = 8;
+// Each XCD gets whole kS x kS-tile super-blocks (greedy, least-loaded first),
+// taken row by row; then the queues are evened out to within one tile.  Short
+// queues are padded with kNoTile entries, which the pair kernels skip.
+// kS = 16 where the 128 screen tiles resident on an XCD's 32 CUs (4
+// workgroups per CU: 8 rows of one super-block, 8 A and 16 B tile columns of
+// 64 NP bytes) fit its 4 MB L2 (C4: 3 MB): 0.86 GB per C4 screen launch past
+// L2 instead of 1.11 GB with kS = 8, step -0.5% (profiles/r03ar, r03as,
+// r03au).  Otherwise kS = 8, two whole super-blocks resident (C5, 323 KB
+// columns: 3% faster than 16).
+std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t, uint32_t kS) {
+    constexpr uint32_t kX = 8;
     std::vector<std::vector<uint32_t>> blocks;
     uint64_t last = ~0ull;
     std::vector<uint32_t> sorted(t);
-    auto block_of = [](uint32_t v) { return ((v >> 16) / kS) << 16 | ((v & 0xFFFFu) / kS); };
+    auto block_of = [kS](uint32_t v) { return ((v >> 16) / kS) << 16 | ((v & 0xFFFFu) / kS); };
     std::sort(sorted.begin(), sorted.end(), [&](uint32_t x, uint32_t y) {
         const uint32_t bx = block_of(x), by = block_of(y);
         return bx != by ? bx < by : x < y;
@@ -435,7 +439,8 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
     std::sort(t.begin(), t.end());
     // only with many rounds of resident tiles: whole super-blocks per XCD
     // leave up to one super-block of imbalance (C2's 528 tiles: +14%)
-    if (!c->opt_tile_rows && t.size() >= 4096 && T_used < 65535) t = xcd_order(t);
+    if (!c->opt_tile_rows && t.size() >= 4096 && T_used < 65535)
+        t = xcd_order(t, 24ull * kTile * c->NP <= (4ull << 20) ? 16u : 8u);
     c->n_tiles = (uint32_t)t.size();
     WLD_TRY(ensure(c->tiles, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)));
     // screen candidates: 16 weight buckets of tiles, then of their sub-block bits
