@@ -10,15 +10,22 @@ the timed region.  Total work is fixed as N grows (strong scaling).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c5]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU)
 
-Rank 0 prints ONE JSON line.  The CPU baseline (rank 0, N=1 only) is the C
-restatement of the lib.rs simd path (oracle/wld_oracle.c, "port"), threaded
-like rayon over 256x256 chunks, timed on a bounded sample of the same workload.
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts its
+own N ranks (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE set) before
+anything touches torch or the GPU, and relays rank 0's line; under torchrun
+WORLD_SIZE must equal --gpus.  Rank 0 prints ONE JSON line.  The CPU baseline
+(rank 0, at every N, after the timed region) is the C restatement of the
+lib.rs simd path (oracle/wld_oracle.c, "port"), threaded like rayon over
+256x256 chunks, timed on a bounded sample of the same workload.
 """
 import argparse
 import collections
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -193,6 +200,56 @@ def load_traffic(config, kernel):
         return None
 
 
+def launch_ranks(n, argv):
+    """--gpus N > 1 without a launcher: N child ranks of this script (one per
+    GPU, LOCAL_RANK = RANK), started before this process imports torch or
+    touches a GPU.  Rank 0's stdout (the JSON line) is relayed to stdout, the
+    other ranks' to stderr.  A rank that fails stops the others; returns the
+    first nonzero exit status (0 when all succeed)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs, relays = [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WLD_BENCH_SPAWNED="1")
+        p = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env,
+                             stdout=subprocess.PIPE, text=True, bufsize=1)
+        procs.append(p)
+
+        def relay(src, dst):
+            for line in src:
+                dst.write(line)
+                dst.flush()
+
+        t = threading.Thread(target=relay, args=(p.stdout, sys.stdout if r == 0 else sys.stderr), daemon=True)
+        t.start()
+        relays.append(t)
+    rc, kill_at = 0, None
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0 and rc == 0:
+                rc = c
+                print("bench.py: rank %d exited with status %d; stopping the other ranks" % (r, c), file=sys.stderr)
+                for k in live:
+                    procs[k].terminate()
+                kill_at = time.time() + 20.0
+        if kill_at is not None and time.time() > kill_at:
+            for k in live:
+                procs[k].kill()
+            kill_at = None
+        time.sleep(0.05)
+    for t in relays:
+        t.join(timeout=10)
+    return rc if rc >= 0 else 128 - rc
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -231,27 +288,52 @@ def main():
     ap.add_argument("--exact-sums", action="store_true",
                     help="exact sums rounded once (WLD_OPT_REF_SUMS 0) instead of the default, lib.rs's own f32 "
                          "summation order (rows bit-identical to lib.rs)")
+    ap.add_argument("--collectives", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (default): RCCL over xGMI, one GPU per rank; gloo: counts and rows exchanged as host "
+                         "tensors, ranks may share a GPU (rank r on device r mod the visible count: the multi-rank "
+                         "test of the launcher on a one-GPU box, never a headline line)")
+    ap.add_argument("--check-steps", type=int, default=0, metavar="K",
+                    help="after the timed region, K more steps whose gathered rows rank 0 compares with the "
+                         "oracle's (every row and bit, in reference order)")
     args = ap.parse_args()
     args.ref_sums = not args.exact_sums
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start the N ranks here, before torch or the GPU is touched
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print("warning: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d (launch with --nproc-per-node equal to --gpus)" %
+                         (args.gpus, world))
 
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    host_coll = args.collectives == "gloo"
+    n_dev = torch.cuda.device_count()
+    if n_dev == 0:
+        raise SystemExit("bench.py: rank %d of %d: no GPU visible" % (rank, world))
+    if not host_coll and local_rank >= n_dev:
+        raise SystemExit("bench.py: rank %d needs GPU %d but %d are visible (one GPU per rank over RCCL)" %
+                         (rank, local_rank, n_dev))
+    dev_index = local_rank % n_dev
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
+    # small control collectives (settle-step count, max-over-ranks times):
+    # device tensors over RCCL, host tensors over gloo
+    cdev = torch.device("cpu") if host_coll else device
     dist_on = world > 1 or args.rehearse_dist  # the N>1 step path (a group of one when rehearsing)
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29571")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=device)
+        if host_coll:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     sys.path.insert(0, REPO)
     import weightedld_amd as W
@@ -283,7 +365,7 @@ def main():
     kernel = {"auto": W.KERNEL_AUTO, "valu": W.KERNEL_VALU, "mfma": W.KERNEL_MFMA}[args.kernel]
     # the same pre-pass on the device from the resident raw
     # buffer (filter + Henikoff + encode), checked bit for bit against the host's
-    pre = W.Context(local_rank, kernel)
+    pre = W.Context(dev_index, kernel)
     dev_ms = []
     for _ in range(3):
         assert pre.load_filtered_device(d_buf.data_ptr(), L, N, unweighted=args.unweighted) == L
@@ -292,7 +374,7 @@ def main():
         assert np.array_equal(pre.weights().view(np.uint32), weights.view(np.uint32))
     pre.close()
     def new_ctx():
-        c = W.Context(local_rank, kernel)
+        c = W.Context(dev_index, kernel)
         if args.no_screen or args.no_prefilter:
             c.set_option("screen", 0)
         if args.no_prefilter:
@@ -317,7 +399,7 @@ def main():
     # RCCL count all_gather ordered after them on that stream, one host wait;
     # rows (if any) then gathered to rank 0 in reference order (shards
     # concatenate in descending rank order: chunk rows descend)
-    shard_step = wdist.ShardStep(ctx, rank, world, device)
+    shard_step = wdist.ShardStep(ctx, rank, world, device, host_collectives=host_coll)
     # N>1 timed steps: two contexts on the same resident inputs, step i's
     # kernel queued on the device behind step i-1's while step i-1's count
     # exchange / host read / row gather complete (PipelinedShardStep)
@@ -347,7 +429,8 @@ def main():
                                         # step i's pair kernel waits on the device for step i-1's screen
                                         # (wld_run_after); 1: for step i-1's whole run (profiles/r02pc/,
                                         # profiles/r03i/)
-                                        serialize_kernels={"0": False, "1": True}.get(serialize, "pair"))
+                                        serialize_kernels={"0": False, "1": True}.get(serialize, "pair"),
+                                        host_collectives=host_coll)
 
     def nrows(res):
         return int(res[1].shape[1]) if res is not None and res[1] is not None else 0
@@ -403,7 +486,7 @@ def main():
         per = (time.perf_counter() - t1) / 3
         settle_steps = int(np.ceil(args.settle_s / max(per, 1e-4)))
         if dist_on:
-            t = torch.tensor([settle_steps], dtype=torch.int64, device=device)
+            t = torch.tensor([settle_steps], dtype=torch.int64, device=cdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             settle_steps = int(t.item())
         run_steps(settle_steps)
@@ -438,19 +521,25 @@ def main():
     # the same steps without the screen (every tile, every plane; same rows),
     # reported alongside: a few sequential runs after the timed region
     unscreened_ms = None
-    if screened:
+    if dist_on:  # every rank runs the same steps (their collectives pair up), whatever its own policy chose
+        t = torch.tensor([int(screened)], dtype=torch.int64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        screened_any = bool(t.item())
+    else:
+        screened_any = screened
+    if screened_any:
         ctx.set_option("screen", 0)
         ums = []
         for _ in range(5):
             step()
             ums.append(ctx.stats()["pair_kernel_ms"])
         ctx.set_option("screen", 1)
-        unscreened_ms = float(np.mean(ums[1:]))
+        unscreened_ms = float(np.mean(ums[1:])) if screened else None
     if dist_on:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        km = torch.tensor([float(np.mean(kms)), float(np.mean(sms))], dtype=torch.float64, device=device)
+        km = torch.tensor([float(np.mean(kms)), float(np.mean(sms))], dtype=torch.float64, device=cdev)
         dist.all_reduce(km, op=dist.ReduceOp.MAX)
         kernel_ms, screen_ms = float(km[0].item()), float(km[1].item())
     else:
@@ -459,9 +548,33 @@ def main():
     kern_name = "mfma" if st["kernel"] == W.KERNEL_MFMA else "valu"
     planes = st["mfma_planes"]
 
+    # --check-steps: K more steps through the same step path (pipelined
+    # contexts and the row gather at N>1); rank 0 keeps every step's rows
+    checked = []
+    if args.check_steps > 0:
+        if not dist_on:
+            for _ in range(args.check_steps):
+                ctx.run_chunks(thr, cb, ce)
+                g = ctx.rows()
+                checked.append({f: np.array(getattr(g, f)) for f in wdist.ROW_FIELDS})
+        else:
+            res = []
+            if pipe is not None:
+                for _ in range(args.check_steps):
+                    r = pipe.submit(thr, cb, ce)
+                    if r is not None:
+                        res.append(r)
+                res += pipe.drain_all()
+            else:
+                res = [shard_step(thr, cb, ce) for _ in range(args.check_steps)]
+            if rank == 0:
+                checked = [wdist.unpack_rows(g) for _, g in res]
+    torch.cuda.synchronize()
+    if dist_on:
+        # no collective after this: the other ranks leave, so that rank 0's
+        # CPU baseline runs with no rank polling beside it
+        dist.destroy_process_group()
     if rank != 0:
-        if dist_on:
-            dist.destroy_process_group()
         return
 
     total_pairs = L * (L - 1) // 2
@@ -586,8 +699,15 @@ def main():
             "Henikoff, every 10th x 2^-8 (--wide-weights)" if args.wide_weights else "Henikoff"),
         "config": {"workload": desc, "n_seqs": N, "n_sites": L, "r2_threshold": thr, "pairs": total_pairs,
                    "rows_passing": rows, "kernel": kern_name, "mfma_planes": planes,
+                   "launch": ("bench.py spawned %d ranks" % world if os.environ.get("WLD_BENCH_SPAWNED") else
+                              "external launcher (WORLD_SIZE=%d)" % world if "WORLD_SIZE" in os.environ else
+                              "single process"),
+                   # gloo host collectives may put several ranks on one GPU
+                   # (the launcher's multi-rank test): count the devices used
+                   "devices": min(world, n_dev) if host_coll else world,
                    "parallelism": "chunk-range shard x%d%s%s" % (
-                       world, (" + RCCL gather" if dist_on else ""),
+                       world, ((" + gloo host-tensor gather" if host_coll else " + RCCL count all_gather, exact-size "
+                                "send/recv to rank 0") if dist_on else ""),
                        (", pipelined steps (%d contexts, %s)" % (
                            depth, {"0": "screens may overlap", "1": "serialized on the whole step",
                                    "stream": "one stream"}.get(
@@ -606,7 +726,31 @@ def main():
                       "device_encode_prep": load_ms, "pair_phase": kernel_ms, "order_assembly": float(np.mean(oms)),
                       "step_minus_kernel_rank0": float(np.median(gms))},
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if checked:
+        # every checked step's rows (gathered to rank 0 at N>1) against the
+        # oracle over the same chunk range: the same rows in the same order,
+        # d / d' / r2 bit for bit in lib.rs's order (within 1e-5 otherwise)
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import _oracle as O  # checker only
+        O.use_native()
+        ref = O.all_pairs(buf, weights, np.float32(thr), n_threads=int(os.environ.get("OMP_NUM_THREADS") or 0) or
+                          (os.cpu_count() or 1), chunk_lo=0 if world > 1 else cb, chunk_hi=ctx.chunks(L)
+                          if world > 1 else ce)
+        equal = 0
+        for g in checked:
+            same = len(g["site_a"]) == len(ref["site_a"]) and all(
+                np.array_equal(g[f].astype(np.uint32), ref[f].astype(np.uint32)) for f in ("site_a", "site_b"))
+            for f in ("d", "d_prime", "r2"):
+                if not same:
+                    break
+                a, b = np.asarray(g[f], dtype=np.float32), np.asarray(ref[f], dtype=np.float32)
+                same = np.array_equal(a.view(np.uint32), b.view(np.uint32)) if args.ref_sums else bool(
+                    np.all(np.abs(a.astype(np.float64) - b) <= 1e-5 * np.maximum(1.0, np.abs(b))))
+            equal += bool(same)
+        out["steps_check"] = {"steps": len(checked), "equal_to_oracle": equal, "rows_per_step": len(ref["site_a"]),
+                              "compare": "bitwise" if args.ref_sums else "within 1e-5"}
+        assert equal == len(checked) == args.check_steps, out["steps_check"]
+    if not args.no_cpu_baseline:
         oref, ochunks, out["cpu_baseline"] = cpu_baseline(buf, weights, thr, args.cpu_seconds)
         # the same chunks on the GPU: rows against the oracle's (lib.rs
         # semantics).  Exact sums rounded once may put a pair whose r2 lies
@@ -629,8 +773,6 @@ def main():
         assert not args.ref_sums or len(one_sided) == 0, out["rows_check"]
         assert not whole or rows == len(kg), (rows, len(kg))
     print(json.dumps(out), flush=True)
-    if dist_on:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -35,7 +35,9 @@ extern "C" {
 #define WLD_E_NODEV (-4)  /* no usable gfx950 device                             */
 #define WLD_E_IO (-5)     /* file could not be read / written                    */
 #define WLD_E_FORMAT (-6) /* input violates the reference's format (it panics)  */
-#define WLD_E_STATE (-7)  /* call order violated (e.g. run before load)          */
+#define WLD_E_STATE (-7)  /* call order violated (e.g. run before load), or a
+                             device guard refused an out-of-range index (the
+                             run produced no rows; the context stays usable)    */
 
 #define WLD_SYM_A 0
 #define WLD_SYM_C 1
@@ -206,6 +208,10 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *   WLD_OPT_STAGING_ROWS   initial staging capacity in rows (default 2^25;
  *                      grown on overflow by a re-run).
  *   WLD_OPT_HOST_BATCH_PAIRS  pairs per batch of wld_run_host (default 2^31).
+ *   WLD_OPT_FUSED_SCAN 1 (default): after a screen, the run's chunk scan runs
+ *                      in the candidate launch's last workgroup (ranges up to
+ *                      4096 chunks); 0: as a launch of its own (the kernel
+ *                      boundary orders it).  Same rows.
  *                      (Ids 9 and 10, an experimental 64x128-tile screen and an fp4
  *                      screen of round 2, are retired: WLD_E_ARG.) */
 #define WLD_OPT_PREFILTER 1
@@ -217,6 +223,7 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
 #define WLD_OPT_STAGING_ROWS 7
 #define WLD_OPT_HOST_BATCH_PAIRS 8
 #define WLD_OPT_REF_SUMS 11
+#define WLD_OPT_FUSED_SCAN 12
 int wld_set_option(wld_ctx *ctx, int option, int64_t value);
 int wld_get_option(wld_ctx *ctx, int option, int64_t *value);
 

@@ -72,3 +72,50 @@ def test_bench_json_line():
     cb = out["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["value"] > 0 and cb["cores"] >= 1
     assert out["config"]["workload"]
+
+
+def test_launcher_starts_n_ranks_before_the_gpu():
+    """--gpus 2 with no WORLD_SIZE: bench.py starts ranks 0 and 1 itself
+    (RANK/LOCAL_RANK/WORLD_SIZE set, no external launcher); here, with no GPU,
+    each rank stops with its own error and the launcher returns nonzero with
+    no JSON line on stdout."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""  # (a GPU box too: no device for the ranks)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert "rank 0 of 2" in r.stderr + r.stdout or "rank 1 of 2" in r.stderr + r.stdout, r.stderr[-2000:]
+
+
+def test_world_size_must_match_gpus():
+    """Under an external launcher WORLD_SIZE must equal --gpus (no silent
+    fallback to another rank count)."""
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--steps", "1"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "--gpus 4 but WORLD_SIZE=2" in r.stderr
+
+
+@pytest.mark.gpu
+def test_launcher_two_ranks_rows_equal_oracle_every_step():
+    """`bench.py --gpus 2` starts its own two ranks (here both on the box's one
+    GPU, counts and rows exchanged as host tensors over gloo); BASELINE config
+    2 at threshold 0 (1,999,000 rows a step, split over the two shards and
+    gathered to rank 0 with exact-size transfers): every checked step's rows
+    equal the oracle's bit for bit, in reference order; the line says n_gpus 2
+    and carries the CPU baseline."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--collectives", "gloo", "--config", "c2",
+                        "--steps", "5", "--warmup", "2", "--settle-s", "0", "--check-steps", "4",
+                        "--cpu-seconds", "2"], cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert REQUIRED <= set(out), sorted(REQUIRED - set(out))
+    assert out["n_gpus"] == 2 and out["config"]["launch"] == "bench.py spawned 2 ranks"
+    sc = out["steps_check"]
+    assert sc["steps"] == 4 and sc["equal_to_oracle"] == 4 and sc["rows_per_step"] > 1_900_000
+    assert out["config"]["rows_passing"] == sc["rows_per_step"]
+    assert out["cpu_baseline"]["value"] > 0

@@ -7,6 +7,7 @@ come in the reference order (triu chunk order, then a, then b).
 """
 import math
 import os
+import re
 import subprocess
 
 import numpy as np
@@ -879,3 +880,72 @@ def test_progress_once_per_chunk_config2(W, devices):
     assert steps == sorted(chunk_pairs(L, i) for i in range(n_chunks))
     assert len(store) > 1_990_000
 
+
+
+# ------------------------------------------------------------------ CLI progress bars (main.rs:89-116, 170-190)
+def _write_c2_fasta(path):
+    sys_path_bench()
+    from bench import synth as bench_synth
+    codes = bench_synth(2000, 500)  # BASELINE config 2: 500 sequences x 2000 sites, all kept
+    lut = np.frombuffer(b"ACGT-N", dtype=np.uint8)
+    with open(path, "wb") as f:
+        for k in range(codes.shape[1]):
+            f.write(b">s%d\n" % k + lut[codes[:, k]].tobytes() + b"\n")
+
+
+def _run_cli_pty(cmd, env):
+    """Runs the CLI with stderr on a pseudo-terminal (as an interactive shell
+    would): returns (exit status, everything written to the terminal)."""
+    import pty
+    master, slave = pty.openpty()
+    p = subprocess.Popen(cmd, stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL, stderr=slave, env=env)
+    os.close(slave)
+    out = b""
+    while True:
+        try:
+            data = os.read(master, 65536)
+        except OSError:
+            break
+        if not data:
+            break
+        out += data
+    os.close(master)
+    return p.wait(timeout=120), out
+
+
+@pytest.mark.parametrize("prepass", [False, True], ids=["host_prepass", "gpu_prepass"])
+def test_cli_progress_bars(tmp_path, prepass):
+    """The CLI feeds the LD pass's progress_report closure (main.rs:184-188) to
+    a progress bar: at BASELINE config 2 (36 chunks) the closure is called 37
+    times (progress(0), then one per chunk; logged at debug level).  The bars
+    (LD pass and TSV write, indicatif's template) are drawn only when info is
+    enabled AND stderr is a terminal; the TSV is byte-identical either way, and
+    with stderr on a pipe the log lines carry no bar."""
+    fa = tmp_path / "c2.fasta"
+    _write_c2_fasta(fa)
+    extra = ["--gpu-prepass"] if prepass else []
+    env = dict(os.environ)
+
+    def cmd(out):
+        return [CLI, "--fasta-input", str(fa), "--pair-output", str(out), "--r2-threshold", "0.0"] + extra
+
+    # debug level, stderr on a pipe: the closure's call count, no bar
+    r = subprocess.run(cmd(tmp_path / "a.tsv"), capture_output=True, text=True, timeout=120,
+                       env=dict(env, RUST_LOG="debug"))
+    assert r.returncode == 0, r.stderr
+    m = re.search(r"progress: (\d+) progress_report calls, last (\d+) pairs", r.stderr)
+    assert m, r.stderr[-2000:]
+    assert int(m.group(1)) == 37
+    assert 0 < int(m.group(2)) < 2000 * 1999 // 2  # the last value: every pair but the last chunk's
+    assert "\x1b[2K" not in r.stderr and "pairs computed at" in r.stderr
+    # info level on a terminal: bar frames on stderr, same TSV
+    rc, term = _run_cli_pty(cmd(tmp_path / "b.tsv"), dict(env, RUST_LOG="info"))
+    assert rc == 0, term[-2000:]
+    text = term.decode("utf-8", "replace")
+    assert "\x1b[2K" in text and re.search(r"\] \d+% \(\d+/s \d\d:\d\d:\d\d\)", text), text[-2000:]
+    assert "pairs computed at" in text
+    assert (tmp_path / "b.tsv").read_bytes() == (tmp_path / "a.tsv").read_bytes()
+    # warn level on a terminal: no bar (log_enabled!(Level::Info) is false)
+    rc, term = _run_cli_pty(cmd(tmp_path / "c.tsv"), dict(env, RUST_LOG="warn"))
+    assert rc == 0 and b"\x1b[2K" not in term and b"%" not in term, term[-2000:]
+    assert (tmp_path / "c.tsv").read_bytes() == (tmp_path / "a.tsv").read_bytes()

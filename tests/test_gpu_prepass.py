@@ -1,12 +1,16 @@
-"""Device pre-pass (wld_load_filtered, prepass.hip) against the host restatement
-of main.rs:139-156: the kept-site map, the Henikoff weights (bit for bit) and
-the rows computed from them must be identical to the host path
-(wld_siteset_filter_sites_of_interest + wld_henikoff_weights + wld_load)."""
+"""Device pre-pass (wld_load_filtered, prepass.hip) against the oracle and the
+host restatement of main.rs:139-156: the kept-site map equals the oracle's
+is_site_of_interest mask (lib.rs:309-338, wldo_is_site_of_interest), the
+Henikoff weights equal the oracle's on the kept buffer bit for bit
+(lib.rs:340-380, wldo_henikoff_weights), and the rows computed from them are
+identical to the host path's (wld_siteset_filter_sites_of_interest +
+wld_henikoff_weights + wld_load)."""
 import os
 
 import numpy as np
 import pytest
 
+import _oracle as O  # checker only
 from conftest import FIXTURES
 from test_gpu_parity import synth
 
@@ -28,12 +32,25 @@ def host_path(W, ss, params, unweighted):
     return kept, w
 
 
+def check_oracle(dev, buf, params, unweighted):
+    """The device pre-pass against the oracle itself: kept sites = the
+    oracle's mask, weights = the oracle's Henikoff weights of the kept buffer
+    (unit weights when unweighted, main.rs:150-153), bit for bit."""
+    buf = np.minimum(buf, 5).astype(np.uint8)  # Symbol codes are 0..5 (the product clamps larger bytes to Unknown)
+    mask = O.site_mask(buf, *params)
+    assert np.array_equal(dev.site_map(), np.nonzero(mask)[0].astype(np.uint64))
+    ref_w = np.ones(buf.shape[1], dtype=np.float32) if unweighted else O.henikoff_weights(buf[mask])
+    wd = dev.weights()
+    assert np.array_equal(wd.view(np.uint32), ref_w.view(np.uint32)), (wd[:5], ref_w[:5])
+
+
 def check_equal(W, buf, params=(0.8, 0.02, 0.5), unweighted=False, thr=0.0, kernel=None):
     ss = W.SiteSet.from_buffer(buf)
     kept, w = host_path(W, ss, params, unweighted)
     kernel = W.KERNEL_AUTO if kernel is None else kernel
     dev = W.Context(0, kernel)
     n = dev.load_filtered(buf, *params, unweighted=unweighted)
+    check_oracle(dev, buf, params, unweighted)
     assert n == kept.n_sites()
     sm = kept.site_map if kept.site_map is not None else np.arange(kept.n_sites(), dtype=np.uint64)
     assert np.array_equal(dev.site_map(), sm)
@@ -137,3 +154,25 @@ def test_cli_gpu_prepass_same_output(tmp_path, name, unweighted):
         assert r.returncode == 0, r.stderr
         outs.append((pairs.read_bytes(), wts.read_bytes()))
     assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("config", ["c2", "c4", "c5"])
+def test_prepass_bench_workloads_vs_oracle(W, config):
+    """The full bench inputs (BASELINE configs 2, 4 and 5: up to 50,000 sites
+    x 5,000 sequences), random and (C4) linkage blocks with Unknown symbols
+    sprinkled in: the device's kept-site map and Henikoff weights equal the
+    oracle's bit for bit."""
+    import bench
+    N, L, _, _ = bench.CONFIGS[config]
+    bufs = [bench.synth(L, N)]
+    if config == "c4":
+        ld = bench.ld_blocks(L, N)
+        rng = np.random.default_rng(11)
+        ld[rng.random(ld.shape) < 0.01] = 5  # Unknown: the Henikoff fill term
+        bufs.append(ld)
+    for buf in bufs:
+        dev = W.Context(0)
+        n = dev.load_filtered(buf, 0.8, 0.02, 0.5)
+        assert n > 0
+        check_oracle(dev, buf, (0.8, 0.02, 0.5), False)
+        dev.close()

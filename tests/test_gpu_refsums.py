@@ -277,17 +277,20 @@ def test_report_full_bench_workloads(W, cfg):
     """BASELINE configs 4 and 5 at full size (the bench's own seeded inputs,
     Henikoff weights): every row of the GPU paths against the oracle over the
     whole pair space (about 5 s / 30 s of oracle on 16 threads), at the bench
-    threshold 0.05 and at 0.01 (thousands of rows)."""
+    threshold 0.05 and at a low threshold that emits rows on random data:
+    0.01 at C4 (~1,500 rows), 0.003 at C5 (~10^5 rows: N r2 = 15 is the
+    chi-square tail the null pairs of 5,000 sequences reach)."""
     N, L, thr, _ = bench.CONFIGS[cfg]
     buf = bench.synth(L, N)
     w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
-    lo = np.float32(0.01)
+    lo = np.float32(0.01 if cfg == "c4" else 0.003)
     ref = O.all_pairs(buf, w, lo)
     assert ref["pairs"] == L * (L - 1) // 2
+    assert len(ref["r2"]) > (1000 if cfg == "c4" else 50000), len(ref["r2"])
     for mode in ("exact", "ref_sums"):
         ctx = W.Context(0, W.KERNEL_AUTO, ref_sums=mode == "ref_sums")
         ctx.load(buf, w)
-        for t in (thr, 0.01):
+        for t in (thr, float(lo)):
             t32 = np.float32(t)
             sub = {f: v[ref["r2"] > t32] for f, v in ref.items() if f != "pairs"}
             ctx.run(t)
@@ -301,6 +304,26 @@ def test_report_full_bench_workloads(W, cfg):
                 assert res["one_sided_outside_band"] == 0, res
                 assert res["beyond_tol_d"] == 0 and res["beyond_tol_r2"] == 0, res
         ctx.close()
+
+
+def test_c5_ldblocks_rows_bit_exact(W):
+    """BASELINE config 5's size with linkage blocks (bench --data ldblocks at
+    5,000 x 50,000): at the bench threshold 0.05 hundreds of thousands of rows
+    pass — the screen's candidate tiles, staging, the chunk scan and the
+    reference-order gather at 1.25e9 pairs — and every row equals the
+    oracle's, bit for bit and in order (the default, lib.rs's order)."""
+    N, L, thr, _ = bench.CONFIGS["c5"]
+    buf = bench.ld_blocks(L, N)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ref = O.all_pairs(buf, w, np.float32(thr))
+    assert len(ref["r2"]) > 100000, len(ref["r2"])
+    ctx = W.Context(0, W.KERNEL_AUTO)
+    ctx.load(buf, w)
+    n = ctx.run(thr)
+    REF_REPORT.append("c5 ldblocks %dx%d thr %g: rows %d (oracle %d), screened %d" % (
+        N, L, thr, n, len(ref["r2"]), ctx.stats()["screened"]))
+    assert_rows_bit_exact(ctx.rows(), {f: v for f, v in ref.items() if f != "pairs"})
+    ctx.close()
 
 
 def test_ref_screen_policy(W):

@@ -237,7 +237,7 @@ class Context:
     def set_option(self, name, value):
         """wld_set_option: name is a key of OPTIONS ("prefilter", "screen",
         "tile_order", "all_planes", "mfma_layout", "valu_plain", "staging_rows",
-        "host_batch_pairs", "ref_sums"); only "ref_sums" changes a result."""
+        "host_batch_pairs", "ref_sums", "fused_scan"); only "ref_sums" changes a result."""
         check(lib().wld_set_option(self._h, OPTIONS[name], int(value)), "wld_set_option")
 
     def get_option(self, name):

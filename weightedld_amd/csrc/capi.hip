@@ -101,8 +101,11 @@ struct wld_ctx {
     hipEvent_t ev[7] = {};  // 2..3 pair phase (6: after the screen), 3..4/5 order phase
     RunPending pend;                      // the run between run_enqueue and run_complete
     bool run_dirty = true;                // run state (cursor, chunk totals) may be nonzero: re-initialise
-    unsigned long long *h_cnt = nullptr;  // mapped pinned {cursor, rows, candidate tiles, sub-blocks} (the scan)
+    // mapped pinned {cursor, rows, candidate tiles, sub-blocks} (the scan), then
+    // the kernels' guard word (OrderArgs::guard; 0 unless an index was refused)
+    unsigned long long *h_cnt = nullptr;
     unsigned long long *d_hcnt = nullptr;
+    int cand_set = 0;  // the candidate set (counter words) of the next pass; flips after each scan
     int kernel_pref = WLD_KERNEL_AUTO;
     // wld_set_option (include/weightedld.h)
     bool opt_prefilter = true, opt_tile_rows = false, opt_all_planes = false;
@@ -116,6 +119,7 @@ struct wld_ctx {
     float ref_pairs_bad_thr = -1.0f;
     bool ref_pairs_pass = false;  // the pass staged exact candidate pairs (ref_rows_kernel)
     bool opt_site_major = false, opt_valu_plain = false;
+    bool opt_fused_scan = true;  // WLD_OPT_FUSED_SCAN: the chunk scan in the candidate launch's last workgroup
     bool opt_ref_sums = true;  // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order (default)
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
 
@@ -470,6 +474,7 @@ OrderArgs order_args(wld_ctx *c) {
     o.prog_n = c->prog_pass ? ptr<unsigned>(c->prog_n) : nullptr;
     o.prog_log = c->prog_pass ? c->d_plog : nullptr;
     o.L = (uint32_t)c->L;
+    o.guard = reinterpret_cast<unsigned *>(c->d_hcnt + 4);
     return o;
 }
 
@@ -566,9 +571,11 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         for (int t = 0; t < 3; ++t) m.resid[t] = c->wst.resid[t];
         for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
         m.cand_list = ptr<uint32_t>(c->cand);
-        m.cand_count = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 2);
-        m.cand_work = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 3) + 1;  // beside the ticket
-        m.cand_buckets = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 4);
+        // this pass's candidate set (the scan zeroes the other one, enqueue_pass)
+        unsigned long long *set = ptr<unsigned long long>(c->counters) + kCandSet0 + kCandSetWords * c->cand_set;
+        m.cand_count = reinterpret_cast<unsigned *>(set);
+        m.cand_work = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 2) + 1;  // beside the ticket
+        m.cand_buckets = reinterpret_cast<unsigned *>(set + 1);
         if (scan && !dense) m.scan = *scan;
         RefRowsLaunch rr{};
         if (ref_screen) {
@@ -635,7 +642,7 @@ int wld_create(int device, wld_ctx **out) {
             delete c;
             return fail(WLD_E_HIP, "hipEventCreate failed");
         }
-    if (hipHostMalloc((void **)&c->h_cnt, 4 * sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent) !=
+    if (hipHostMalloc((void **)&c->h_cnt, 5 * sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent) !=
             hipSuccess ||
         hipHostGetDevicePointer((void **)&c->d_hcnt, c->h_cnt, 0) != hipSuccess) {
         (void)hipGetLastError();
@@ -714,6 +721,7 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
             if (value < 1) return fail(WLD_E_ARG, "WLD_OPT_HOST_BATCH_PAIRS must be >= 1");
             c->opt_host_batch_pairs = (uint64_t)value;
             break;
+        case WLD_OPT_FUSED_SCAN: c->opt_fused_scan = value != 0; break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }
     return WLD_OK;
@@ -731,6 +739,7 @@ int wld_get_option(wld_ctx *c, int option, int64_t *value) {
         case WLD_OPT_REF_SUMS: *value = c->opt_ref_sums; break;
         case WLD_OPT_STAGING_ROWS: *value = (int64_t)c->opt_staging_rows; break;
         case WLD_OPT_HOST_BATCH_PAIRS: *value = (int64_t)c->opt_host_batch_pairs; break;
+        case WLD_OPT_FUSED_SCAN: *value = c->opt_fused_scan; break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }
     return WLD_OK;
@@ -965,21 +974,31 @@ int enqueue_pass(wld_ctx *c) {
         HIP_TRY(hipGetLastError());
     }
     c->run_dirty = true;  // until run_complete has seen this pass's scan
+    // the reference-order layout is built (once per load) before the pass's
+    // first event, so its kernel never lands in the pair phase's time
+    if (c->opt_ref_sums && c->n_tiles) WLD_TRY(ensure_ref_layout(c));
     const OrderArgs o = order_args(c);
-    // counters: {cursor, total, {candidate tiles, sub-blocks}, {ticket, work}, 16 bucket counts}
+    // counters: {cursor, total, {ticket, work}, candidate set 0, candidate set 1}
+    // (kernels.hpp).  The pass appends to set cand_set; its scan reads that
+    // set's counts and zeroes the other one, which the next pass then uses —
+    // no kernel of this pass can read a count its own scan has reset.
     unsigned long long *cn = ptr<unsigned long long>(c->counters);
+    unsigned long long *cur = cn + kCandSet0 + kCandSetWords * c->cand_set;
+    unsigned long long *nxt = cn + kCandSet0 + kCandSetWords * (c->cand_set ^ 1);
     ScanArgs sa{ptr<uint32_t>(c->chunk_total), r.lin_begin, lin_count, ptr<uint32_t>(c->chunk_base), cn + 1, cn,
-                c->d_hcnt, r.count_out, reinterpret_cast<unsigned *>(cn + 2), reinterpret_cast<unsigned *>(cn + 4),
-                reinterpret_cast<unsigned *>(cn + 3)};
+                c->d_hcnt, r.count_out, reinterpret_cast<unsigned *>(cur), reinterpret_cast<unsigned *>(nxt),
+                reinterpret_cast<unsigned *>(nxt + 1), reinterpret_cast<unsigned *>(cn + 2)};
     c->h_cnt[0] = c->h_cnt[1] = lin_count ? ~0ull : 0ull;
     c->h_cnt[2] = c->h_cnt[3] = 0;
+    c->h_cnt[4] = 0;  // the guard word
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     c->screened = c->screened2 = false;
     // the scan is fused into the launch after a screen for ranges up to 4096
     // chunks (C4: 3,160, ~10 us in one 256-thread workgroup); a larger range
     // (C5: 19,306 chunks, ~70 us fused) gets the 1024-thread scan kernel
-    const bool fuse_scan = lin_count && lin_count <= 4096;
+    const bool fuse_scan = c->opt_fused_scan && lin_count && lin_count <= 4096;
     if (c->n_tiles) WLD_TRY(launch_pairs(c, r.thr, o, nullptr, &c->screened, fuse_scan ? &sa : nullptr));
+    if (lin_count) c->cand_set ^= 1;  // this pass's scan (fused or below) zeroes the other set
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     if (lin_count && !(c->screened && fuse_scan)) {  // else the candidate launch's last workgroup ran it
         sa.ticket = nullptr;
@@ -1043,8 +1062,11 @@ int run_enqueue(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uns
 
 // The progress log of a pass with per-chunk progress: every chunk pair count
 // logged so far, in slot order, to on_chunk (on the calling thread), polled
-// while the pass runs; then the rest once it has completed.
-int drain_progress(wld_ctx *c, uint32_t n_chunks) {
+// while the pass runs; then the rest once it has completed.  Progress is a
+// report, not a result: entries still missing once the pass has completed
+// (a re-run, a refused tile) are reported from the chunk pair counts the host
+// knows, never turned into a failed run.
+int drain_progress(wld_ctx *c, uint32_t lin_begin, uint32_t n_chunks) {
     uint32_t seen = 0;
     auto drain = [&] {
         while (seen < n_chunks) {
@@ -1064,8 +1086,37 @@ int drain_progress(wld_ctx *c, uint32_t n_chunks) {
     // the pass has completed: every chunk's entry is written (system-scope
     // stores); allow the last ones a moment to land
     for (int spin = 0; seen < n_chunks && spin < 100000; ++spin) drain();
-    if (seen < n_chunks) return fail(WLD_E_HIP, "internal: %u of %u chunk progress entries arrived", seen, n_chunks);
+    if (seen < n_chunks) {
+        // the logged chunks' pairs, then the pairs of the chunks whose entries
+        // did not arrive, one report each (the sum is the range's pairs)
+        uint64_t logged = 0;
+        for (uint32_t k = 0; k < seen; ++k) logged += c->h_plog[k];
+        uint64_t rest = pairs_in_chunks(c->L, lin_begin, lin_begin + n_chunks) - std::min<uint64_t>(
+                            logged, pairs_in_chunks(c->L, lin_begin, lin_begin + n_chunks));
+        const uint32_t missing = n_chunks - seen;
+        for (uint32_t k = 0; k < missing; ++k) {
+            const uint64_t v = rest / (missing - k);
+            (*c->on_chunk)(v);
+            rest -= v;
+        }
+    }
     return WLD_OK;
+}
+
+// The kernels' guard word (OrderArgs::guard) after a completed phase: nonzero
+// when a kernel refused an out-of-range index (a candidate entry or tile, a
+// staged pair, a gather destination) instead of reading or writing through
+// it.  The run is then wrong, not just slow: WLD_E_STATE, and the next run
+// starts from re-initialised run state.
+int check_guard(wld_ctx *c, const char *phase) {
+    const unsigned g = (unsigned)__atomic_load_n(&c->h_cnt[4], __ATOMIC_ACQUIRE);
+    if (!g) return WLD_OK;
+    c->run_dirty = true;
+    c->have_rows = false;
+    return fail(WLD_E_STATE, "internal: the %s refused an out-of-range index (guard 0x%x: %s%s%s%s%s); no rows", phase,
+                g, g & kGuardEntry ? "candidate entry " : "", g & kGuardTile ? "tile " : "",
+                g & kGuardPair ? "staged pair " : "", g & kGuardSlice ? "candidate slice " : "",
+                g & kGuardGather ? "gather destination" : "");
 }
 
 // Phase 2: one host wait, the overflow re-run if needed, then (only when rows
@@ -1080,11 +1131,12 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     for (int attempt = 0; attempt < 2; ++attempt) {
         if (c->prog_pass) {
             c->prog_pass = false;  // a re-run after a staging overflow does not report again
-            WLD_TRY(drain_progress(c, lin_count));
+            WLD_TRY(drain_progress(c, r.lin_begin, lin_count));
         }
         // the pass's end, not the stream's: on a shared stream (wld_set_stream)
         // the next context's run may already be queued behind it
         HIP_TRY(hipEventSynchronize(c->ev[4]));
+        WLD_TRY(check_guard(c, "pair phase"));
         c->run_dirty = false;  // the pass completed: its scan cleaned the run state
         h[0] = __atomic_load_n(&c->h_cnt[0], __ATOMIC_ACQUIRE);
         h[1] = __atomic_load_n(&c->h_cnt[1], __ATOMIC_ACQUIRE);
@@ -1107,13 +1159,14 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     WLD_TRY(ensure(c->out_r2, std::max<uint64_t>(rows, 1) * 4));
     int order_end = 4;  // with no rows the order phase ends at the scan
     if (rows && lin_count) {
-        launch_gather(order_args(c), ptr<uint32_t>(c->chunk_base), r.lin_begin, lin_count, n, (uint32_t)c->L,
+        launch_gather(order_args(c), ptr<uint32_t>(c->chunk_base), r.lin_begin, lin_count, n, (uint32_t)c->L, rows,
                       c->has_map ? ptr<uint32_t>(c->site_map) : nullptr, ptr<uint32_t>(c->out_a),
                       ptr<uint32_t>(c->out_b), ptr<float>(c->out_d), ptr<float>(c->out_dp), ptr<float>(c->out_r2),
                       c->stream);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ev[5], c->stream));
         HIP_TRY(hipEventSynchronize(c->ev[5]));
+        WLD_TRY(check_guard(c, "reference-order gather"));
         order_end = 5;
     }
     c->rows = rows;
@@ -1123,7 +1176,8 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     c->stats.rows = rows;
     c->stats.pair_kernel_ms = event_ms(c->ev[2], c->ev[3]);
     c->stats.order_ms = event_ms(c->ev[3], c->ev[order_end]);
-    c->stats.pair_kernel_launches = c->n_tiles ? (c->screened ? 2 : 1) : 0;
+    // (exact candidate pairs: the i8 pass, ref_sums_kernel, ref_compact_kernel)
+    c->stats.pair_kernel_launches = c->n_tiles ? (c->ref_pairs_pass ? 3 : c->screened ? 2 : 1) : 0;
     c->stats.tiles = c->n_tiles;
     c->stats.screened = c->ref_pairs_pass ? 4 : c->screened ? (c->screened2 ? 3 : 1) : 0;
     c->stats.candidate_pairs = c->ref_pairs_pass ? h[0] : 0;

@@ -25,6 +25,7 @@
 #include <mutex>
 #include <thread>
 
+#include <sys/ioctl.h>
 #include <unistd.h>
 #include <vector>
 
@@ -101,6 +102,72 @@ std::string human(double v, const char *units = "") {
     snprintf(buf, sizeof buf, "%.2f %s%s", x, pre[k], units);
     return buf;
 }
+
+// indicatif 0.15's ProgressBar as main.rs sets it up (main.rs:89-97, 170-178):
+// template "{spinner:.green} [{elapsed_precise}] [{wide_bar:.cyan/blue}]
+// {percent}% ({per_sec} {eta_precise})", progress chars "#>-", drawn on stderr
+// only when the log level enables info (log_enabled!(Level::Info)) and stderr
+// is a terminal (indicatif's stderr target draws nothing otherwise), at most
+// 15 frames a second; dropped unfinished, it clears its line.  So TSVs and
+// log lines are byte-identical whether or not a bar was drawn.
+class ProgressBar {
+  public:
+    explicit ProgressBar(uint64_t len)
+        : len_(len), on_(g_level >= 3 && isatty(2)), start_(std::chrono::steady_clock::now()), last_(start_) {}
+    ~ProgressBar() {
+        if (on_ && drawn_) fputs("\r\x1b[2K", stderr), fflush(stderr);
+    }
+    void set_position(uint64_t pos) {
+        ++updates_;
+        last_pos_ = pos;
+        pos_ = std::min(pos, len_);
+        if (!on_) return;
+        const auto now = std::chrono::steady_clock::now();
+        if (drawn_ && now - last_ < std::chrono::milliseconds(66)) return;  // indicatif's 15 Hz draw rate
+        last_ = now;
+        draw(now);
+    }
+    uint64_t updates() const { return updates_; }
+    uint64_t last_position() const { return last_pos_; }
+
+  private:
+    static std::string hms(uint64_t secs) {
+        char b[32];
+        snprintf(b, sizeof b, "%02" PRIu64 ":%02" PRIu64 ":%02" PRIu64, secs / 3600, secs / 60 % 60, secs % 60);
+        return b;
+    }
+    void draw(std::chrono::steady_clock::time_point now) {
+        static const char *ticks[] = {"\u2801", "\u2802", "\u2804", "\u2840", "\u2880",
+                                      "\u2820", "\u2810", "\u2808"};  // indicatif's default tick chars
+        const double el = std::chrono::duration<double>(now - start_).count();
+        const double frac = len_ ? (double)pos_ / (double)len_ : 1.0;
+        const uint64_t per_sec = el > 0.0 ? (uint64_t)((double)pos_ / el) : 0;
+        const uint64_t eta = pos_ && per_sec ? (uint64_t)((double)(len_ - pos_) / (double)per_sec) : 0;
+        char tail[96];
+        snprintf(tail, sizeof tail, "] %d%% (%" PRIu64 "/s %s)", (int)(frac * 100.0), per_sec, hms(eta).c_str());
+        struct winsize ws{};
+        const int cols = ioctl(2, TIOCGWINSZ, &ws) == 0 && ws.ws_col ? ws.ws_col : 80;
+        const int width = std::max(1, cols - 14 - (int)strlen(tail));  // "T [hh:mm:ss] [" is 14 columns
+        const int fill = std::min(width, (int)(frac * width));
+        std::string done((size_t)fill, '#'), rest;
+        if (fill < width) {
+            done += '>';
+            rest.assign((size_t)(width - fill - 1), '-');
+        }
+        fprintf(stderr, "\r\x1b[2K\x1b[32m%s\x1b[0m [%s] [\x1b[36m%s\x1b[34m%s\x1b[0m%s", ticks[tick_++ % 8],
+                hms((uint64_t)el).c_str(), done.c_str(), rest.c_str(), tail);
+        fflush(stderr);
+        drawn_ = true;
+    }
+    uint64_t len_, pos_ = 0, last_pos_ = 0, updates_ = 0;
+    bool on_, drawn_ = false;
+    unsigned tick_ = 0;
+    std::chrono::steady_clock::time_point start_, last_;
+};
+
+// The LD pass's progress_report closure (main.rs:184-188): pb.set_position
+// per completed chunk, on the calling thread (wld_progress_fn)
+void on_progress(uint64_t pairs_done, void *user) { static_cast<ProgressBar *>(user)->set_position(pairs_done); }
 
 // Rust `{:.3}` of an f32 (main.rs:76,106): exact integer rounding, tsv_format.hpp
 using wld_tsv::fmt3;
@@ -304,6 +371,7 @@ int write_pair_stats(const std::string &path, const wld_pairs &p) {
     bool ok = fwrite(hdr, 1, strlen(hdr), f) == strlen(hdr);
     const uint64_t n = p.n, block = 1 << 16;
     const uint64_t n_blocks = (n + block - 1) / block;
+    ProgressBar pb(n);  // main.rs:89-97: set_position every 5000 rows written (main.rs:111-116)
     const unsigned nt =
         (unsigned)std::max<uint64_t>(1, std::min<uint64_t>({std::thread::hardware_concurrency(), 32, n_blocks}));
     const uint64_t n_slots = 2 * (uint64_t)nt;
@@ -364,6 +432,8 @@ int write_pair_stats(const std::string &path, const wld_pairs &p) {
             cv_ready.wait(lk, [&] { return sl.ready == b; });
         }
         if (ok && fwrite(sl.buf.data(), 1, sl.len, f) != sl.len) ok = false;
+        const uint64_t written = std::min(n, (b + 1) * block);
+        if (written / 5000 > b * block / 5000) pb.set_position(written / 5000 * 5000);
         {
             std::lock_guard<std::mutex> lk(mu);
             sl.ready = UINT64_MAX;
@@ -376,6 +446,13 @@ int write_pair_stats(const std::string &path, const wld_pairs &p) {
     for (auto &x : th) x.join();
     if (fclose(f) != 0) ok = false;
     return ok ? WLD_OK : WLD_E_IO;
+}
+
+// (debug level only, so info-level output is the reference's: the LD pass's
+// progress_report calls — progress(0), then one per 256x256 chunk)
+void log_progress(const ProgressBar &pb) {
+    log_at(4, "progress: %" PRIu64 " progress_report calls, last %" PRIu64 " pairs", pb.updates(),
+           pb.last_position());
 }
 
 // main.rs:186-212 after the pair computation: timing logs, TSV, clean-up.
@@ -429,8 +506,12 @@ int run_gpu_prepass(const Opt &opt, wld_siteset *siteset, wld_ctx *ctx) {
     sw = clk::now();
     const uint64_t total_pairs = ((uint64_t)L - 1) * ((uint64_t)L - 2) / 2;  // main.rs:168 (sic, wraps)
     wld_pairs pairs;  // any L: batches of <= 2^31 pairs, rows appended in reference order
-    if ((st = wld_run_host(ctx, opt.r2_threshold, nullptr, nullptr, &pairs)) != WLD_OK)
-        die(st, "all_weighted_ld_pairs");
+    {
+        ProgressBar pb(total_pairs);  // main.rs:170-178
+        if ((st = wld_run_host(ctx, opt.r2_threshold, on_progress, &pb, &pairs)) != WLD_OK)
+            die(st, "all_weighted_ld_pairs");
+        log_progress(pb);
+    }
     return finish(opt, ctx, pairs, clk::now() - sw, total_pairs);
 }
 
@@ -514,9 +595,13 @@ int main(int argc, char **argv) {
     const uint64_t total_pairs = ((uint64_t)L - 1) * ((uint64_t)L - 2) / 2;  // main.rs:168 (sic, wraps)
     get_ctx();
     wld_pairs pairs;
-    st = wld_all_weighted_ld_pairs(ctx, wld_siteset_buffer(filtered), L, N, wld_siteset_site_map(filtered),
-                                   weights.data(), opt.r2_threshold, nullptr, nullptr, &pairs);
-    if (st != WLD_OK) die(st, "all_weighted_ld_pairs");
+    {
+        ProgressBar pb(total_pairs);  // main.rs:170-178, fed by the closure of main.rs:184-188
+        st = wld_all_weighted_ld_pairs(ctx, wld_siteset_buffer(filtered), L, N, wld_siteset_site_map(filtered),
+                                       weights.data(), opt.r2_threshold, on_progress, &pb, &pairs);
+        if (st != WLD_OK) die(st, "all_weighted_ld_pairs");
+        log_progress(pb);
+    }
     const int rc = finish(opt, ctx, pairs, clk::now() - sw, total_pairs);
     wld_siteset_free(filtered);
     wld_siteset_free(siteset);

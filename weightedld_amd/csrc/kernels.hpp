@@ -40,7 +40,29 @@ struct OrderArgs {
     unsigned *prog_n;
     unsigned long long *prog_log;
     uint32_t L;  // sites of the loaded set (a chunk's pair count)
+    // guard word in mapped host memory (report_guard): a kernel that finds an
+    // index out of range (a candidate-list entry, a tile, a staged pair, a
+    // gather destination) records what it found here and skips the access
+    // instead of faulting the context; run_complete turns it into WLD_E_STATE
+    unsigned *guard;
 };
+
+// report_guard bits (wld_run_stats.guard and the WLD_E_STATE message)
+enum : unsigned {
+    kGuardEntry = 1u,   // a candidate-list entry outside the list's buckets
+    kGuardTile = 2u,    // a listed tile with ta > tb or tb past the set's last tile
+    kGuardPair = 4u,    // a staged candidate pair with a >= b or b past the set
+    kGuardSlice = 8u,   // a candidate slice outside staging or with a bad tile
+    kGuardGather = 16u  // a gather destination past the run's row count, or a source past staging
+};
+__device__ inline void report_guard(const OrderArgs &o, unsigned bit) {
+    if (o.guard) __hip_atomic_store(o.guard, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// a tile (ta << 16 | tb) the pair kernels may compute: ta <= tb < T_used
+__device__ inline bool tile_in_range(uint32_t tile, uint32_t L) {
+    const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
+    return ta <= tb && (uint64_t)tb * kTile < L;
+}
 
 // The run's chunk scan (order.hip): exclusive scan of the chunk totals
 // [lin_begin, lin_begin + count) into chunk_base; the row total into *total,
@@ -56,13 +78,22 @@ struct ScanArgs {
     uint32_t lin_begin, count;
     uint32_t *chunk_base;
     unsigned long long *total, *cursor, *host_out, *count_out;
-    unsigned *cand_count;  // {candidate tiles, their candidate sub-blocks}
-    unsigned *cand_buckets;  // the 16 bucket counts of the candidate list (zeroed too; may be null)
+    unsigned *cand_count;  // this pass's {candidate tiles, their candidate sub-blocks} (read)
+    // the OTHER candidate set (the next pass's: {count, sub-blocks} and 16
+    // bucket counts), zeroed here; this pass's set is never written by its
+    // own scan, so a workgroup still reading it cannot see it reset (capi.hip
+    // enqueue_pass alternates the sets by pass parity)
+    unsigned *cand_reset;
+    unsigned *cand_buckets_reset;
     unsigned *ticket;  // 0 between launches; null: the scan is launched on its own
 };
 
-// 64-bit words of a context's run counters (capi.hip enqueue_pass)
-constexpr uint32_t kCounterWords = 12;
+// 64-bit words of a context's run counters (capi.hip enqueue_pass):
+// {cursor, total, {ticket, work}, set 0: {candidates, sub-blocks} + 16 bucket
+// counts (9 words), set 1: the same}
+constexpr uint32_t kCounterWords = 21;
+constexpr uint32_t kCandSetWords = 9;
+constexpr uint32_t kCandSet0 = 3;
 
 struct DenseArgs {
     float *d, *dp, *r2;
@@ -210,9 +241,10 @@ void launch_progress_init(unsigned *chunk_left, uint32_t lin_begin, uint32_t cou
 void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t n_chunks, hipStream_t s);
 // the run's chunk scan as a launch of its own (ScanArgs; ticket unused)
 void launch_chunk_scan(const ScanArgs &a, hipStream_t s);
+// (rows: the run's row count, the bound of every destination)
 void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,
-                   uint32_t n_chunk_rows, uint32_t L, const uint32_t *site_map, uint32_t *out_a, uint32_t *out_b,
-                   float *out_d, float *out_dp, float *out_r2, hipStream_t s);
+                   uint32_t n_chunk_rows, uint32_t L, uint64_t rows, const uint32_t *site_map, uint32_t *out_a,
+                   uint32_t *out_b, float *out_d, float *out_dp, float *out_r2, hipStream_t s);
 
 // Linear index of chunk (row, col) in the reference's triu_index order
 // (lib.rs:623-632): rows descend, so row r starts at (n-1-r)(n-r)/2.

@@ -49,7 +49,7 @@ constexpr uint32_t kGatherRows = 16;
 
 __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t *__restrict__ chunk_base,
                                                       uint32_t lin_begin, uint32_t n_chunk_rows, uint32_t L,
-                                                      const uint32_t *__restrict__ site_map,
+                                                      uint64_t rows, const uint32_t *__restrict__ site_map,
                                                       uint32_t *__restrict__ out_a, uint32_t *__restrict__ out_b,
                                                       float *__restrict__ out_d, float *__restrict__ out_dp,
                                                       float *__restrict__ out_r2) {
@@ -96,6 +96,10 @@ __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t
         if (e < sCnt[r][s]) {
             const uint64_t src = (uint64_t)sOff[r][s] + e;
             const uint64_t dst = (uint64_t)sPre[r][s] + e;
+            if (dst >= rows || src >= o.st_capacity) {  // (the run's counts disagree: not written)
+                report_guard(o, kGuardGather);
+                continue;
+            }
             const uint32_t fa = o.st_a[src], fb = o.st_b[src];
             out_a[dst] = site_map ? site_map[fa] : fa;
             out_b[dst] = site_map ? site_map[fb] : fb;
@@ -138,12 +142,11 @@ void launch_chunk_scan(const ScanArgs &a, hipStream_t s) {
 }
 
 void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,
-                   uint32_t n_chunk_rows, uint32_t L, const uint32_t *site_map, uint32_t *out_a, uint32_t *out_b,
-                   float *out_d, float *out_dp, float *out_r2, hipStream_t s) {
+                   uint32_t n_chunk_rows, uint32_t L, uint64_t rows, const uint32_t *site_map, uint32_t *out_a,
+                   uint32_t *out_b, float *out_d, float *out_dp, float *out_r2, hipStream_t s) {
     if (!count) return;
     hipLaunchKernelGGL(gather_kernel, dim3(count, kChunk / kGatherRows), dim3(256), 0, s, o, chunk_base, lin_begin,
-                       n_chunk_rows, L,
-                       site_map, out_a, out_b, out_d, out_dp, out_r2);
+                       n_chunk_rows, L, rows, site_map, out_a, out_b, out_d, out_dp, out_r2);
 }
 
 }  // namespace wld

@@ -259,10 +259,12 @@ __device__ inline void chunk_scan_block(const ScanArgs &a) {
         if (a.cand_count) {
             cand = ld32(a.cand_count);
             blocks = ld32(a.cand_count + 1);
-            a.cand_count[0] = a.cand_count[1] = 0;
         }
-        if (a.cand_buckets)
-            for (int b = 0; b < 16; ++b) a.cand_buckets[b] = 0;
+        // the next pass's candidate set starts at 0 (nothing in this launch
+        // reads or writes it)
+        if (a.cand_reset) a.cand_reset[0] = a.cand_reset[1] = 0;
+        if (a.cand_buckets_reset)
+            for (int b = 0; b < 16; ++b) a.cand_buckets_reset[b] = 0;
         if (a.host_out) {
             a.host_out[0] = cur;
             a.host_out[1] = run;
@@ -313,6 +315,18 @@ __device__ inline uint32_t cand_entry(const uint32_t *s_pre, uint32_t cap, uint3
     while (b < 15 && s_pre[b + 1] <= u) ++b;
     return b * cap + (u - s_pre[b]);
 }
+// ... guarded: ~0u (and kGuardEntry reported) unless the u-th candidate lies
+// inside the buckets the screen filled (u below their total, its bucket slot
+// below the capacity)
+__device__ inline uint32_t cand_entry_checked(const OrderArgs &o, const uint32_t *s_pre, uint32_t cap, uint32_t u) {
+    uint32_t b = 0;
+    while (b < 15 && s_pre[b + 1] <= u) ++b;
+    if (u >= s_pre[16] || u - s_pre[b] >= cap) {
+        report_guard(o, kGuardEntry);
+        return ~0u;
+    }
+    return b * cap + (u - s_pre[b]);
+}
 
 // The end of every workgroup of a candidate launch (a grid-stride loop over
 // the screen's n_work candidate tiles).  With the scan fused (a.ticket set)
@@ -320,11 +334,15 @@ __device__ inline uint32_t cand_entry(const uint32_t *s_pre, uint32_t cap, uint3
 // run's chunk scan (with no candidate, workgroup 0 alone): one launch (and
 // its dispatch gap) less per run, and no ticket traffic in the common case.
 // What the scan reads from this launch — the chunk totals and the staging
-// cursor — only wave 0 writes (lane 63's atomics in the compaction), so wave
-// 0 waits for its memory operations before lane 0 takes the ticket, and the
-// last workgroup reads them with agent-scope loads (MI355X_MICROARCH.md,
-// inter-workgroup visibility: one lane per workgroup adding to one counter,
-// the last adder told by the returned value; no per-workgroup L2 write-back).
+// cursor — is written only by agent-scope atomics (lane 63's in the
+// compaction; an atomic leaves no copy of its line in the issuing XCD's L2).
+// Each writing wave waits for its atomics (s_waitcnt vmcnt(0)) before lane 0
+// takes the ticket; the winner then runs an agent-scope ACQUIRE (buffer_inv
+// sc1: no line of the run state cached in its CU's L1 or its XCD's L2
+// survives) before the scan's agent-scope loads (MI355X_MICROARCH.md,
+// inter-workgroup visibility).  The acquire is the last workgroup's alone;
+// no workgroup pays an L2 write-back.  WLD_OPT_FUSED_SCAN 0 runs the scan as
+// a launch of its own instead (the kernel boundary orders everything).
 // The screen before the launch only appended candidates (atomics, before the
 // kernel boundary).
 // (all_waves: every wave wrote what the scan reads, and drains before the ticket)
@@ -340,7 +358,13 @@ __device__ inline void scan_tail(const ScanArgs &a, uint32_t n_work, bool all_wa
     // every wave has drained (waves that work independently may still be
     // writing when wave 0 arrives) before the workgroup takes its ticket
     if (all_waves) __syncthreads();
-    if (threadIdx.x == 0) s_run = p <= 1 || atomicAdd(a.ticket, 1u) == p - 1;
+    if (threadIdx.x == 0) {
+        s_run = p <= 1 || atomicAdd(a.ticket, 1u) == p - 1;
+        if (s_run) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completed before the barrier
+        }
+    }
     __syncthreads();
     if (!s_run) return;
     if (threadIdx.x == 0 && p > 1) atomicExch(a.ticket, 0u);

@@ -595,7 +595,9 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
             }
         }
     }
-    if (tid == 0) tile_done(o, ta, tb, n_chunk_rows);
+    // (kModeRefPairs: the tile's candidates are summed and compacted by
+    // ref_sums / ref_compact, which reports the tile done after that)
+    if (MODE != kModeRefPairs && tid == 0) tile_done(o, ta, tb, n_chunk_rows);
 }
 
 // LDS-streaming kernel over fragment-major, selector-coded codes, one 64x64
@@ -748,7 +750,13 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
             // out of the loop and held live across the epilogue
             uint32_t tid = threadIdx.x;
             asm volatile("" : "+v"(tid));
-            compute_tile(tiles[cand_entry(s_pre, sc.cand_cap, bi)], tid);
+            // (the entry, then its tile, checked before anything is read through them)
+            const uint32_t e = cand_entry_checked(o, s_pre, sc.cand_cap, bi);
+            const uint32_t tile = e != ~0u ? tiles[e] : kNoTile;
+            if (tile_in_range(tile, L))
+                compute_tile(tile, tid);
+            else if (e != ~0u && threadIdx.x == 0)
+                report_guard(o, kGuardTile);
             if (threadIdx.x == 0) s_next = gridDim.x + atomicAdd(sc.cand_work, 1u);
             __syncthreads();  // (also: the next tile's first DMA reuses buffer 0 and the compaction state)
             bi = s_next;

@@ -72,8 +72,8 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
 __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) : 2) void pair_valu_kernel(
     const uint8_t *__restrict__ codes, const float *__restrict__ w, const uint8_t *__restrict__ site_ok,
-    const uint32_t *__restrict__ tiles, const unsigned *tile_count, const uint32_t *__restrict__ tile_bits,
-    unsigned *tile_work, const unsigned *tile_buckets, uint32_t bucket_cap,
+    const uint32_t *__restrict__ tiles, uint32_t n_tiles, const unsigned *tile_count,
+    const uint32_t *__restrict__ tile_bits, unsigned *tile_work, const unsigned *tile_buckets, uint32_t bucket_cap,
     uint32_t L, uint32_t NP, uint32_t flush,
     uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, OrderArgs o, DenseArgs dn, ScanArgs sa) {
     __shared__ __attribute__((aligned(16))) uint8_t sA[kTile * kStride];
@@ -442,6 +442,8 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
         const uint32_t tile = tiles[blockIdx.x];
         if (tile != kNoTile) compute_tile(tile, threadIdx.x, 0xFFFFu);  // kNoTile: padding of an XCD-ordered list
     } else {
+        // (the list entries come from the screen's atomics: each is checked —
+        // bucket slot, then the tile — before anything is read through it)
         // the first tile by workgroup id, the next ones from a work counter
         // (tile_work, zeroed by the screen): the workgroups that finish first
         // take the list's tail, not fixed ones (tiles differ in their computed
@@ -463,8 +465,12 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
         }
         if (tile_buckets && first < nt) cand_prefix(tile_buckets, s_pre);  // (a workgroup without a tile skips it)
         for (uint32_t bi = first; bi < nt;) {
-            const uint32_t e = tile_buckets ? cand_entry(s_pre, bucket_cap, bi) : bi;
-            compute_tile(tiles[e], threadIdx.x, tile_bits ? tile_bits[e] : 0xFFFFu);
+            const uint32_t e = tile_buckets ? cand_entry_checked(o, s_pre, bucket_cap, bi) : bi < n_tiles ? bi : ~0u;
+            const uint32_t tile = e != ~0u ? tiles[e] : kNoTile;
+            if (tile_in_range(tile, L))
+                compute_tile(tile, threadIdx.x, tile_bits ? tile_bits[e] : 0xFFFFu);
+            else if (e != ~0u && threadIdx.x == 0)
+                report_guard(o, kGuardTile);
             if (threadIdx.x == 0) s_next = gridDim.x + atomicAdd(tile_work, 1u);
             __syncthreads();  // (also: the next tile's staging and compaction reuse the LDS)
             bi = s_next;
@@ -576,11 +582,19 @@ __global__ __launch_bounds__(256) void ref_sums_kernel(RefRowsLaunch r, OrderArg
     const uint64_t n = min((uint64_t)*o.cursor, o.st_capacity);  // (an overflowing pass re-runs)
     const uint64_t threads = (uint64_t)gridDim.x * 256, gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t cls = r.ref_cls;
+    // a staged pair outside a < b < L is not read through (kGuardPair)
+    auto pair_ok = [&](uint32_t a, uint32_t b) {
+        const bool ok = a < b && b < o.L;
+        if (!ok) report_guard(o, kGuardPair);
+        return ok;
+    };
     if (n * 8 <= threads) {
         const uint64_t i = gid >> 3;
         if (i >= n) return;  // (a row's 8 lanes leave together)
         const uint32_t c = (uint32_t)(gid & 7);
-        const uint8_t *ra = r.rcodes + (size_t)o.st_a[i] * r.NPr, *rb = r.rcodes + (size_t)o.st_b[i] * r.NPr;
+        const uint32_t sa = o.st_a[i], sb = o.st_b[i];
+        if (!pair_ok(sa, sb)) return;  // (the row's 8 lanes alike)
+        const uint8_t *ra = r.rcodes + (size_t)sa * r.NPr, *rb = r.rcodes + (size_t)sb * r.NPr;
         float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f}, tot[4];
         ref_chain(ra, rb, r.rw, c * cls, (c + 1) * cls, acc);
         const int first = (int)(threadIdx.x & 63) & ~7;
@@ -600,7 +614,9 @@ __global__ __launch_bounds__(256) void ref_sums_kernel(RefRowsLaunch r, OrderArg
         return;
     }
     for (uint64_t i = gid; i < n; i += threads) {
-        const uint8_t *ra = r.rcodes + (size_t)o.st_a[i] * r.NPr, *rb = r.rcodes + (size_t)o.st_b[i] * r.NPr;
+        const uint32_t sa = o.st_a[i], sb = o.st_b[i];
+        if (!pair_ok(sa, sb)) continue;
+        const uint8_t *ra = r.rcodes + (size_t)sa * r.NPr, *rb = r.rcodes + (size_t)sb * r.NPr;
         float tot[4] = {0.0f, 0.0f, 0.0f, 0.0f};
         for (uint32_t k = 0; k < (cls ? 8u : 0u); ++k) {
             float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -632,7 +648,9 @@ __global__ __launch_bounds__(256) void ref_compact_kernel(RefRowsLaunch r, Order
     for (uint32_t si = 4 * blockIdx.x + wv; si < ns;) {
         const uint32_t base = r.slices[3 * si], total = r.slices[3 * si + 1], tile = r.slices[3 * si + 2];
         const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu, a0 = ta * kTile;
-        if ((uint64_t)base + total <= o.st_capacity) {  // else not stored: the pass re-runs
+        if (!tile_in_range(tile, o.L) || total > kTile * kTile) {
+            if (lane == 0) report_guard(o, kGuardSlice);
+        } else if ((uint64_t)base + total <= o.st_capacity) {  // else not stored: the pass re-runs
             cnt[lane] = 0;
             uint32_t kept = 0;
             for (uint32_t c0 = 0; c0 < total; c0 += 64) {
@@ -661,6 +679,9 @@ __global__ __launch_bounds__(256) void ref_compact_kernel(RefRowsLaunch r, Order
                 atomicSub(&o.chunk_total[chunk_linear(r.n_chunk_rows, ta / kTilesPerChunk, tb / kTilesPerChunk)],
                           total - kept);
         }
+        // the tile is finished now (per-chunk progress: its candidates are
+        // summed and compacted; tile_epilogue left it to this kernel)
+        if (lane == 0 && tile_in_range(tile, o.L)) tile_done(o, ta, tb, r.n_chunk_rows);
         si += 4 * gridDim.x;  // (static: tens of thousands of small slices would queue on one work counter)
     }
     // every wave's atomics (chunk totals) are drained before the ticket
@@ -695,8 +716,8 @@ template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
 void launch_v(const ValuLaunch &v, uint32_t grid, uint32_t flush, uint32_t cs, const OrderArgs &o,
               const DenseArgs &dn, hipStream_t s) {
     hipLaunchKernelGGL((pair_valu_kernel<DENSE, SAFE, MF, REF, LOOP>), dim3(grid), dim3(256), 0, s, v.codes, v.w,
-                       v.site_ok, v.tiles, v.tile_count, v.tile_bits, v.tile_work, v.tile_buckets, v.bucket_cap, v.L, v.NP, flush, cs, v.ref_tail_n, v.n_chunk_rows, v.thr, o,
-                       dn, v.scan);
+                       v.site_ok, v.tiles, v.n_tiles, v.tile_count, v.tile_bits, v.tile_work, v.tile_buckets,
+                       v.bucket_cap, v.L, v.NP, flush, cs, v.ref_tail_n, v.n_chunk_rows, v.thr, o, dn, v.scan);
 }
 }  // namespace
 

@@ -64,7 +64,10 @@ class RowGather:
     """Per-step gather of every rank's [5, n_r] rows to rank 0, with the
     count exchange on persistent buffers: one all_gather_into_tensor of the
     int64 counts (no host-to-device tensor build, no list of outputs) and one
-    host read of the result; only when some rank has rows, one padded gather.
+    host read of the result; only when some rank has rows, one group of
+    exact-size point-to-point transfers: each rank with rows
+    sends its n_r rows, rank 0 receives each into a buffer of that size
+    (batch_isend_irecv: one RCCL group; no padding to the largest count).
     Rank 0 gets the [5, sum n_r] concatenation in reference order (shards in
     descending rank order), other ranks None."""
 
@@ -86,17 +89,28 @@ class RowGather:
             self.cnt.fill_(packed.shape[1])
             dist.all_gather_into_tensor(self.cnts, self.cnt, group=self.group)
             counts = self.cnts.tolist()  # the one host sync of a step without rows
-        m = max(counts)
-        if m == 0:
+        counts = [int(c) for c in counts]
+        if max(counts) == 0:
             return packed[:, :0] if self.rank == 0 else None
-        if packed.shape[1] < m:
-            pad = torch.zeros((5, m - packed.shape[1]), dtype=torch.int32, device=packed.device)
-            packed = torch.cat([packed, pad], dim=1)
-        gl = [torch.empty_like(packed) for _ in range(self.world)] if self.rank == 0 else None
-        dist.gather(packed.contiguous(), gl, dst=0, group=self.group)
+        peer = (lambda r: dist.get_global_rank(self.group, r)) if self.group is not None else (lambda r: r)
         if self.rank != 0:
+            n = counts[self.rank]
+            if n:
+                assert packed.shape[1] >= n, (packed.shape, n)
+                for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, packed[:, :n].contiguous(), peer(0),
+                                                            group=self.group)]):
+                    w.wait()
             return None
-        return torch.cat([gl[g][:, :counts[g]] for g in reversed(range(self.world))], dim=1)
+        parts = {0: packed[:, :counts[0]]}
+        ops = []
+        for r in range(1, self.world):
+            if counts[r]:
+                parts[r] = torch.empty((5, counts[r]), dtype=torch.int32, device=packed.device)
+                ops.append(dist.P2POp(dist.irecv, parts[r], peer(r), group=self.group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        return torch.cat([parts[r] for r in reversed(range(self.world)) if r in parts], dim=1)
 
 
 class _HostStream:
