@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256) void progress_init_kernel(unsigned *__restrict
     chunk_of_linear(n_chunk_rows, lin_begin + i, row, col);
     const uint32_t ra = min(T_used - min(T_used, row * kTilesPerChunk), (uint32_t)kTilesPerChunk);
     const uint32_t rb = min(T_used - min(T_used, col * kTilesPerChunk), (uint32_t)kTilesPerChunk);
-    chunk_left[lin_begin + i] = row == col ? ra * (ra + 1) / 2 : ra * rb;
+    chunk_left[lin_begin + i] = (row == col ? ra * (ra + 1) / 2 : ra * rb) * kTileQuarters;  // (tile_done)
 }
 
 void launch_progress_init(unsigned *chunk_left, uint32_t lin_begin, uint32_t count, uint32_t n_chunk_rows, uint32_t L,

@@ -183,14 +183,18 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
 }
 
-// A tile of the run is finished (one thread of its workgroup): with per-chunk
-// progress on, the workgroup that finishes its chunk's last tile appends the
-// chunk's pair count to the host log (the value lib.rs's per-chunk
-// fetch_add adds, lib.rs:670-671; the host sums the log in slot order).
-__device__ __forceinline__ void tile_done(const OrderArgs &o, uint32_t ta, uint32_t tb, uint32_t n_chunk_rows) {
+// A tile (or part of one) of the run is finished (one thread of its
+// workgroup): with per-chunk progress on, the workgroup that finishes its
+// chunk's last tile appends the chunk's pair count to the host log (the value
+// lib.rs's per-chunk fetch_add adds, lib.rs:670-671; the host sums the log in
+// slot order).  A chunk counts kTileQuarters per tile (progress_init_kernel):
+// a work item that finishes q of a tile's four 16-row blocks counts q.
+constexpr uint32_t kTileQuarters = 4;
+__device__ __forceinline__ void tile_done(const OrderArgs &o, uint32_t ta, uint32_t tb, uint32_t n_chunk_rows,
+                                          uint32_t quarters = kTileQuarters) {
     if (!o.chunk_left) return;
     const uint32_t row = ta / kTilesPerChunk, col = tb / kTilesPerChunk;
-    if (atomicSub(&o.chunk_left[chunk_linear(n_chunk_rows, row, col)], 1u) == 1u) {
+    if (atomicSub(&o.chunk_left[chunk_linear(n_chunk_rows, row, col)], quarters) == quarters) {
         const unsigned slot = atomicAdd(o.prog_n, 1u);
         __hip_atomic_store(&o.prog_log[slot], (unsigned long long)chunk_pairs(o.L, row, col), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);

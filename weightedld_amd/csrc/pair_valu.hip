@@ -69,13 +69,21 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 #ifndef WLD_VALU_REF_WG
 #define WLD_VALU_REF_WG 3  // MF + REF: three workgroups per CU (<= 168 VGPRs; 2 leave 208)
 #endif
-template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
-__global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) : 2) void pair_valu_kernel(
+#ifndef WLD_VALU_REF1_WG
+#define WLD_VALU_REF1_WG 6  // MF + REF, one slot per wave: six workgroups per CU (<= 85 VGPRs)
+#endif
+// NS: 16x16 slots per wave (4: a whole 64x64 tile per workgroup; 1, MF +
+// REF only: one 16-row block of a tile per workgroup, one sub-block per wave —
+// a quarter of the accumulators, so more workgroups fit a CU)
+template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP, int NS = 4>
+__global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? WLD_VALU_REF1_WG : WLD_VALU_REF_WG) : WLD_VALU_MF_WG)
+                                     : 2) void pair_valu_kernel(
     const uint8_t *__restrict__ codes, const float *__restrict__ w, const uint8_t *__restrict__ site_ok,
     const uint32_t *__restrict__ tiles, uint32_t n_tiles, const unsigned *tile_count,
     const uint32_t *__restrict__ tile_bits, unsigned *tile_work, const unsigned *tile_buckets, uint32_t bucket_cap,
     uint32_t L, uint32_t NP, uint32_t flush,
-    uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, OrderArgs o, DenseArgs dn, ScanArgs sa) {
+    uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, uint32_t split, OrderArgs o, DenseArgs dn,
+    ScanArgs sa) {
     __shared__ __attribute__((aligned(16))) uint8_t sA[kTile * kStride];
     __shared__ __attribute__((aligned(16))) uint8_t sB[kTile * kStride];
     __shared__ __attribute__((aligned(16))) float sW[64];
@@ -83,29 +91,34 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
     __shared__ uint32_t sRowBase[kTile];
 
     // bits: the 16x16 sub-blocks whose pairs are computed (bit 4 (a / 16) +
-    // b / 16); the others' pairs provably fail (the screen's bound)
-    auto compute_tile = [&](uint32_t tile, uint32_t tid, uint32_t bits) {
+    // b / 16); the others' pairs provably fail (the screen's bound).  owned:
+    // the tile's 16-row blocks whose segment counts this work item writes (a
+    // tile split over several items gives each its own row blocks)
+    auto compute_tile = [&](uint32_t tile, uint32_t tid, uint32_t bits, uint32_t owned) {
         const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
         const uint32_t a0 = ta * kTile, b0 = tb * kTile;
         const uint32_t tx = tid & 15, ty = tid >> 4;
 
-        float acc[4][4][4], tot[4][4][4];
-        v4f accM[4][4];  // MF: [slot j][sum q], element e = a row slot
+        static_assert(NS == 4 || (MF && REF), "one slot per wave: the f32 MFMA reference-order path only");
+        float acc[4][4][4], tot[4][NS][4];
+        v4f accM[NS][4];  // MF: [slot j][sum q], element e = a row slot
         // MF + REF: the computed sub-blocks dealt over the waves.  In
         // column-major order (k = 4 n + i: a rows 16 i.., b columns 16 n..)
         // the u-th computed one goes to wave u % 4, slot u / 4: the stage
         // barriers pace a tile by its busiest wave, and a diagonal tile's 10
         // sub-blocks then take 3 slots on it instead of 4; all 16 give wave w
         // the a rows 16 w.. against b block j in slot j.
-        uint32_t ui[4] = {0, 0, 0, 0}, un[4] = {0, 1, 2, 3};
-        bool us[4] = {true, true, true, true};
+        uint32_t ui[NS], un[NS];
+        bool us[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) ui[j] = 0, un[j] = j, us[j] = true;
         if constexpr (MF && REF) {
             const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
             uint32_t cm = 0;
             for (uint32_t k = 0; k < 16; ++k) cm |= ((bits >> (4 * (k & 3) + (k >> 2))) & 1u) << k;
             cm = __builtin_amdgcn_readfirstlane(cm);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < NS; ++j) {
                 uint32_t m = cm;
                 for (uint32_t t = 0; t < 4 * (uint32_t)j + wave; ++t) m &= m - 1u;  // drop the first 4j + w
                 const uint32_t k = m ? (uint32_t)__builtin_ctz(m) : 0u;
@@ -126,7 +139,7 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < NS; ++j)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) tot[i][j][q] = 0.0f;
 
@@ -134,11 +147,21 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
         const uint8_t *gA = codes + (size_t)(a0 + lr) * NP + part * 16;
         const uint8_t *gB = codes + (size_t)(b0 + lr) * NP + part * 16;
 
-        // one 64-sequence stage of both panels' codes and the weights into LDS
-        auto load_stage = [&](uint32_t k0) {
-            const uint4 va = *reinterpret_cast<const uint4 *>(gA + k0);
-            const uint4 vb = *reinterpret_cast<const uint4 *>(gB + k0);
-            const float wv = tid < 64 ? w[k0 + tid] : 0.0f;
+        // one 64-sequence stage of both panels' codes and the weights: fetch
+        // (global loads into registers, issued a stage ahead so that their
+        // latency overlaps the previous stage's MFMAs), then store (into LDS).
+        // PF: the fetch a stage ahead; a whole tile per workgroup in lib.rs's
+        // order has no registers to spare for it (it would spill), and fetches
+        // each stage just before storing it
+        constexpr bool PF = !(REF && NS == 4);
+        uint4 va, vb;
+        float wv;
+        auto fetch_stage = [&](uint32_t k0) {
+            va = *reinterpret_cast<const uint4 *>(gA + k0);
+            vb = *reinterpret_cast<const uint4 *>(gB + k0);
+            wv = tid < 64 ? w[k0 + tid] : 0.0f;
+        };
+        auto store_stage = [&]() {
             __syncthreads();
             uint32_t *pa = reinterpret_cast<uint32_t *>(sA + lr * kStride + part * 16);
             uint32_t *pb = reinterpret_cast<uint32_t *>(sB + lr * kStride + part * 16);
@@ -161,7 +184,7 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
                     const float we[4] = {w4.x, w4.y, w4.z, w4.w};
                     float u[4], v[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
+                    for (int j = 0; j < NS; ++j) {
                         if (!us[j]) continue;  // (slots fill in order: us[j] implies us[j - 1])
                         if (j == 0 || ui[j] != ui[j - 1]) {  // a rows of a new row block (all 16: slot 0 only)
                             const uint32_t a4 =
@@ -284,7 +307,7 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < NS; ++j)
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         if constexpr (MF) accM[j][q][i] = 0.0f;
@@ -295,19 +318,25 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < NS; ++j)
 #pragma unroll
                     for (int q = 0; q < 4; ++q) tot[i][j][q] += MF ? accM[j][q][i] : acc[i][j][q];
         };
 
         if constexpr (REF) {
             // the eight lane classes, each a chain from 0 folded into the
-            // ordered horizontal sum; then the tail stage on that sum
+            // ordered horizontal sum; then the tail stage on that sum.  The
+            // stages are consecutive (class c's are [c cls, (c + 1) cls), the
+            // tail's 8 cls), so each stage's fetch is issued before the
+            // previous stage's compute.
             const uint32_t cls = 64 * ref_cs;
+            if (PF && (ref_cs || ref_tail_n)) fetch_stage(0);
             for (uint32_t c = 0; c < (ref_cs ? 8u : 0u); ++c) {
                 acc_zero();
                 for (uint32_t k0 = c * cls; k0 < (c + 1) * cls; k0 += 64) {
-                    load_stage(k0);
+                    if (!PF) fetch_stage(k0);
+                    store_stage();
+                    if (PF && (k0 + 64 < 8 * cls || ref_tail_n)) fetch_stage(k0 + 64);
                     compute_stage();
                 }
                 acc_fold();
@@ -316,13 +345,14 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
                 // the scalar tail (lib.rs:461-480): its <= 7 sequences added
                 // onto the horizontal sums one by one, in order, on the VALU
                 // (fmaf(u, f, tot) = tot + u f rounded once: u f is exact)
-                load_stage(8 * cls);
+                if (!PF) fetch_stage(8 * cls);
+                store_stage();
                 for (uint32_t t = 0; t < ref_tail_n; ++t) {
                     const float we = sW[t];
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) {
+                        for (int j = 0; j < NS; ++j) {
                             const uint32_t ca = sA[pa(i, j) * kStride + t], cb = sB[pb(i, j) * kStride + t];
                             const float u = (ca & kCodeIn) ? we : 0.0f;
                             const float v = (ca & kCodeMaj) ? we : 0.0f;
@@ -344,10 +374,12 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
             }
         } else {
             // blocks of `flush` stages
+            fetch_stage(0);
             for (uint32_t k0 = 0; k0 < NP; k0 += 64 * flush) {
                 acc_zero();
                 for (uint32_t k1 = k0; k1 < min(NP, k0 + 64 * flush); k1 += 64) {
-                    load_stage(k1);
+                    store_stage();
+                    if (k1 + 64 < NP) fetch_stage(k1 + 64);
                     compute_stage();
                 }
                 acc_fold();
@@ -356,11 +388,11 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
 
         // ---- epilogue ------------------------------------------------------
         uint32_t passmask[4] = {0, 0, 0, 0};  // bit j per row slot i
-        float res[4][4][3];
+        float res[4][NS][3];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < NS; ++j) {
                 const uint32_t al = pa(i, j), bl = pb(i, j), a = a0 + al, b = b0 + bl;
                 float d, dp, r2;
                 ld_epilogue(tot[i][j][0], tot[i][j][1], tot[i][j][2], tot[i][j][3], d, dp, r2);
@@ -388,9 +420,11 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
 
         // ---- compaction: a 64x64 pass-bit matrix in LDS, rows in b order ----
         // (a tile with no passing pair writes only its 64 zero counts)
+        const bool own_row = tid < kTile && ((owned >> (tid >> 4)) & 1u);  // (row tid: its 16-row block)
+        const uint32_t quarters = (uint32_t)__popc(owned);
         if (!__syncthreads_or((passmask[0] | passmask[1] | passmask[2] | passmask[3]) != 0)) {
-            if (tid < kTile) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
-            if (tid == 0) tile_done(o, ta, tb, n_chunk_rows);
+            if (own_row) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
+            if (tid == 0) tile_done(o, ta, tb, n_chunk_rows, quarters);
             return;
         }
         if (tid < kTile) sBits[tid] = 0ull;
@@ -398,7 +432,7 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < NS; ++j)
                 if (passmask[i] & (1u << j)) atomicOr(&sBits[pa(i, j)], 1ull << pb(i, j));
         __syncthreads();
         if (tid < kTile) {
@@ -412,8 +446,10 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
             base = __shfl(base, 63, 64);
             sRowBase[r] = (uint32_t)base + excl;
             const uint32_t a = a0 + r;
-            o.seg_cnt[(size_t)a * o.T + tb] = (uint8_t)cnt;
-            o.seg_off[(size_t)a * o.T + tb] = (uint32_t)base + excl;
+            if (own_row) {  // (a row outside the item's blocks has no pass: cnt 0)
+                o.seg_cnt[(size_t)a * o.T + tb] = (uint8_t)cnt;
+                o.seg_off[(size_t)a * o.T + tb] = (uint32_t)base + excl;
+            }
             if (r == 63 && total)
                 atomicAdd(&o.chunk_total[chunk_linear(n_chunk_rows, ta / kTilesPerChunk, tb / kTilesPerChunk)], total);
         }
@@ -422,7 +458,7 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
         for (int i = 0; i < 4; ++i) {
             if (!passmask[i]) continue;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < NS; ++j) {
                 if (!(passmask[i] & (1u << j))) continue;
                 const uint32_t al = pa(i, j), bl = pb(i, j);
                 const uint64_t pos = (uint64_t)sRowBase[al] + __popcll(sBits[al] & ((1ull << bl) - 1ull));
@@ -435,12 +471,16 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
                 }
             }
         }
-        if (tid == 0) tile_done(o, ta, tb, n_chunk_rows);
+        if (tid == 0) tile_done(o, ta, tb, n_chunk_rows, quarters);
     };
 
     if constexpr (!LOOP) {
-        const uint32_t tile = tiles[blockIdx.x];
-        if (tile != kNoTile) compute_tile(tile, threadIdx.x, 0xFFFFu);  // kNoTile: padding of an XCD-ordered list
+        // split 4 (REF, few tiles): workgroup 4t + q computes tile t's 16-row
+        // block q (its four 16x16 sub-blocks, one per wave) — four times the
+        // work items where one tile per workgroup would leave CUs idle
+        const uint32_t tile = tiles[blockIdx.x / split], q = blockIdx.x % split;
+        if (tile != kNoTile)  // kNoTile: padding of an XCD-ordered list
+            compute_tile(tile, threadIdx.x, split == 1 ? 0xFFFFu : 0xFu << (4 * q), split == 1 ? 0xFu : 1u << q);
     } else {
         // (the list entries come from the screen's atomics: each is checked —
         // bucket slot, then the tile — before anything is read through it)
@@ -468,7 +508,7 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
             const uint32_t e = tile_buckets ? cand_entry_checked(o, s_pre, bucket_cap, bi) : bi < n_tiles ? bi : ~0u;
             const uint32_t tile = e != ~0u ? tiles[e] : kNoTile;
             if (tile_in_range(tile, L))
-                compute_tile(tile, threadIdx.x, tile_bits ? tile_bits[e] : 0xFFFFu);
+                compute_tile(tile, threadIdx.x, tile_bits ? tile_bits[e] : 0xFFFFu, 0xFu);
             else if (e != ~0u && threadIdx.x == 0)
                 report_guard(o, kGuardTile);
             if (threadIdx.x == 0) s_next = gridDim.x + atomicAdd(tile_work, 1u);
@@ -712,12 +752,12 @@ void launch_ref_layout(const uint8_t *codes, const float *w_pad, size_t LP, size
 }
 
 namespace {
-template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
+template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP, int NS = 4>
 void launch_v(const ValuLaunch &v, uint32_t grid, uint32_t flush, uint32_t cs, const OrderArgs &o,
-              const DenseArgs &dn, hipStream_t s) {
-    hipLaunchKernelGGL((pair_valu_kernel<DENSE, SAFE, MF, REF, LOOP>), dim3(grid), dim3(256), 0, s, v.codes, v.w,
+              const DenseArgs &dn, hipStream_t s, uint32_t split = 1) {
+    hipLaunchKernelGGL((pair_valu_kernel<DENSE, SAFE, MF, REF, LOOP, NS>), dim3(grid * split), dim3(256), 0, s, v.codes, v.w,
                        v.site_ok, v.tiles, v.n_tiles, v.tile_count, v.tile_bits, v.tile_work, v.tile_buckets,
-                       v.bucket_cap, v.L, v.NP, flush, cs, v.ref_tail_n, v.n_chunk_rows, v.thr, o, dn, v.scan);
+                       v.bucket_cap, v.L, v.NP, flush, cs, v.ref_tail_n, v.n_chunk_rows, v.thr, split, o, dn, v.scan);
 }
 }  // namespace
 
@@ -738,7 +778,11 @@ void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
             if (v.safe) launch_v<false, true, false, true, true>(v, grid, flush, cs, o, dn, s);
             else launch_v<false, false, true, true, true>(v, grid, flush, cs, o, dn, s);
         } else {
+            // every tile of the run: with fewer tiles than four rounds of
+            // resident workgroups (BASELINE config 2: 528 tiles), each tile's
+            // four 16-row blocks are separate work items (f32 MFMA path)
             if (v.safe) launch_v<false, true, false, true, false>(v, grid, flush, cs, o, dn, s);
+            else if (v.n_tiles <= 4 * kRefCandidateGrid) launch_v<false, false, true, true, false, 1>(v, grid, flush, cs, o, dn, s, 4);
             else launch_v<false, false, true, true, false>(v, grid, flush, cs, o, dn, s);
         }
         return;
