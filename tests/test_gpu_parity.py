@@ -882,6 +882,36 @@ def test_progress_once_per_chunk_config2(W, devices):
 
 
 
+@pytest.mark.parametrize("thr,screen", [(0.05, 1), (0.002, 4)], ids=["screen_items", "candidate_pairs"])
+def test_progress_once_per_chunk_screened(W, thr, screen):
+    """Per-chunk progress through the screened paths on linkage-block data:
+    at 0.05 the i8 screen and the f32 candidate launch over 16-row-block items
+    (a chunk finishes when the screen's rejected row blocks and every item's
+    row block are done), at 0.002 the exact candidate pairs (a tile is done
+    after ref_compact).  One callback per chunk, values in lib.rs's fetch_add
+    sequence; the rows equal the oracle's bit for bit."""
+    sys_path_bench()
+    from bench import chunk_pairs, ld_blocks
+    L, N = 3000, 600
+    buf = ld_blocks(L, N)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ctx = W.Context(0)
+    ctx.set_option("screen", screen)
+    seen = []
+    store = W.all_weighted_ld_pairs(W.SiteSet.from_buffer(buf), w, thr, progress_report=seen.append, ctx=ctx)
+    st = ctx.stats()
+    assert st["screened"] == screen and st["candidate_tiles"] > 0, st
+    n_chunks = ctx.chunks(L)
+    assert len(seen) == 1 + n_chunks and seen[0] == 0 and seen == sorted(seen)
+    steps = sorted(np.diff(seen[1:]).tolist() + [L * (L - 1) // 2 - seen[-1]])
+    assert steps == sorted(chunk_pairs(L, i) for i in range(n_chunks))
+    ref = O.all_pairs(buf, w, np.float32(thr))
+    assert len(store) == len(ref["r2"]) > 0
+    assert np.array_equal(store.site_a.astype(np.uint64), ref["site_a"])
+    assert np.array_equal(store.r2.view(np.uint32), ref["r2"].view(np.uint32))
+    ctx.close()
+
+
 # ------------------------------------------------------------------ CLI progress bars (main.rs:89-116, 170-190)
 def _write_c2_fasta(path):
     sys_path_bench()
@@ -893,34 +923,16 @@ def _write_c2_fasta(path):
             f.write(b">s%d\n" % k + lut[codes[:, k]].tobytes() + b"\n")
 
 
-def _run_cli_pty(cmd, env):
-    """Runs the CLI with stderr on a pseudo-terminal (as an interactive shell
-    would): returns (exit status, everything written to the terminal)."""
-    import pty
-    master, slave = pty.openpty()
-    p = subprocess.Popen(cmd, stdin=subprocess.DEVNULL, stdout=subprocess.DEVNULL, stderr=slave, env=env)
-    os.close(slave)
-    out = b""
-    while True:
-        try:
-            data = os.read(master, 65536)
-        except OSError:
-            break
-        if not data:
-            break
-        out += data
-    os.close(master)
-    return p.wait(timeout=120), out
-
-
 @pytest.mark.parametrize("prepass", [False, True], ids=["host_prepass", "gpu_prepass"])
 def test_cli_progress_bars(tmp_path, prepass):
     """The CLI feeds the LD pass's progress_report closure (main.rs:184-188) to
     a progress bar: at BASELINE config 2 (36 chunks) the closure is called 37
     times (progress(0), then one per chunk; logged at debug level).  The bars
     (LD pass and TSV write, indicatif's template) are drawn only when info is
-    enabled AND stderr is a terminal; the TSV is byte-identical either way, and
-    with stderr on a pipe the log lines carry no bar."""
+    enabled AND stderr is a terminal (here forced with the CLI's test hook
+    WLD_FORCE_PROGRESS_BAR: the GPU box has no pseudo-terminals); the TSV is
+    byte-identical either way, and with stderr on a pipe the log lines carry
+    no bar."""
     fa = tmp_path / "c2.fasta"
     _write_c2_fasta(fa)
     extra = ["--gpu-prepass"] if prepass else []
@@ -938,14 +950,23 @@ def test_cli_progress_bars(tmp_path, prepass):
     assert int(m.group(1)) == 37
     assert 0 < int(m.group(2)) < 2000 * 1999 // 2  # the last value: every pair but the last chunk's
     assert "\x1b[2K" not in r.stderr and "pairs computed at" in r.stderr
-    # info level on a terminal: bar frames on stderr, same TSV
-    rc, term = _run_cli_pty(cmd(tmp_path / "b.tsv"), dict(env, RUST_LOG="info"))
-    assert rc == 0, term[-2000:]
-    text = term.decode("utf-8", "replace")
-    assert "\x1b[2K" in text and re.search(r"\] \d+% \(\d+/s \d\d:\d\d:\d\d\)", text), text[-2000:]
-    assert "pairs computed at" in text
+    # info level on a terminal: bar frames on stderr, same TSV, and the same
+    # log lines once the frames are taken out
+    r2 = subprocess.run(cmd(tmp_path / "b.tsv"), capture_output=True, text=True, timeout=120,
+                        env=dict(env, RUST_LOG="info", WLD_FORCE_PROGRESS_BAR="1"))
+    assert r2.returncode == 0, r2.stderr[-2000:]
+    assert "\x1b[2K" in r2.stderr and re.search(r"\] \d+% \(\d+/s \d\d:\d\d:\d\d\)", r2.stderr), r2.stderr[-2000:]
     assert (tmp_path / "b.tsv").read_bytes() == (tmp_path / "a.tsv").read_bytes()
-    # warn level on a terminal: no bar (log_enabled!(Level::Info) is false)
-    rc, term = _run_cli_pty(cmd(tmp_path / "c.tsv"), dict(env, RUST_LOG="warn"))
-    assert rc == 0 and b"\x1b[2K" not in term and b"%" not in term, term[-2000:]
+    plain = subprocess.run(cmd(tmp_path / "d.tsv"), capture_output=True, text=True, timeout=120,
+                           env=dict(env, RUST_LOG="info"))
+    # a frame is "\r\x1b[2K\x1b[32m<spinner>...", up to the next frame or the clear "\r\x1b[2K"
+    unbar = lambda t: re.sub(r"\r\x1b\[2K", "", re.sub(r"\r\x1b\[2K\x1b\[32m[^\r\n]*", "", t))  # noqa: E731
+    strip = lambda t: [re.sub(r"\[\S+Z ", "[", ln) for ln in unbar(t).splitlines()]  # noqa: E731
+    assert "\x1b[2K" not in plain.stderr
+    keep = lambda t: [ln for ln in strip(t) if not re.search(r"computed at| in \d|Writing output", ln)]  # noqa: E731
+    assert keep(r2.stderr) == keep(plain.stderr) and len(keep(plain.stderr)) >= 3, (keep(r2.stderr), keep(plain.stderr))
+    # warn level: no bar (log_enabled!(Level::Info) is false)
+    r3 = subprocess.run(cmd(tmp_path / "c.tsv"), capture_output=True, text=True, timeout=120,
+                        env=dict(env, RUST_LOG="warn", WLD_FORCE_PROGRESS_BAR="1"))
+    assert r3.returncode == 0 and "\x1b[2K" not in r3.stderr and "%" not in r3.stderr, r3.stderr[-2000:]
     assert (tmp_path / "c.tsv").read_bytes() == (tmp_path / "a.tsv").read_bytes()

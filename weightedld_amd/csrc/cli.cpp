@@ -110,10 +110,13 @@ std::string human(double v, const char *units = "") {
 // is a terminal (indicatif's stderr target draws nothing otherwise), at most
 // 15 frames a second; dropped unfinished, it clears its line.  So TSVs and
 // log lines are byte-identical whether or not a bar was drawn.
+// (WLD_FORCE_PROGRESS_BAR=1 draws on a non-terminal stderr too: the tests'
+// hook, where no pseudo-terminal is available.)
 class ProgressBar {
   public:
     explicit ProgressBar(uint64_t len)
-        : len_(len), on_(g_level >= 3 && isatty(2)), start_(std::chrono::steady_clock::now()), last_(start_) {}
+        : len_(len), on_(g_level >= 3 && (isatty(2) || forced())), start_(std::chrono::steady_clock::now()),
+          last_(start_) {}
     ~ProgressBar() {
         if (on_ && drawn_) fputs("\r\x1b[2K", stderr), fflush(stderr);
     }
@@ -131,6 +134,10 @@ class ProgressBar {
     uint64_t last_position() const { return last_pos_; }
 
   private:
+    static bool forced() {
+        const char *e = getenv("WLD_FORCE_PROGRESS_BAR");
+        return e && *e == '1';
+    }
     static std::string hms(uint64_t secs) {
         char b[32];
         snprintf(b, sizeof b, "%02" PRIu64 ":%02" PRIu64 ":%02" PRIu64, secs / 3600, secs / 60 % 60, secs % 60);
@@ -508,6 +515,7 @@ int run_gpu_prepass(const Opt &opt, wld_siteset *siteset, wld_ctx *ctx) {
     wld_pairs pairs;  // any L: batches of <= 2^31 pairs, rows appended in reference order
     {
         ProgressBar pb(total_pairs);  // main.rs:170-178
+        on_progress(0, &pb);  // all_weighted_ld_pairs' initial report (lib.rs:584); wld_run_host reports chunks only
         if ((st = wld_run_host(ctx, opt.r2_threshold, on_progress, &pb, &pairs)) != WLD_OK)
             die(st, "all_weighted_ld_pairs");
         log_progress(pb);

@@ -139,6 +139,9 @@ struct ValuLaunch {
     const unsigned *tile_buckets;
     uint32_t bucket_cap;
     ScanArgs scan;        // tile_count launches: the run's scan fused into the last workgroup (ticket set)
+    // tile_count launches: the list's entries are 16-row blocks of candidate
+    // tiles (pair_mfma.hip ScreenArgs::rb_items), counted by the buckets
+    bool rb_items;
 };
 void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
 // The candidate pairs a kModeRefPairs launch (pair_mfma.hip) staged: summed in
@@ -188,6 +191,8 @@ constexpr uint32_t kCandidateGrid = 2048;
 // workgroups (three per CU, 256 CUs); extra workgroups would only queue (and
 // cost dispatch time when there is no candidate at all)
 constexpr uint32_t kRefCandidateGrid = 768;
+// ... and of its 16-row-block items (one sub-block per wave: five per CU)
+constexpr uint32_t kRefItemGrid = 1280;
 // ... and of ref_sums_kernel / ref_compact_kernel (low-register: eight per CU)
 constexpr uint32_t kRefRowsGrid = 2048;
 

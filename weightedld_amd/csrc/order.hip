@@ -43,13 +43,19 @@ __device__ inline void chunk_of_linear(uint32_t n, uint32_t i, uint32_t &row, ui
 }
 
 // One workgroup per (chunk, 16-row slice): every slice re-derives the chunk's
-// row prefix from the segment counts (256 rows x 4 bytes), then copies only
-// its 16 rows, so a chunk full of rows spreads over 16 workgroups.
+// row prefix from the segment counts (256 rows x 4 bytes, one dword per row:
+// T is a multiple of 4), then copies only its 16 rows, so a chunk full of rows
+// spreads over 16 workgroups.  A chunk without rows (its base equals the
+// next chunk's) and a slice without rows leave at once.  The copy issues all
+// 16 rows' loads before any store (wave s: b tile s of the chunk, lane e: the
+// e-th row of that segment), so a workgroup waits for one round of staging
+// loads, not sixteen.
 constexpr uint32_t kGatherRows = 16;
 
 __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t *__restrict__ chunk_base,
-                                                      uint32_t lin_begin, uint32_t n_chunk_rows, uint32_t L,
-                                                      uint64_t rows, const uint32_t *__restrict__ site_map,
+                                                      uint32_t lin_begin, uint32_t count, uint32_t n_chunk_rows,
+                                                      uint32_t L, uint64_t rows,
+                                                      const uint32_t *__restrict__ site_map,
                                                       uint32_t *__restrict__ out_a, uint32_t *__restrict__ out_b,
                                                       float *__restrict__ out_d, float *__restrict__ out_dp,
                                                       float *__restrict__ out_r2) {
@@ -57,26 +63,31 @@ __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t
     __shared__ uint32_t sOff[kGatherRows][kTilesPerChunk];
     __shared__ uint32_t sPre[kGatherRows][kTilesPerChunk];
     __shared__ uint32_t sWave[4];
+    const uint32_t base = chunk_base[blockIdx.x];
+    const uint64_t next = blockIdx.x + 1 < count ? chunk_base[blockIdx.x + 1] : rows;
+    if (next == base) return;  // (uniform) no row in this chunk
     const uint32_t lin = lin_begin + blockIdx.x;
     uint32_t row, col;
     chunk_of_linear(n_chunk_rows, lin, row, col);
-    const uint32_t base = chunk_base[blockIdx.x];
     const uint32_t tid = threadIdx.x;
     const uint32_t r0 = blockIdx.y * kGatherRows;
     const uint32_t a = row * kChunk + tid;
+    // the tiles the pair kernel computed (b tile >= a tile, inside L) each
+    // wrote their 64 counts; the other bytes of the dword are stale
+    uint32_t word = 0;
+    if (a < L) word = *reinterpret_cast<const uint32_t *>(o.seg_cnt + (size_t)a * o.T + col * kTilesPerChunk);
     uint32_t cnt[kTilesPerChunk], rowtot = 0;
 #pragma unroll
     for (int s = 0; s < kTilesPerChunk; ++s) {
         const uint32_t tb = col * kTilesPerChunk + s;
-        // the tiles the pair kernel computed (b tile >= a tile, inside L) each
-        // wrote their 64 counts; the rest of the chunk holds no rows
-        cnt[s] = (a < L && tb * kTile < L && tb >= a / kTile) ? o.seg_cnt[(size_t)a * o.T + tb] : 0u;
+        cnt[s] = (a < L && tb * kTile < L && tb >= a / kTile) ? (word >> (8 * s)) & 0xFFu : 0u;
         rowtot += cnt[s];
     }
     const uint32_t incl = wave_inclusive_scan(rowtot);
     if ((tid & 63) == 63) sWave[tid >> 6] = incl;
-    __syncthreads();
     const uint32_t slice_end = r0 + kGatherRows;
+    // the slice's own rows: any?
+    if (!__syncthreads_or(tid >= r0 && tid < slice_end && rowtot != 0)) return;
     if (tid >= r0 && tid < slice_end) {  // this slice's rows
         uint32_t wbase = 0;
         for (uint32_t k = 0; k < (tid >> 6); ++k) wbase += sWave[k];
@@ -92,21 +103,35 @@ __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t
     }
     __syncthreads();
     const uint32_t s = tid >> 6, e = tid & 63;
+    uint32_t fa[kGatherRows], fb[kGatherRows];
+    float fd[kGatherRows], fdp[kGatherRows], fr2[kGatherRows];
+    uint64_t dst[kGatherRows];
+    bool has[kGatherRows];
+#pragma unroll
     for (uint32_t r = 0; r < kGatherRows; ++r) {
-        if (e < sCnt[r][s]) {
-            const uint64_t src = (uint64_t)sOff[r][s] + e;
-            const uint64_t dst = (uint64_t)sPre[r][s] + e;
-            if (dst >= rows || src >= o.st_capacity) {  // (the run's counts disagree: not written)
-                report_guard(o, kGuardGather);
-                continue;
-            }
-            const uint32_t fa = o.st_a[src], fb = o.st_b[src];
-            out_a[dst] = site_map ? site_map[fa] : fa;
-            out_b[dst] = site_map ? site_map[fb] : fb;
-            out_d[dst] = o.st_d[src];
-            out_dp[dst] = o.st_dp[src];
-            out_r2[dst] = o.st_r2[src];
+        has[r] = e < sCnt[r][s];
+        const uint64_t src = (uint64_t)sOff[r][s] + e;
+        dst[r] = (uint64_t)sPre[r][s] + e;
+        if (has[r] && (dst[r] >= rows || src >= o.st_capacity)) {  // (the run's counts disagree: not written)
+            report_guard(o, kGuardGather);
+            has[r] = false;
         }
+        if (has[r]) {
+            fa[r] = o.st_a[src];
+            fb[r] = o.st_b[src];
+            fd[r] = o.st_d[src];
+            fdp[r] = o.st_dp[src];
+            fr2[r] = o.st_r2[src];
+        }
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kGatherRows; ++r) {
+        if (!has[r]) continue;
+        out_a[dst[r]] = site_map ? site_map[fa[r]] : fa[r];
+        out_b[dst[r]] = site_map ? site_map[fb[r]] : fb[r];
+        out_d[dst[r]] = fd[r];
+        out_dp[dst[r]] = fdp[r];
+        out_r2[dst[r]] = fr2[r];
     }
 }
 
@@ -146,7 +171,7 @@ void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_
                    uint32_t *out_b, float *out_d, float *out_dp, float *out_r2, hipStream_t s) {
     if (!count) return;
     hipLaunchKernelGGL(gather_kernel, dim3(count, kChunk / kGatherRows), dim3(256), 0, s, o, chunk_base, lin_begin,
-                       n_chunk_rows, L, rows, site_map, out_a, out_b, out_d, out_dp, out_r2);
+                       count, n_chunk_rows, L, rows, site_map, out_a, out_b, out_d, out_dp, out_r2);
 }
 
 }  // namespace wld

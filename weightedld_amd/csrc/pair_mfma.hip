@@ -388,6 +388,12 @@ struct ScreenArgs {
     unsigned *cand_work;    // the candidate launch's work counter (kModeScreen: workgroup 0 zeroes it)
     unsigned *cand_buckets; // the list's 16 bucket counts (cand_entry; the list and bits: 16 cand_cap each)
     uint32_t cand_cap;
+    // kModeScreen for the f32 reference-order candidate launch: one list
+    // entry per 16-row block of a candidate tile that holds a candidate
+    // sub-block (bits: that block's sub-blocks, buckets 4 - count, cand_cap =
+    // 4 tiles), each computed by one workgroup (pair_valu_kernel NS = 1); the
+    // tile's row blocks without one get their zero counts here
+    int rb_items;
     ScanArgs scan;          // screen and candidate launches: the fused chunk scan (scan_tail)
 };
 
@@ -492,14 +498,32 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
                 if (pair_cand(i)) m |= 1u << sub_block<Acc>(i, wave, lane);
             if (m) atomicOr(sMask, (unsigned long long)m);
             __syncthreads();
+            const uint32_t bits = (uint32_t)*sMask;
             if (tid == 0) {
-                const uint32_t bits = (uint32_t)*sMask, nb = (uint32_t)__popc(bits);  // nb >= 1
-                const uint32_t e = (16u - nb) * sc.cand_cap + atomicAdd(&sc.cand_buckets[16u - nb], 1u);
+                const uint32_t nb = (uint32_t)__popc(bits);  // nb >= 1
                 atomicAdd(sc.cand_count, 1u);
                 atomicAdd(sc.cand_count + 1, nb);  // sub-blocks to compute (stats)
-                sc.cand_list[e] = (ta << 16) | tb;
-                sc.cand_bits[e] = bits;
+                if (!sc.rb_items) {
+                    const uint32_t e = (16u - nb) * sc.cand_cap + atomicAdd(&sc.cand_buckets[16u - nb], 1u);
+                    sc.cand_list[e] = (ta << 16) | tb;
+                    sc.cand_bits[e] = bits;
+                } else {
+                    uint32_t empty = 0;
+                    for (uint32_t q = 0; q < 4; ++q) {
+                        const uint32_t rb = (bits >> (4 * q)) & 0xFu, k = (uint32_t)__popc(rb);
+                        if (!k) {
+                            ++empty;
+                            continue;
+                        }
+                        const uint32_t e = (4u - k) * sc.cand_cap + atomicAdd(&sc.cand_buckets[4u - k], 1u);
+                        sc.cand_list[e] = (ta << 16) | tb;
+                        sc.cand_bits[e] = rb << (4 * q);
+                    }
+                    if (empty) tile_done(o, ta, tb, n_chunk_rows, empty);  // (quarters: no candidate there)
+                }
             }
+            if (sc.rb_items && tid < kTile && !((bits >> (4 * (tid >> 4))) & 0xFu))
+                o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;  // a row block without a candidate: no rows
         } else {
             if (tid < kTile) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
             if (tid == 0) tile_done(o, ta, tb, n_chunk_rows);  // rejected: finished here
@@ -877,6 +901,7 @@ void launch_candidates(const MfmaLaunch &m, uint32_t n, uint32_t idx, const uint
         v.tile_work = sc.cand_work;
         v.tile_buckets = sc.cand_buckets;
         v.bucket_cap = sc.cand_cap;
+        v.rb_items = sc.rb_items != 0;
         v.scan = sc.scan;
         launch_pair_valu(v, o, nullptr, s);
         return;
@@ -892,7 +917,7 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     const uint64_t *ok_bits = reinterpret_cast<const uint64_t *>(m.wplanes + okbits_offset(m.NP));
     const bool prefilter = !dense && m.prefilter && m.thr > 0.0f;
     ScreenArgs sc{0.0,         0.0f,         0.0f,      0.0f,        0, m.nonneg, m.cand_list, m.cand_count,
-                  m.cand_list + 16 * (size_t)m.n_tiles, m.cand_work, m.cand_buckets, m.n_tiles, ScanArgs{}};
+                  m.cand_list + 16 * (size_t)m.n_tiles, m.cand_work, m.cand_buckets, m.n_tiles, 0, ScanArgs{}};
     if (!m.frag) {  // site-major kernel (all three planes)
         const dim3 g(m.n_tiles), b(256);
         if (dense)
@@ -958,6 +983,12 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
         return false;
     }
     sc.scan = m.scan;  // from here on a screen runs (and a candidate launch after it)
+    // lib.rs's order on the f32 kernel: candidates as 16-row-block items
+    // (buckets 0-3 of capacity 4 n_tiles: the 16 n_tiles list entries)
+    if (m.ref_valu && !m.ref_valu->safe) {
+        sc.rb_items = 1;
+        sc.cand_cap = 4 * m.n_tiles;
+    }
     // Screen: the top plane alone over every tile, the residual of the lower
     // planes bounded by R (in top-digit units: exact, a power-of-two scaling
     // of an integer below 2^53); candidate tiles then get every plane.  With

@@ -72,11 +72,16 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 #ifndef WLD_VALU_REF1_WG
 #define WLD_VALU_REF1_WG 6  // MF + REF, one slot per wave: six workgroups per CU (<= 85 VGPRs)
 #endif
+#ifndef WLD_VALU_REF1L_WG
+#define WLD_VALU_REF1L_WG 5  // ... the candidate loop (its loop state: <= 102 VGPRs, no spill)
+#endif
 // NS: 16x16 slots per wave (4: a whole 64x64 tile per workgroup; 1, MF +
 // REF only: one 16-row block of a tile per workgroup, one sub-block per wave —
 // a quarter of the accumulators, so more workgroups fit a CU)
 template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP, int NS = 4>
-__global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? WLD_VALU_REF1_WG : WLD_VALU_REF_WG) : WLD_VALU_MF_WG)
+__global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_WG : WLD_VALU_REF1_WG)
+                                                                : WLD_VALU_REF_WG)
+                                              : WLD_VALU_MF_WG)
                                      : 2) void pair_valu_kernel(
     const uint8_t *__restrict__ codes, const float *__restrict__ w, const uint8_t *__restrict__ site_ok,
     const uint32_t *__restrict__ tiles, uint32_t n_tiles, const unsigned *tile_count,
@@ -488,27 +493,38 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? WLD_VALU_REF1_WG : WLD_
         // (tile_work, zeroed by the screen): the workgroups that finish first
         // take the list's tail, not fixed ones (tiles differ in their computed
         // sub-blocks)
+        // NS = 1: the list holds 16-row-block items (the screen's rb_items),
+        // as many as the buckets count; each owns its row block's segments
         __shared__ uint32_t s_next, s_pre[17];
-        const uint32_t nt = *tile_count;
+        if constexpr (NS == 1) cand_prefix(tile_buckets, s_pre);
+        const uint32_t nt = NS == 1 ? s_pre[16] : *tile_count;
 #ifndef WLD_CAND_MIX
 #define WLD_CAND_MIX 1
 #endif
-        // first tiles: the list is heaviest first and the dispatcher deals
-        // workgroups i, i + m, i + 2m (m = grid / 3) to one CU, so that CU
-        // would start three of the heaviest tiles at once (one wave of each on
-        // every SIMD): deal it ranks j, 2m - 1 - j and 2m + j instead, a heavy,
-        // a light and a middle one (a permutation of [0, grid))
+        // first items: the list is heaviest first and the dispatcher deals
+        // workgroups i, i + m, i + 2m, ... (m = grid / R, R resident per CU)
+        // to one CU, so that CU would start R of the heaviest items at once
+        // (one wave of each on every SIMD): deal the rounds in snake order
+        // instead (j, 2m - 1 - j, 2m + j, ...), heavy next to light (a
+        // permutation of [0, grid))
         uint32_t first = blockIdx.x;
         if (WLD_CAND_MIX && tile_buckets) {
-            const uint32_t m = gridDim.x / 3, k = m ? blockIdx.x / m : 3u, j = blockIdx.x - (k < 3 ? k * m : 0u);
-            if (k < 3) first = k == 0 ? j : k == 1 ? 2 * m - 1 - j : 2 * m + j;
+            constexpr uint32_t R = NS == 1 ? WLD_VALU_REF1L_WG : WLD_VALU_REF_WG;
+            const uint32_t m = gridDim.x / R, k = m ? blockIdx.x / m : R, j = blockIdx.x - (k < R ? k * m : 0u);
+            if (k < R) first = (k & 1) ? (k + 1) * m - 1 - j : k * m + j;
         }
-        if (tile_buckets && first < nt) cand_prefix(tile_buckets, s_pre);  // (a workgroup without a tile skips it)
+        if (NS != 1 && tile_buckets && first < nt) cand_prefix(tile_buckets, s_pre);  // (a workgroup without a tile skips it)
         for (uint32_t bi = first; bi < nt;) {
             const uint32_t e = tile_buckets ? cand_entry_checked(o, s_pre, bucket_cap, bi) : bi < n_tiles ? bi : ~0u;
             const uint32_t tile = e != ~0u ? tiles[e] : kNoTile;
-            if (tile_in_range(tile, L))
-                compute_tile(tile, threadIdx.x, tile_bits ? tile_bits[e] : 0xFFFFu, 0xFu);
+            const uint32_t bits = tile_bits ? tile_bits[e] : 0xFFFFu;
+            uint32_t owned = 0xFu;  // a whole-tile entry writes all 64 rows' segments
+            if constexpr (NS == 1) {
+                owned = 0;
+                for (uint32_t q = 0; q < 4; ++q) owned |= ((bits >> (4 * q)) & 0xFu) ? 1u << q : 0u;
+            }
+            if (tile_in_range(tile, L) && (NS != 1 || __popc(owned) == 1))
+                compute_tile(tile, threadIdx.x, bits, owned);
             else if (e != ~0u && threadIdx.x == 0)
                 report_guard(o, kGuardTile);
             if (threadIdx.x == 0) s_next = gridDim.x + atomicAdd(tile_work, 1u);
@@ -776,6 +792,9 @@ void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
             else launch_v<true, false, true, true, false>(v, grid, flush, cs, o, dn, s);
         } else if (v.tile_count) {
             if (v.safe) launch_v<false, true, false, true, true>(v, grid, flush, cs, o, dn, s);
+            else if (v.rb_items)  // 16-row-block items, one sub-block per wave, six workgroups per CU
+                launch_v<false, false, true, true, true, 1>(v, std::min<uint32_t>(4 * v.n_tiles, kRefItemGrid), flush,
+                                                             cs, o, dn, s);
             else launch_v<false, false, true, true, true>(v, grid, flush, cs, o, dn, s);
         } else {
             // every tile of the run: with fewer tiles than four rounds of
