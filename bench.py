@@ -272,7 +272,7 @@ def main():
     ap.add_argument("--pipe-depth", type=int, default=0, metavar="D",
                     help="contexts of the pipelined step loop, D - 1 steps in flight (default: 3 for the N>1 "
                          "step path, where unserialized screens take rank 0's 1/8 shard of C4 from 0.142 to "
-                         "0.118 ms/step, profiles/r03j/; 2 at N=1, where three measured equal, profiles/r03q/)")
+                         "0.118 ms/step, archive/profiles_r01_r03/r03j/; 2 at N=1, where three measured equal, archive/profiles_r01_r03/r03q/)")
     ap.add_argument("--rehearse-shard", type=int, default=0, metavar="K",
                     help="with --rehearse-dist: run rank 0's shard of a K-way split (the per-rank work at "
                          "N=K; value counts that shard's pairs); a rehearsal line, never the headline")
@@ -427,8 +427,8 @@ def main():
                                         # a shard's last round of tiles overlaps the next step's first and
                                         # no cross-queue event wait (~20 us) sits between them; "pair":
                                         # step i's pair kernel waits on the device for step i-1's screen
-                                        # (wld_run_after); 1: for step i-1's whole run (profiles/r02pc/,
-                                        # profiles/r03i/)
+                                        # (wld_run_after); 1: for step i-1's whole run (archive/profiles_r01_r03/r02pc/,
+                                        # archive/profiles_r01_r03/r03i/)
                                         serialize_kernels={"0": False, "1": True}.get(serialize, "pair"),
                                         host_collectives=host_coll)
 
@@ -475,7 +475,7 @@ def main():
     # Clock settle (untimed, before the warmup): back-to-back steps for about
     # settle_s seconds.  The pair kernel's time falls over the first ~30
     # launches as the clock settles (rocprofv3 trace of `--steps 20 --warmup
-    # 5`, profiles/r03c/: a C4 screen launch 1.07 -> 0.90 ms), so a short
+    # 5`, archive/profiles_r01_r03/r03c/: a C4 screen launch 1.07 -> 0.90 ms), so a short
     # warmup would time the ramp, not the kernel.  Every rank runs the same
     # number of steps (their collectives pair up).
     settle_steps = 0

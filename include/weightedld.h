@@ -354,7 +354,10 @@ void *wld_stream(wld_ctx *ctx);
  * with nothing between their kernels (the N=1 pipelined loop: the next run
  * queued behind the previous one without a cross-queue event, cf.
  * wld_run_after, which then returns at once).  WLD_E_STATE during a run,
- * WLD_E_ARG for device groups. */
+ * WLD_E_ARG for device groups.  The stream is borrowed: it must outlive its
+ * use by ctx (set the context back to NULL, or destroy ctx, before destroying
+ * the stream or the context that owns it); wld_destroy waits for the work ctx
+ * queued on a borrowed stream. */
 int wld_set_stream(wld_ctx *ctx, void *stream);
 /* All pairs of the loaded set, any size, rows to host: runs the reference's
  * chunk sequence in batches of at most 2^31 pairs (one wld_run_chunks each),

@@ -737,6 +737,16 @@ def test_contexts_on_one_stream(W):
     assert cs[1].stream_ptr() not in (0, cs[0].stream_ptr())
     assert cs[1].run(0.02) == len(refs[0.02]["site_a"])
     _bit_equal_rows(cs[1].rows(), refs[0.02])
+    # the owner closed while cs[2] still runs on its stream: cs[2] gets its
+    # own stream back first and keeps working
+    cs[2].run_chunks_async(0.0, 0, 0)
+    with pytest.raises(W.WldError):
+        cs[0].close()  # cs[2] has a run in flight on cs[0]'s stream: refused, nothing destroyed
+    assert cs[2].run_wait() == len(refs[0.0]["site_a"])
+    cs[0].close()
+    assert cs[2].stream_ptr() not in (0,)
+    assert cs[2].run(0.3) == len(refs[0.3]["site_a"])
+    _bit_equal_rows(cs[2].rows(), refs[0.3])
 
 
 def _bit_equal_rows(store, ref):

@@ -6,6 +6,7 @@ weights) runs in the library's C++ host code, the all-pairs hot path on the
 gfx950 GPU.  There is no CPU fallback for the hot path.
 """
 import ctypes
+import weakref
 import enum
 from collections import namedtuple
 
@@ -206,6 +207,8 @@ class Context:
         context (wld_create_multi) that shards load/run_host/all-pairs calls.
         ref_sums (WLD_OPT_REF_SUMS): None keeps the library default (lib.rs's
         own f32 summation order, bit-identical rows); False: exact sums."""
+        self._borrowers = weakref.WeakSet()  # contexts running on this one's stream (set_stream)
+        self._stream_owner = None
         h = ctypes.c_void_p()
         self._lib = lib()  # kept: module globals may be gone when __del__ runs at exit
         if devices is not None:
@@ -223,6 +226,15 @@ class Context:
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
+            # contexts running on this one's stream get their own back first
+            # (wld_set_stream waits for their queued work)
+            for b in list(getattr(self, "_borrowers", ())):
+                if getattr(b, "_h", None) is not None and b._h.value:
+                    b.set_stream(None)
+            owner = getattr(self, "_stream_owner", None)
+            if owner is not None:
+                owner._borrowers.discard(self)
+                self._stream_owner = None
             self._lib.wld_destroy(self._h)
             self._h = None
 
@@ -340,9 +352,17 @@ class Context:
 
     def set_stream(self, stream):
         """wld_set_stream: run on another context's stream (a Context), a
-        hipStream_t given as an int, or None for the context's own."""
+        hipStream_t given as an int, or None for the context's own.  A borrowed
+        Context stream stays referenced here, and the owner hands this context
+        back its own stream before its close() destroys the borrowed one."""
         ptr = stream.stream_ptr() if isinstance(stream, Context) else (stream or 0)
         check(lib().wld_set_stream(self._h, ctypes.c_void_p(ptr) if ptr else None), "wld_set_stream")
+        old = getattr(self, "_stream_owner", None)
+        if old is not None:
+            old._borrowers.discard(self)
+        self._stream_owner = stream if isinstance(stream, Context) else None
+        if self._stream_owner is not None:
+            self._stream_owner._borrowers.add(self)
 
     def rows(self):
         v = Pairs()

@@ -168,6 +168,9 @@ struct wld_ctx {
         for (wld_ctx *m : members) delete m;
         if (!members.empty()) return;
         (void)hipSetDevice(device);
+        // work queued on a borrowed stream (wld_set_stream) may still use the
+        // buffers: it completes before they are freed
+        if (stream && stream != own_stream) (void)hipStreamSynchronize(stream);
         DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &rcodes, &rw, &tiles, &cand,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &chunk_left, &prog_n, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
@@ -378,7 +381,7 @@ void rows_to_linear(uint32_t n, uint32_t rb, uint32_t re, uint32_t &lb, uint32_t
 // kS = 16 where the 128 screen tiles resident on an XCD's 32 CUs (4
 // workgroups per CU: 8 rows of one super-block, 8 A and 16 B tile columns of
 // 64 NP bytes) fit its 4 MB L2 (C4: 3 MB): 0.86 GB per C4 screen launch past
-// L2 instead of 1.11 GB with kS = 8, step -0.5% (profiles/r03ar, r03as,
+// L2 instead of 1.11 GB with kS = 8, step -0.5% (archive/profiles_r01_r03/r03ar, r03as,
 // r03au).  Otherwise kS = 8, two whole super-blocks resident (C5, 323 KB
 // columns: 3% faster than 16).
 std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t, uint32_t kS) {
@@ -1189,7 +1192,7 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     // kernel: half the C4 tiles ~3 ms over the 0.9 ms screen, about the exact
     // candidate pairs' cost)
     // ... and one at which the two-plane screen (0.8 of the full kernel's
-    // time at BASELINE config 4, profiles/r02s2/) leaves more than a fifth
+    // time at BASELINE config 4, archive/profiles_r01_r03/r02s2/) leaves more than a fifth
     // goes to the full kernel (the exact mode; lib.rs's order takes the two-
     // plane screen only when asked, WLD_OPT_SCREEN 3)
     if (c->screened && !c->ref_pairs_pass && !c->screened2 && h[2] * 2 > c->n_tiles)
