@@ -962,8 +962,10 @@ def test_cli_progress_bars(tmp_path, prepass):
     assert "\x1b[2K" not in r.stderr and "pairs computed at" in r.stderr
     # info level on a terminal: bar frames on stderr, same TSV, and the same
     # log lines once the frames are taken out
-    r2 = subprocess.run(cmd(tmp_path / "b.tsv"), capture_output=True, text=True, timeout=120,
+    # (bytes, decoded by hand: text mode would turn every "\r" into a newline)
+    r2 = subprocess.run(cmd(tmp_path / "b.tsv"), capture_output=True, timeout=120,
                         env=dict(env, RUST_LOG="info", WLD_FORCE_PROGRESS_BAR="1"))
+    r2.stderr = r2.stderr.decode("utf-8")
     assert r2.returncode == 0, r2.stderr[-2000:]
     assert "\x1b[2K" in r2.stderr and re.search(r"\] \d+% \(\d+/s \d\d:\d\d:\d\d\)", r2.stderr), r2.stderr[-2000:]
     assert (tmp_path / "b.tsv").read_bytes() == (tmp_path / "a.tsv").read_bytes()

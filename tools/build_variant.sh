@@ -3,7 +3,8 @@
 # pair_mfma.hip (other objects shared with the main build):
 #   tools/build_variant.sh NAME "-DFLAG ..."   -> build/exp/NAME/libweightedld.so
 # SLP=1 builds the source without -fno-slp-vectorize (packed-f32 probe);
-# SRC=pair_valu varies pair_valu.hip instead of pair_mfma.hip.
+# SRC=pair_valu varies pair_valu.hip instead of pair_mfma.hip; SRC="pair_valu
+# pair_mfma" both.
 set -e
 cd "$(dirname "$0")/.."
 name=$1; flags=$2
@@ -13,11 +14,13 @@ make -s build/obj/encode.o build/obj/prepass.o build/obj/pair_valu.o build/obj/p
 out=build/exp/$name; mkdir -p $out
 slp=-fno-slp-vectorize
 [ "${SLP:-0}" = 1 ] && slp=
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $slp -Wall -Iinclude \
-  -Iweightedld_amd/csrc $flags -c weightedld_amd/csrc/$src.hip -o $out/$src.o
+for one in $src; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $slp -Wall -Iinclude \
+    -Iweightedld_amd/csrc $flags -c weightedld_amd/csrc/$one.hip -o $out/$one.o
+done
 objs=""
 for o in encode prepass pair_valu pair_mfma order capi host; do
-  if [ $o = $src ]; then objs="$objs $out/$o.o"; else objs="$objs build/obj/$o.o"; fi
+  if [[ " $src " == *" $o "* ]]; then objs="$objs $out/$o.o"; else objs="$objs build/obj/$o.o"; fi
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/libweightedld.so $objs -lpthread
 echo "$out/libweightedld.so"

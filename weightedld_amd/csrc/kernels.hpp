@@ -193,6 +193,12 @@ constexpr uint32_t kCandidateGrid = 2048;
 constexpr uint32_t kRefCandidateGrid = 768;
 // ... and of its 16-row-block items (one sub-block per wave: five per CU)
 constexpr uint32_t kRefItemGrid = 1280;
+// lib.rs's order on f32 MFMA in work items of one sub-block per wave: the
+// candidate launch after a screen, and full runs of few tiles (0: whole
+// 64x64 tiles per workgroup, the round-3 shape; A/B builds only)
+#ifndef WLD_REF_ITEMS
+#define WLD_REF_ITEMS 1
+#endif
 // ... and of ref_sums_kernel / ref_compact_kernel (low-register: eight per CU)
 constexpr uint32_t kRefRowsGrid = 2048;
 

@@ -388,11 +388,13 @@ struct ScreenArgs {
     unsigned *cand_work;    // the candidate launch's work counter (kModeScreen: workgroup 0 zeroes it)
     unsigned *cand_buckets; // the list's 16 bucket counts (cand_entry; the list and bits: 16 cand_cap each)
     uint32_t cand_cap;
-    // kModeScreen for the f32 reference-order candidate launch: one list
-    // entry per 16-row block of a candidate tile that holds a candidate
-    // sub-block (bits: that block's sub-blocks, buckets 4 - count, cand_cap =
-    // 4 tiles), each computed by one workgroup (pair_valu_kernel NS = 1); the
-    // tile's row blocks without one get their zero counts here
+    // kModeScreen for the f32 reference-order candidate launch: list entries
+    // are items of a candidate tile's 16-row blocks that hold candidate
+    // sub-blocks, packed in row order up to four sub-blocks per item (bits:
+    // the item's sub-blocks; bucket 4 - count, cand_cap = 4 tiles), each
+    // computed by one workgroup, one sub-block per wave (pair_valu_kernel NS
+    // = 1), which owns its row blocks' segments; the tile's row blocks
+    // without a candidate get their zero counts here
     int rb_items;
     ScanArgs scan;          // screen and candidate launches: the fused chunk scan (scan_tail)
 };
@@ -508,17 +510,28 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
                     sc.cand_list[e] = (ta << 16) | tb;
                     sc.cand_bits[e] = bits;
                 } else {
-                    uint32_t empty = 0;
+                    // the tile's 16-row blocks in order, packed greedily into
+                    // items of at most four computed sub-blocks (one per wave)
+                    uint32_t empty = 0, cur = 0, cur_k = 0;
+                    auto emit = [&]() {
+                        const uint32_t e = (4u - cur_k) * sc.cand_cap + atomicAdd(&sc.cand_buckets[4u - cur_k], 1u);
+                        sc.cand_list[e] = (ta << 16) | tb;
+                        sc.cand_bits[e] = cur;
+                    };
                     for (uint32_t q = 0; q < 4; ++q) {
                         const uint32_t rb = (bits >> (4 * q)) & 0xFu, k = (uint32_t)__popc(rb);
                         if (!k) {
                             ++empty;
                             continue;
                         }
-                        const uint32_t e = (4u - k) * sc.cand_cap + atomicAdd(&sc.cand_buckets[4u - k], 1u);
-                        sc.cand_list[e] = (ta << 16) | tb;
-                        sc.cand_bits[e] = rb << (4 * q);
+                        if (cur_k + k > 4) {
+                            emit();
+                            cur = cur_k = 0;
+                        }
+                        cur |= rb << (4 * q);
+                        cur_k += k;
                     }
+                    if (cur_k) emit();
                     if (empty) tile_done(o, ta, tb, n_chunk_rows, empty);  // (quarters: no candidate there)
                 }
             }
@@ -985,7 +998,7 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     sc.scan = m.scan;  // from here on a screen runs (and a candidate launch after it)
     // lib.rs's order on the f32 kernel: candidates as 16-row-block items
     // (buckets 0-3 of capacity 4 n_tiles: the 16 n_tiles list entries)
-    if (m.ref_valu && !m.ref_valu->safe) {
+    if (WLD_REF_ITEMS && m.ref_valu && !m.ref_valu->safe) {
         sc.rb_items = 1;
         sc.cand_cap = 4 * m.n_tiles;
     }

@@ -151,6 +151,18 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_
         const uint32_t lr = tid >> 2, part = tid & 3;  // loader: site row, 16-byte part
         const uint8_t *gA = codes + (size_t)(a0 + lr) * NP + part * 16;
         const uint8_t *gB = codes + (size_t)(b0 + lr) * NP + part * 16;
+        // only the a rows of row blocks and the b rows of column blocks that
+        // hold a computed sub-block are staged (the other LDS rows are never read)
+        // (NS = 1 items; a whole-tile workgroup stages every row)
+        uint32_t rows_used = 0xFu, cols_used = 0xFu;
+        if constexpr (NS == 1) {
+            rows_used = cols_used = 0;
+            for (uint32_t q = 0; q < 4; ++q) {
+                rows_used |= ((bits >> (4 * q)) & 0xFu) ? 1u << q : 0u;
+                cols_used |= (bits >> (4 * q)) & 0xFu;
+            }
+        }
+        const bool ldA = NS != 1 || ((rows_used >> (lr >> 4)) & 1u), ldB = NS != 1 || ((cols_used >> (lr >> 4)) & 1u);
 
         // one 64-sequence stage of both panels' codes and the weights: fetch
         // (global loads into registers, issued a stage ahead so that their
@@ -162,16 +174,16 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_
         uint4 va, vb;
         float wv;
         auto fetch_stage = [&](uint32_t k0) {
-            va = *reinterpret_cast<const uint4 *>(gA + k0);
-            vb = *reinterpret_cast<const uint4 *>(gB + k0);
+            if (ldA) va = *reinterpret_cast<const uint4 *>(gA + k0);
+            if (ldB) vb = *reinterpret_cast<const uint4 *>(gB + k0);
             wv = tid < 64 ? w[k0 + tid] : 0.0f;
         };
         auto store_stage = [&]() {
             __syncthreads();
             uint32_t *pa = reinterpret_cast<uint32_t *>(sA + lr * kStride + part * 16);
             uint32_t *pb = reinterpret_cast<uint32_t *>(sB + lr * kStride + part * 16);
-            pa[0] = va.x; pa[1] = va.y; pa[2] = va.z; pa[3] = va.w;
-            pb[0] = vb.x; pb[1] = vb.y; pb[2] = vb.z; pb[3] = vb.w;
+            if (ldA) pa[0] = va.x, pa[1] = va.y, pa[2] = va.z, pa[3] = va.w;
+            if (ldB) pb[0] = vb.x, pb[1] = vb.y, pb[2] = vb.z, pb[3] = vb.w;
             if (tid < 64) sW[tid] = wv;
             __syncthreads();
         };
@@ -523,7 +535,7 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_
                 owned = 0;
                 for (uint32_t q = 0; q < 4; ++q) owned |= ((bits >> (4 * q)) & 0xFu) ? 1u << q : 0u;
             }
-            if (tile_in_range(tile, L) && (NS != 1 || __popc(owned) == 1))
+            if (tile_in_range(tile, L) && (NS != 1 || __popc(bits) <= 4))
                 compute_tile(tile, threadIdx.x, bits, owned);
             else if (e != ~0u && threadIdx.x == 0)
                 report_guard(o, kGuardTile);
@@ -801,7 +813,8 @@ void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
             // resident workgroups (BASELINE config 2: 528 tiles), each tile's
             // four 16-row blocks are separate work items (f32 MFMA path)
             if (v.safe) launch_v<false, true, false, true, false>(v, grid, flush, cs, o, dn, s);
-            else if (v.n_tiles <= 4 * kRefCandidateGrid) launch_v<false, false, true, true, false, 1>(v, grid, flush, cs, o, dn, s, 4);
+            else if (WLD_REF_ITEMS && v.n_tiles <= 4 * kRefCandidateGrid)
+                launch_v<false, false, true, true, false, 1>(v, grid, flush, cs, o, dn, s, 4);
             else launch_v<false, false, true, true, false>(v, grid, flush, cs, o, dn, s);
         }
         return;
