@@ -208,6 +208,14 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *   WLD_OPT_STAGING_ROWS   initial staging capacity in rows (default 2^25;
  *                      grown on overflow by a re-run).
  *   WLD_OPT_HOST_BATCH_PAIRS  pairs per batch of wld_run_host (default 2^31).
+ *   WLD_OPT_SCREEN_FP6 1 (default, auto): the one-plane screen multiplies
+ *                      fp6 (e2m3) weights by fp4 codes on the block-scaled
+ *                      MFMA (128 sequences per instruction, twice the i8
+ *                      rate) when the weights are nonnegative, at most 16,384
+ *                      sequences, and their fp6 rounding leaves a residual
+ *                      within twice the i8 top digit's; 0: the i8 screen;
+ *                      2: fp6 whenever it applies.  Same rows (a screen only
+ *                      decides which tiles are computed).
  *   WLD_OPT_FUSED_SCAN 1 (default): after a screen, the run's chunk scan runs
  *                      in the candidate launch's last workgroup (ranges up to
  *                      4096 chunks); 0: as a launch of its own (the kernel
@@ -224,6 +232,7 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
 #define WLD_OPT_HOST_BATCH_PAIRS 8
 #define WLD_OPT_REF_SUMS 11
 #define WLD_OPT_FUSED_SCAN 12
+#define WLD_OPT_SCREEN_FP6 13
 int wld_set_option(wld_ctx *ctx, int option, int64_t value);
 int wld_get_option(wld_ctx *ctx, int option, int64_t *value);
 
@@ -405,6 +414,7 @@ typedef struct {
                                   could not reject (16 x candidate_tiles unless screened); with
                                   WLD_OPT_REF_SUMS only these are computed */
     uint64_t candidate_pairs; /* screened == 4: the pairs summed one by one in lib.rs's order */
+    int screen_fp6;          /* screened == 1 on fp6 x fp4 block-scaled MFMA (WLD_OPT_SCREEN_FP6), not i8 */
 } wld_run_stats;
 int wld_last_stats(wld_ctx *ctx, wld_run_stats *out);
 

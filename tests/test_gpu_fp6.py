@@ -1,0 +1,141 @@
+"""The fp6 screen (pair_mfma.hip pair_fp6_screen_kernel, WLD_OPT_SCREEN_FP6):
+the one-plane screen's sums on block-scaled fp6 x fp4 MFMA.  A screen only
+decides which tiles the candidate launch computes, so rows must be
+bit-identical to the i8 screen's, to the unscreened kernel's and (the default,
+lib.rs's summation order) to the oracle's, on every data kind — including
+linkage blocks and rare alleles, where many tiles are candidates and the
+screen's residual bound is what keeps a passing pair from being skipped.
+Reference semantics: lib.rs:482-520 (epilogue), :660 (strict r2 > thr),
+:623-683 (row order).
+"""
+import numpy as np
+import pytest
+
+import _oracle as O
+from conftest import REPO  # noqa: F401
+from test_gpu_parity import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def W():
+    import weightedld_amd as W
+    return W
+
+
+def _bits_equal(store, ref):
+    assert len(store) == len(ref["site_a"]), (len(store), len(ref["site_a"]))
+    assert np.array_equal(store.site_a.astype(np.uint64), ref["site_a"].astype(np.uint64))
+    assert np.array_equal(store.site_b.astype(np.uint64), ref["site_b"].astype(np.uint64))
+    for f in ("d", "d_prime", "r2"):
+        x, y = getattr(store, f), np.asarray(ref[f], dtype=np.float32)
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), f
+
+
+def _store_dict(s):
+    return {f: getattr(s, f) for f in ("site_a", "site_b", "d", "d_prime", "r2")}
+
+
+def _data(kind, L, N, seed):
+    import bench
+    rng = np.random.default_rng(seed)
+    if kind == "random":
+        buf = synth(L, N, seed)
+    elif kind == "ldblocks":
+        buf = bench.ld_blocks(L, N, seed=seed)
+    elif kind == "rare":
+        buf = synth(L, N, seed)
+        for s in range(0, L, 3):  # minor allele on 1-3 sequences
+            buf[s] = np.where(buf[s] == 4, 4, 0)
+            buf[s, rng.choice(N, size=int(rng.integers(1, 4)), replace=False)] = 1
+    else:
+        raise ValueError(kind)
+    return buf
+
+
+@pytest.mark.parametrize("kind", ["random", "ldblocks", "rare"])
+@pytest.mark.parametrize("weights", ["henikoff", "wide", "unit"])
+def test_fp6_screen_rows_bit_identical(W, kind, weights):
+    L, N = 1500, 700
+    buf = _data(kind, L, N, 17)
+    if weights == "henikoff":
+        w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    elif weights == "wide":  # 16x range: the fp6 rounding's relative error is largest
+        w = (np.random.default_rng(5).random(N) * 15 + 1).astype(np.float32)
+    else:
+        w = np.ones(N, dtype=np.float32)
+    ctxs = {}
+    for name, fp6 in (("fp6", 2), ("i8", 0)):
+        c = W.Context(0)
+        c.set_option("screen_fp6", fp6)
+        c.load(buf, w)
+        ctxs[name] = c
+    for thr in (0.05, 0.2, 0.01, 0.5):
+        ref = O.all_pairs(buf, w, np.float32(thr))
+        out = {}
+        for name, c in ctxs.items():
+            n = c.run(thr)
+            st = c.stats()
+            out[name] = (c.rows(), st)
+            assert n == len(ref["site_a"])
+            _bits_equal(out[name][0], ref)
+        st6 = out["fp6"][1]
+        if st6["screened"] == 1:
+            assert st6["screen_fp6"] == 1, st6
+        assert out["i8"][1]["screen_fp6"] == 0
+    for c in ctxs.values():
+        c.close()
+
+
+def test_fp6_exact_mode_rows(W):
+    """Exact sums (WLD_OPT_REF_SUMS 0): the candidate launch's integer kernel
+    behind the fp6 screen gives the same rows as without any screen."""
+    L, N = 1300, 900
+    buf = _data("ldblocks", L, N, 23)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    a, b = W.Context(0, ref_sums=False), W.Context(0, ref_sums=False)
+    a.set_option("screen_fp6", 2)
+    b.set_option("screen", 0)
+    a.load(buf, w)
+    b.load(buf, w)
+    for thr in (0.05, 0.3):
+        assert a.run(thr) == b.run(thr)
+        assert a.stats()["screen_fp6"] == 1
+        _bits_equal(a.rows(), _store_dict(b.rows()))
+
+
+def test_fp6_default_on_bench_data_and_ineligible_weights(W):
+    """Auto: the bench's Henikoff weights (nearly equal) take the fp6 screen;
+    mixed-sign weights never do (its bound assumes nonnegative cells)."""
+    import bench
+    buf = bench.synth(2048, 2000)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    c = W.Context(0)
+    c.load(buf, w)
+    c.run(0.05)
+    st = c.stats()
+    assert st["screened"] == 1 and st["screen_fp6"] == 1 and st["candidate_tiles"] == 0, st
+    _bits_equal(c.rows(), O.all_pairs(buf, w, np.float32(0.05)))
+    wm = w.copy()
+    wm[::7] *= -1
+    c.load(buf, wm)
+    c.run(0.05)
+    assert c.stats()["screen_fp6"] == 0
+    _bits_equal(c.rows(), O.all_pairs(buf, wm, np.float32(0.05)))
+    c.close()
+
+
+@pytest.mark.parametrize("N", [64, 100, 128, 190, 1000, 2049])
+def test_fp6_sequence_counts(W, N):
+    """NP not a multiple of 128 (a zero-padded last fp6 block), tiny N."""
+    L = 700
+    buf = synth(L, N, 31 + N)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    c = W.Context(0)
+    c.set_option("screen_fp6", 2)
+    c.load(buf, w)
+    for thr in (0.02, 0.1):
+        c.run(thr)
+        _bits_equal(c.rows(), O.all_pairs(buf, w, np.float32(thr)))
+    c.close()

@@ -23,7 +23,7 @@ STATUS = {
 KERNEL_AUTO, KERNEL_VALU, KERNEL_MFMA = 0, 1, 2
 # wld_set_option ids (include/weightedld.h)
 OPTIONS = {"prefilter": 1, "screen": 2, "tile_order": 3, "all_planes": 4, "mfma_layout": 5, "valu_plain": 6,
-           "staging_rows": 7, "host_batch_pairs": 8, "ref_sums": 11, "fused_scan": 12}
+           "staging_rows": 7, "host_batch_pairs": 8, "ref_sums": 11, "fused_scan": 12, "screen_fp6": 13}
 
 
 class WldError(RuntimeError):
@@ -62,6 +62,7 @@ class RunStats(ctypes.Structure):
         ("ref_sums", ctypes.c_int),
         ("candidate_blocks", ctypes.c_uint64),
         ("candidate_pairs", ctypes.c_uint64),
+        ("screen_fp6", ctypes.c_int),
     ]
 
 

@@ -120,6 +120,7 @@ struct wld_ctx {
     bool ref_pairs_pass = false;  // the pass staged exact candidate pairs (ref_rows_kernel)
     bool opt_site_major = false, opt_valu_plain = false;
     bool opt_fused_scan = true;  // WLD_OPT_FUSED_SCAN: the chunk scan in the candidate launch's last workgroup
+    int opt_fp6 = 1;             // WLD_OPT_SCREEN_FP6: 0 off, 1 auto, 2 whenever it applies
     bool opt_ref_sums = true;  // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order (default)
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
 
@@ -128,6 +129,13 @@ struct wld_ctx {
     size_t L = 0, N = 0, LP = 0, NP = 0;
     DevBuf raw, wraw, codes, w_pad, wstats, site_ok, site_map, planes, frag;
     DevBuf rcodes, rw;       // WLD_OPT_REF_SUMS: codes and weights in lane-class order (ref_layout_kernel)
+    // the fp6 screen (fp6_prepare): weight codes, packed operands, constants
+    DevBuf w6, f6a, f6b;
+    Fp6Screen f6{};
+    bool fp6_ok = false;      // operands built for this load (the weights allow it)
+    bool fp6_pass = false;    // the last pass screened on fp6
+    bool fp6_better = false;  // ... and its residual is within twice the i8 top digit's (auto)
+    double fp6_rel = 0.0, i8_rel = 0.0;  // the two screens' residuals relative to their sums
     bool have_ref = false;   // rcodes/rw hold this load's layout
     uint32_t ref_cls = 0;    // its positions per lane class
     size_t NPr = 0;          // its positions per site
@@ -171,7 +179,7 @@ struct wld_ctx {
         // work queued on a borrowed stream (wld_set_stream) may still use the
         // buffers: it completes before they are freed
         if (stream && stream != own_stream) (void)hipStreamSynchronize(stream);
-        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &rcodes, &rw, &tiles, &cand,
+        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &rcodes, &rw, &w6, &f6a, &f6b, &tiles, &cand,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &chunk_left, &prog_n, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
@@ -216,6 +224,87 @@ int weight_shift(float maxabs, int planes) {
     while (std::ldexp((double)maxabs, shift + 1) <= lim) ++shift;
     while (std::ldexp((double)maxabs, shift) > lim) --shift;
     return shift;
+}
+
+double ref_extra_residual(const wld_ctx *c);
+
+// e2m3 (fp6) encoding of a value in [0, 7.5] rounded to the nearest grid
+// point (ties to the even code): sign 0, exponent bias 1, 3 mantissa bits
+uint32_t fp6_code(double x, double *rounded) {
+    uint32_t best = 0;
+    double bv = 0.0, be = x;
+    for (uint32_t c = 0; c < 32; ++c) {
+        const uint32_t e = c >> 3, m = c & 7;
+        const double v = e ? (1.0 + m / 8.0) * std::ldexp(1.0, (int)e - 1) : m / 8.0;
+        const double err = std::fabs(x - v);
+        if (err < be || (err == be && !(c & 1))) best = c, bv = v, be = err;
+    }
+    *rounded = bv;
+    return best;
+}
+
+// The fp6 screen's operands for this load (pair_mfma.hip): nonnegative
+// finite weights, NP <= 16384 (its f32 test on doubled sums), the i8 kernel's
+// fragment layout in use.  The weights are rounded to e2m3 at the common
+// scale S (of 51 candidates in [3.75, 7.5] / max w) that minimises the L1
+// rounding residual; R (in fp6 units) bounds each pass's 2x2-cell L1 distance
+// between the screen's sums and the sums the candidate launch computes: the
+// rounding, plus the fixed point's 0.5 per sequence (exact mode) and lib.rs's
+// f32 summation (9 gamma_m sum w, ref_extra_residual) — both added, so one
+// R serves either mode.
+int fp6_prepare(wld_ctx *c) {
+    c->fp6_ok = c->fp6_better = false;
+    if (c->kernel != WLD_KERNEL_MFMA || !c->use_frag || !c->wst.nonneg || c->NP > 16384 || c->N == 0) return WLD_OK;
+    std::vector<float> w(c->NP);
+    HIP_TRY(hipMemcpyAsync(w.data(), c->w_pad.p, c->NP * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    double wmax = 0.0, wsum = 0.0;
+    for (size_t k = 0; k < c->N; ++k) wmax = std::max(wmax, (double)w[k]), wsum += (double)w[k];
+    if (!(wmax > 0.0) || !std::isfinite(wsum)) return WLD_OK;
+    double best_r = INFINITY, best_s = 0.0;
+    for (int f = 0; f <= 50; ++f) {
+        const double S = 7.5 * (0.5 + 0.01 * f) / wmax;
+        double r = 0.0, v;
+        for (size_t k = 0; k < c->N; ++k) {
+            fp6_code(S * w[k], &v);
+            r += std::fabs(S * w[k] - v);
+        }
+        if (r / S < best_r) best_r = r / S, best_s = S;
+    }
+    const double S = best_s;
+    std::vector<uint8_t> codes(c->NP, 0);
+    double r6 = 0.0, sum6 = 0.0, v;
+    for (size_t k = 0; k < c->N; ++k) {
+        codes[k] = (uint8_t)fp6_code(S * w[k], &v);
+        r6 += std::fabs(S * w[k] - v);
+        sum6 += v;
+    }
+    const double u = 0x1p-24, m = (double)(c->N / 8) + 16.0, gamma = m * u / (1.0 - m * u);
+    const double extra = S * (9.0 * gamma * wsum + 0.5 * (double)c->N * std::ldexp(1.0, -c->shift) * (1.0 + 9.0 * gamma));
+    c->f6.R = (r6 + extra) * (1.0 + 1e-9) + 1e-9 * sum6;
+    c->f6.Tg = (float)(2.0 * sum6);  // exact: a multiple of 1/8 below 2^21
+    c->f6.NK = (uint32_t)((c->NP + 127) / 128);
+    c->fp6_rel = c->f6.R / std::max(sum6, 1e-300);
+    // the i8 top digit's: its residual (and the reference's rounding) against
+    // the top plane's digit sum, in the same fixed-point units
+    uint32_t top = 0;
+    for (uint32_t p = 0; p < 4; ++p)
+        if (c->wst.plane_mask >> p & 1) top = p;
+    const double r8 = (top > 0 ? (double)c->wst.resid[top - 1] : 0.0) + ref_extra_residual(c);
+    c->i8_rel = r8 / std::max(std::ldexp((double)c->wst.dsum[top], 8 * (int)top), 1e-300);
+    WLD_TRY(ensure(c->w6, c->NP));
+    WLD_TRY(ensure(c->f6a, fp6_a_bytes(c->LP, c->NP)));
+    WLD_TRY(ensure(c->f6b, fp6_b_bytes(c->LP, c->NP)));
+    HIP_TRY(hipMemcpyAsync(c->w6.p, codes.data(), c->NP, hipMemcpyHostToDevice, c->stream));
+    launch_frag6(ptr<uint8_t>(c->codes), ptr<uint8_t>(c->w6), c->LP, c->NP, ptr<uint8_t>(c->f6a), ptr<uint8_t>(c->f6b),
+                 c->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->f6.a6 = ptr<uint8_t>(c->f6a);
+    c->f6.b4 = ptr<uint8_t>(c->f6b);
+    c->fp6_ok = true;
+    c->fp6_better = c->fp6_rel <= 2.0 * c->i8_rel;
+    return WLD_OK;
 }
 
 int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint64_t *site_map,
@@ -311,6 +400,7 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     const unsigned all_planes = (1u << c->fixed_planes) - 1;
     c->plane_mask = c->kernel == WLD_KERNEL_MFMA && !c->opt_all_planes ? c->wst.plane_mask : all_planes;
     c->stats.load_ms = event_ms(c->ev[0], c->ev[1]);
+    WLD_TRY(fp6_prepare(c));
     c->stats.mfma_planes = c->kernel == WLD_KERNEL_MFMA ? __builtin_popcount(c->plane_mask) : 0;
     c->stats.kernel = c->kernel;
     c->stats.weight_shift = c->shift;
@@ -522,6 +612,7 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
                  const ScanArgs *scan = nullptr) {
     const uint32_t n = chunk_rows_of(c->L);
     bool sc = false;
+    c->fp6_pass = false;
     c->stats.ref_sums = c->opt_ref_sums ? 1 : 0;
     c->ref_pairs_pass = false;
     ValuLaunch rv{};
@@ -572,6 +663,8 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         }
         c->screened2 = m.screen && m.screen2;
         for (int t = 0; t < 3; ++t) m.resid[t] = c->wst.resid[t];
+        // the one-plane screen on fp6 x fp4 MFMA where the load allows it
+        m.fp6 = c->fp6_ok && (c->opt_fp6 == 2 || (c->opt_fp6 == 1 && c->fp6_better)) ? &c->f6 : nullptr;
         for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
         m.cand_list = ptr<uint32_t>(c->cand);
         // this pass's candidate set (the scan zeroes the other one, enqueue_pass)
@@ -598,6 +691,7 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
             launch_pair_valu(rv, o, nullptr, c->stream);  // the policy sends this threshold to the full kernel
         } else {
             sc = launch_pair_mfma(m, o, dense, c->stream, c->ev[6]);
+            c->fp6_pass = sc && m.fp6 && !m.screen2 && !m.ref_rows;  // (launch_pair_mfma's one-plane screen branch)
         }
     } else {
         launch_pair_valu(ValuLaunch{ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), ptr<uint8_t>(c->site_ok),
@@ -725,6 +819,11 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
             c->opt_host_batch_pairs = (uint64_t)value;
             break;
         case WLD_OPT_FUSED_SCAN: c->opt_fused_scan = value != 0; break;
+        case WLD_OPT_SCREEN_FP6:
+            if (value < 0 || value > 2) return fail(WLD_E_ARG, "WLD_OPT_SCREEN_FP6 takes 0 to 2");
+            c->opt_fp6 = (int)value;
+            c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = -1.0f;  // another screen's break-even
+            break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }
     return WLD_OK;
@@ -743,6 +842,7 @@ int wld_get_option(wld_ctx *c, int option, int64_t *value) {
         case WLD_OPT_STAGING_ROWS: *value = (int64_t)c->opt_staging_rows; break;
         case WLD_OPT_HOST_BATCH_PAIRS: *value = (int64_t)c->opt_host_batch_pairs; break;
         case WLD_OPT_FUSED_SCAN: *value = c->opt_fused_scan; break;
+        case WLD_OPT_SCREEN_FP6: *value = c->opt_fp6; break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }
     return WLD_OK;
@@ -1183,6 +1283,7 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     c->stats.pair_kernel_launches = c->n_tiles ? (c->ref_pairs_pass ? 3 : c->screened ? 2 : 1) : 0;
     c->stats.tiles = c->n_tiles;
     c->stats.screened = c->ref_pairs_pass ? 4 : c->screened ? (c->screened2 ? 3 : 1) : 0;
+    c->stats.screen_fp6 = c->fp6_pass ? 1 : 0;
     c->stats.candidate_pairs = c->ref_pairs_pass ? h[0] : 0;
     // auto: a threshold at which even the i8 screen leaves more than half the
     // tiles is not screened from now on (nor any lower one): the screen costs a

@@ -191,8 +191,8 @@ constexpr uint32_t kCandidateGrid = 2048;
 // workgroups (three per CU, 256 CUs); extra workgroups would only queue (and
 // cost dispatch time when there is no candidate at all)
 constexpr uint32_t kRefCandidateGrid = 768;
-// ... and of its 16-row-block items (one sub-block per wave: five per CU)
-constexpr uint32_t kRefItemGrid = 1280;
+// ... and of its items (ref_item_kernel<LOOP>, one sub-block per wave: four per CU)
+constexpr uint32_t kRefItemGrid = 1024;
 // lib.rs's order on f32 MFMA in work items of one sub-block per wave: the
 // candidate launch after a screen, and full runs of few tiles (0: whole
 // 64x64 tiles per workgroup, the round-3 shape; A/B builds only)
@@ -201,6 +201,21 @@ constexpr uint32_t kRefItemGrid = 1280;
 #endif
 // ... and of ref_sums_kernel / ref_compact_kernel (low-register: eight per CU)
 constexpr uint32_t kRefRowsGrid = 2048;
+
+// The fp6 screen's operands (pair_mfma.hip frag6_kernel) and constants: R
+// (residual bound of the rounded weights plus the reference's rounding) and
+// Tg (>= every doubled T), in the units of the fp6 weights (capi.hip).
+struct Fp6Screen {
+    const uint8_t *a6, *b4;
+    uint32_t NK;  // 128-sequence blocks
+    double R;
+    float Tg;
+};
+size_t fp6_a_bytes(size_t LP, size_t NP);
+size_t fp6_b_bytes(size_t LP, size_t NP);
+// w6: NP fp6 (e2m3) codes of the rounded weights (0 for padding)
+void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b4,
+                  hipStream_t s);
 
 struct MfmaLaunch {
     const uint8_t *codes;   // site-major codes (used when frag is null)
@@ -236,6 +251,8 @@ struct MfmaLaunch {
     // with a screen: the run's scan, fused into the screen's or the candidate
     // launch's last workgroup when scan.ticket is set
     ScanArgs scan;
+    // the one-plane screen on fp6 x fp4 MFMA instead of i8 (null: the i8 screen)
+    const Fp6Screen *fp6;
 };
 // Enqueues the MFMA pair kernel(s) of one pass; returns true when a screen
 // (one- or two-plane) ran (then screen_done, if given, is recorded between

@@ -455,7 +455,7 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
         // each term's f32 bits as an int: the maximum is > 0 iff some term is
         // > 0 (finite terms: integer sums <= 2^22)
         auto margin = [&](int i) {
-            const int2 p0 = acc.raw(0, i), p1 = acc.raw(1, i);  // (X, Y) of channel_a in, major
+            const auto p0 = acc.raw(0, i), p1 = acc.raw(1, i);  // (X, Y) of channel_a in, major
             float t2;
             const float t1 = r2_screen_terms_xy((float)p0.x, (float)p0.y, (float)p1.x, (float)p1.y, R2, thr_c, sc.E,
                                                 sc.mloc, t2);
@@ -803,6 +803,168 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
     }
 }
 
+// ---- fp6 screen (block-scaled MFMA, twice the i8 rate) ----------------------
+//
+// The one-plane screen's sums from v_mfma_scale_f32_16x16x128_f8f6f4 with fp6
+// (e2m3) A and fp4 (e2m1) B operands, unit block scales: 128 sequences per
+// instruction at the cycles of the i8 kernel's 64.  Every weight is rounded
+// to its nearest e2m3 value at a common scale S (w6_k = fp6(S w_k), a multiple
+// of 1/8 in [0, 7.5]); A = w6 where the a site's symbol is major or minor
+// ("in") or major, B = minor + 2 major of the b site (0, 1.0, 2.0).  Products
+// are exact and every sum is a multiple of 1/8 below 2^21, so the f32 MFMA
+// sums are the exact sums of the rounded weights, and the screen's f32 bound
+// (r2_screen_terms_xy on doubled sums, sound for any power-of-two unit) holds
+// with R = sum_k |S w_k - w6_k| plus the reference's rounding, in the same
+// units (capi.hip fp6_prepare).  Operands come pre-packed from memory (no
+// per-element VALU; the minor channel is raw & 0x22222222):
+//   a6 [16-site group][128-seq block kb][channel in, major][lane][24 B]: lane l
+//      = site l & 15, sequences 32 (l >> 4) + j at bits 6j (fp6_probe.hip)
+//   b4 [16-site group][kb][lane][16 B]: nibble j = fp4 of minor + 2 major
+// One 64x64 tile per 4-wave workgroup, four per CU; per 128 sequences each
+// wave LDS-DMAs its row block's A (3 KB) and its column block's B (1 KB)
+// into a double-buffered 16 KB stage; wave w computes a rows 16w.. against
+// the four column blocks (16 MFMAs per stage), then the screen epilogue.
+constexpr int kF6ABytes = 3072, kF6BBytes = 1024, kF6Stage = 4 * kF6ABytes + 4 * kF6BBytes;
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+size_t fp6_a_bytes(size_t LP, size_t NP) { return LP / 16 * ((NP + 127) / 128) * kF6ABytes; }
+size_t fp6_b_bytes(size_t LP, size_t NP) { return LP / 16 * ((NP + 127) / 128) * kF6BBytes; }
+
+// one thread per (16-site group, 128-sequence block, lane)
+__global__ __launch_bounds__(256) void frag6_kernel(const uint8_t *__restrict__ codes, const uint8_t *__restrict__ w6,
+                                                     uint32_t LP, uint32_t NP, uint8_t *__restrict__ a6,
+                                                     uint8_t *__restrict__ b4) {
+    const uint32_t NK = (NP + 127) / 128;
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (size_t)LP / 16 * NK * 64) return;
+    const uint32_t lane = idx & 63;
+    const size_t t = idx >> 6, g16 = t / NK;
+    const uint32_t kb = (uint32_t)(t % NK);
+    const uint8_t *row = codes + (g16 * 16 + (lane & 15)) * (size_t)NP;
+    const uint32_t k0 = 128 * kb + 32 * (lane >> 4);
+    uint32_t ai[6] = {0, 0, 0, 0, 0, 0}, am[6] = {0, 0, 0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+    for (uint32_t j = 0; j < 32; ++j) {
+        const uint32_t k = k0 + j;
+        const uint32_t c = k < NP ? row[k] : 0u, v = k < NP ? w6[k] : 0u;
+        const uint32_t vi = (c & kCodeIn) ? v : 0u, vm = (c & kCodeMaj) ? v : 0u;
+        const uint32_t bit = 6 * j, d = bit >> 5, o = bit & 31;
+        ai[d] |= vi << o;
+        am[d] |= vm << o;
+        if (o > 26) {
+            ai[d + 1] |= vi >> (32 - o);
+            am[d + 1] |= vm >> (32 - o);
+        }
+        b[j >> 3] |= ((c & kCodeIn) ? ((c & kCodeMaj) ? 4u : 2u) : 0u) << (4 * (j & 7));
+    }
+    uint32_t *pa = reinterpret_cast<uint32_t *>(a6 + ((g16 * NK + kb) * 2) * (size_t)1536 + lane * 24);
+    uint32_t *pm = pa + 1536 / 4;
+    for (int d = 0; d < 6; ++d) pa[d] = ai[d], pm[d] = am[d];
+    *reinterpret_cast<uint4 *>(b4 + (g16 * NK + kb) * (size_t)kF6BBytes + lane * 16) = make_uint4(b[0], b[1], b[2], b[3]);
+}
+
+// the wave's 16 a rows x 64 b columns as f32 sums of fp6 x fp4 products:
+// [n][channel_a in / major][channel_b X = S(minor + 2 major) / Y = S(minor)]
+// (the layout of Acc16<1, 4>: C/D col = lane & 15, row = 4 (lane >> 4) + e)
+struct AccF6 {
+    static constexpr int kPlanes = 1;
+    static constexpr int kPairs = 16;
+    v4f v[4][2][2];
+    __device__ __forceinline__ float2 raw(int x, int i) const {
+        return make_float2(v[i >> 2][x][0][i & 3], v[i >> 2][x][1][i & 3]);
+    }
+    static __device__ __forceinline__ uint32_t a_local(int i, uint32_t wave, uint32_t lane) {
+        return 16 * (wave & 3) + 4 * (lane >> 4) + (i & 3);
+    }
+    static __device__ __forceinline__ uint32_t b_local(int i, uint32_t wave, uint32_t lane) {
+        return 16 * (i >> 2) + (lane & 15);
+    }
+};
+
+__global__ __launch_bounds__(256, 4) void pair_fp6_screen_kernel(const uint8_t *__restrict__ a6,
+                                                                  const uint8_t *__restrict__ b4,
+                                                                  const uint64_t *__restrict__ ok_bits,
+                                                                  const uint32_t *__restrict__ tiles, uint32_t NK,
+                                                                  uint32_t L, uint32_t n_chunk_rows, float thr,
+                                                                  OrderArgs o, ScreenArgs sc) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6Stage];
+    __shared__ unsigned long long sBits[kTile];
+    __shared__ uint32_t sRowBase[kTile];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
+    const uint32_t tile = tiles[blockIdx.x];
+    if (tile == kNoTile) return;  // padding of an XCD-ordered list (whole workgroup)
+    const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint8_t *srcA = a6 + (size_t)(4 * ta + wave) * NK * kF6ABytes;  // wave-uniform
+    const uint8_t *srcB = b4 + (size_t)(4 * tb + wave) * NK * kF6BBytes;
+    const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
+    auto issue = [&](uint32_t kb, uint32_t buf) {
+        const uint32_t gb = lds + buf * kF6Stage;
+        const uint8_t *a = srcA + (size_t)kb * kF6ABytes;
+        glds16_s(a, lane16, gb + wave * kF6ABytes);
+        glds16_s(a + 1024, lane16, gb + wave * kF6ABytes + 1024);
+        glds16_s(a + 2048, lane16, gb + wave * kF6ABytes + 2048);
+        glds16_s(srcB + (size_t)kb * kF6BBytes, lane16, gb + 4 * kF6ABytes + wave * kF6BBytes);
+    };
+    issue(0, 0);
+    const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
+    AccF6 acc;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) acc.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+    uint32_t buf = 0;
+    for (uint32_t kb = 0; kb < NK; ++kb) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this stage landed
+        __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
+        asm volatile("" ::: "memory");
+        if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
+        const uint8_t *g = smem + buf * kF6Stage;
+        const uint8_t *pa = g + wave * kF6ABytes + lane * 24;
+        const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
+                    i2 = *reinterpret_cast<const uint2 *>(pa + 16);
+        const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536), m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
+                    m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
+        const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
+        const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const uint4 r = *reinterpret_cast<const uint4 *>(g + 4 * kF6ABytes + n * kF6BBytes + lane * 16);
+            constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
+            const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
+            const v8i bmin = {(int)r.x & kMinor, (int)r.y & kMinor, (int)r.z & kMinor, (int)r.w & kMinor, 0, 0, 0, 0};
+            acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, braw, acc.v[n][0][0], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+            acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc.v[n][0][1], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+            acc.v[n][1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, braw, acc.v[n][1][0], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+            acc.v[n][1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, bmin, acc.v[n][1][1], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
+        buf ^= 1;
+    }
+    // (the f64 fallback of pair_cand: exact sums from X, Y; the launch uses
+    // the f32 test, sc.f32 == 2)
+    auto sum = [&](int x, int y, int i) -> double {
+        const float2 p = acc.raw(x, i);
+        return ((double)p.x + (y ? -(double)p.y : (double)p.y)) * 0.5;
+    };
+    const DenseArgs dn{nullptr, nullptr, nullptr, nullptr};
+    tile_epilogue<kModeScreen, AccF6>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, 0, o, dn, sc, sBits,
+                                      sRowBase);
+}
+
+void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b4,
+                  hipStream_t s) {
+    const size_t n = LP / 16 * ((NP + 127) / 128) * 64;
+    hipLaunchKernelGGL(frag6_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, codes, w6, (uint32_t)LP,
+                       (uint32_t)NP, a6, b4);
+}
+
 // Site-major variant (one tile per workgroup, codes read straight into
 // registers, all three digit planes): the reference for the LDS path's race
 // screen (WLD_OPT_MFMA_LAYOUT).
@@ -1021,6 +1183,19 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
         if ((double)sc.Rf < sc.R) sc.Rf = nextafterf(sc.Rf, INFINITY);
         sc.f32 = 0;
         launch_lds<kModeScreen, 2>(m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, lo | (top << 2), o, dn, sc, s);
+        if (screen_done) (void)hipEventRecord(screen_done, s);
+        launch_candidates(m, n, idx, ok_bits, o, dn, sc, s);
+        return true;
+    }
+    if (m.fp6) {
+        // the fp6 screen: R and the sums' bound Tg in its own units (fp6_prepare)
+        sc.R = m.fp6->R;
+        sc.Rf = (float)sc.R;
+        if ((double)sc.Rf < sc.R) sc.Rf = nextafterf(sc.Rf, INFINITY);
+        sc.f32 = 2;
+        screen_consts(m.fp6->Tg, 2.0f * sc.Rf, sc.E, sc.mloc);
+        hipLaunchKernelGGL(pair_fp6_screen_kernel, dim3(m.n_tiles), dim3(256), 0, s, m.fp6->a6, m.fp6->b4, ok_bits,
+                           m.tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
         if (screen_done) (void)hipEventRecord(screen_done, s);
         launch_candidates(m, n, idx, ok_bits, o, dn, sc, s);
         return true;

@@ -574,6 +574,214 @@ __global__ __launch_bounds__(256) void ref_layout_kernel(const uint8_t *__restri
     if (s == 0) rw[p] = seq < N ? w[seq] : 0.0f;
 }
 
+// Work items of lib.rs's order on f32 MFMA with no LDS staging: an item is
+// up to four 16x16 sub-blocks of one 64x64 tile (`bits`), one per wave (the
+// u-th computed sub-block in column-major order goes to wave u), owning the
+// 16-row blocks `owned` of the tile's segments.  Each wave reads its own
+// operands straight from the lane-class layout (L2-resident): per 64-position
+// stage, lane (r, g) loads the dword of its a row and of its b row at 16 grp
+// + 4 g (elements 16 grp + 4 e + g, e = 0..3, of the four 16-element groups
+// grp) and the four weights beside them, one stage ahead of the MFMAs; the
+// waves never wait for each other before the epilogue.  Same sums, same
+// order, same epilogue as pair_valu_kernel<MF, REF> (bit-identical rows).
+// LOOP: the candidate launch over the screen's item list (buckets, work
+// counter, fused chunk scan); else the full run's tiles in four 16-row items
+// each (workgroup 4t + q: tile t's row block q).
+#ifndef WLD_REF_ITEM_WG
+#define WLD_REF_ITEM_WG 5  // workgroups per CU, full runs (<= 102 VGPRs, no spill)
+#endif
+#ifndef WLD_REF_ITEML_WG
+#define WLD_REF_ITEML_WG 4  // ... the candidate loop (its loop state: <= 128 VGPRs)
+#endif
+template <bool LOOP>
+__global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) void ref_item_kernel(
+    const uint8_t *__restrict__ rcodes, const float *__restrict__ rw, const uint8_t *__restrict__ site_ok,
+    const uint32_t *__restrict__ tiles, uint32_t n_tiles, const uint32_t *__restrict__ tile_bits,
+    unsigned *tile_work, const unsigned *tile_buckets, uint32_t bucket_cap, uint32_t L, uint32_t NPr,
+    uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, OrderArgs o, ScanArgs sa) {
+    __shared__ unsigned long long sBits[kTile];  // compaction: passing b per a row
+    __shared__ uint32_t sRowBase[kTile];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    auto compute_item = [&](uint32_t tile, uint32_t bits, uint32_t owned) {
+        const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
+        const uint32_t a0 = ta * kTile, b0 = tb * kTile;
+        // this wave's sub-block: the wave-th set bit in column-major order
+        uint32_t cm = 0;
+        for (uint32_t k = 0; k < 16; ++k) cm |= ((bits >> (4 * (k & 3) + (k >> 2))) & 1u) << k;
+        for (uint32_t t = 0; t < wave; ++t) cm &= cm - 1u;
+        cm = __builtin_amdgcn_readfirstlane(cm);
+        const bool has = cm != 0;
+        const uint32_t kq = has ? (uint32_t)__builtin_ctz(cm) : 0u, ui = kq & 3u, un = kq >> 2;
+        // lane (r, g) holds the pairs (a = 16 ui + 4 g + e, b = 16 un + r), e = 0..3
+        float tot[4][4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) tot[e][q] = 0.0f;
+        if (has) {
+            const uint8_t *rowA = rcodes + (size_t)(a0 + 16 * ui + r) * NPr + 4 * g;
+            const uint8_t *rowB = rcodes + (size_t)(b0 + 16 * un + r) * NPr + 4 * g;
+            const float *wg = rw + 4 * g;
+            const uint32_t cls = 64 * ref_cs, n_st = 8 * ref_cs;
+            uint32_t ca[4], cb[4];
+            float4 cw[4];
+            auto fetch = [&](uint32_t k0) {
+#pragma unroll
+                for (int grp = 0; grp < 4; ++grp) {
+                    ca[grp] = *reinterpret_cast<const uint32_t *>(rowA + k0 + 16 * grp);
+                    cb[grp] = *reinterpret_cast<const uint32_t *>(rowB + k0 + 16 * grp);
+                    cw[grp] = *reinterpret_cast<const float4 *>(wg + k0 + 16 * grp);
+                }
+            };
+            if (n_st) fetch(0);
+            v4f acc[4];
+            for (uint32_t st = 0; st < n_st; ++st) {
+                if (st % ref_cs == 0)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[q] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+                uint32_t A[4], B[4];
+                float4 Wt[4];
+#pragma unroll
+                for (int grp = 0; grp < 4; ++grp) A[grp] = ca[grp], B[grp] = cb[grp], Wt[grp] = cw[grp];
+                if (st + 1 < n_st) fetch(64 * (st + 1));  // (classes are consecutive: stage st at 64 st)
+#pragma unroll
+                for (int grp = 0; grp < 4; ++grp) {
+                    const float we[4] = {Wt[grp].x, Wt[grp].y, Wt[grp].z, Wt[grp].w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const uint32_t xa = A[grp] >> (8 * e), xb = B[grp] >> (8 * e);
+                        const float u = (xa & kCodeIn) ? we[e] : 0.0f, v = (xa & kCodeMaj) ? we[e] : 0.0f;
+                        const float fi = (float)(xb & 1u), fm = (float)((xb >> 1) & 1u);
+                        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fi, acc[0], 0, 0, 0);
+                        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fi, acc[1], 0, 0, 0);
+                        acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fm, acc[2], 0, 0, 0);
+                        acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fm, acc[3], 0, 0, 0);
+                    }
+                }
+                // end of a class: its chain joins the ordered horizontal sum
+                if ((st + 1) % ref_cs == 0)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) tot[e][q] += acc[q][e];
+            }
+            (void)cls;
+            // the scalar tail (lib.rs:461-480), onto the horizontal sums in order
+            for (uint32_t t = 0; t < ref_tail_n; ++t) {
+                const uint32_t p = 8 * cls + t;
+                const float we = rw[p];
+                const uint32_t xb = rcodes[(size_t)(b0 + 16 * un + r) * NPr + p];
+                const float fi = (float)(xb & 1u), fm = (float)(xb >> 1);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t xa = rcodes[(size_t)(a0 + 16 * ui + 4 * g + e) * NPr + p];
+                    const float u = (xa & kCodeIn) ? we : 0.0f, v = (xa & kCodeMaj) ? we : 0.0f;
+                    tot[e][0] = __builtin_fmaf(u, fi, tot[e][0]);
+                    tot[e][1] = __builtin_fmaf(v, fi, tot[e][1]);
+                    tot[e][2] = __builtin_fmaf(u, fm, tot[e][2]);
+                    tot[e][3] = __builtin_fmaf(v, fm, tot[e][3]);
+                }
+            }
+        }
+        // ---- epilogue (lib.rs:482-520, 660) --------------------------------
+        uint32_t passmask = 0;  // bit e
+        float res[4][3];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t al = 16 * ui + 4 * g + e, bl = 16 * un + r, a = a0 + al, b = b0 + bl;
+            float d, dp, r2;
+            ld_epilogue(tot[e][0], tot[e][1], tot[e][2], tot[e][3], d, dp, r2);
+            res[e][0] = d;
+            res[e][1] = dp;
+            res[e][2] = r2;
+            if (has && a < b && b < L && site_ok[a] && site_ok[b] && r2 > thr) passmask |= 1u << e;
+        }
+        // ---- compaction: the tile's 64x64 pass bits, rows in b order ---------
+        const bool own_row = tid < kTile && ((owned >> (tid >> 4)) & 1u);
+        const uint32_t quarters = (uint32_t)__popc(owned);
+        if (!__syncthreads_or(passmask != 0)) {
+            if (own_row) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
+            if (tid == 0) tile_done(o, ta, tb, n_chunk_rows, quarters);
+            return;
+        }
+        if (tid < kTile) sBits[tid] = 0ull;
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (passmask & (1u << e)) atomicOr(&sBits[16 * ui + 4 * g + e], 1ull << (16 * un + r));
+        __syncthreads();
+        if (tid < kTile) {
+            const uint32_t row = tid;
+            const uint32_t cnt = __popcll(sBits[row]);
+            const uint32_t incl = wave_inclusive_scan(cnt);
+            const uint32_t excl = incl - cnt;
+            const uint32_t total = __shfl(incl, 63, 64);
+            unsigned long long base = 0;
+            if (row == 63 && total) base = atomicAdd(o.cursor, (unsigned long long)total);
+            base = __shfl(base, 63, 64);
+            sRowBase[row] = (uint32_t)base + excl;
+            if (own_row) {  // (a row outside the item's blocks has no pass: cnt 0)
+                o.seg_cnt[(size_t)(a0 + row) * o.T + tb] = (uint8_t)cnt;
+                o.seg_off[(size_t)(a0 + row) * o.T + tb] = (uint32_t)base + excl;
+            }
+            if (row == 63 && total)
+                atomicAdd(&o.chunk_total[chunk_linear(n_chunk_rows, ta / kTilesPerChunk, tb / kTilesPerChunk)], total);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (!(passmask & (1u << e))) continue;
+            const uint32_t al = 16 * ui + 4 * g + e, bl = 16 * un + r;
+            const uint64_t pos = (uint64_t)sRowBase[al] + __popcll(sBits[al] & ((1ull << bl) - 1ull));
+            if (pos < o.st_capacity) {
+                o.st_a[pos] = a0 + al;
+                o.st_b[pos] = b0 + bl;
+                o.st_d[pos] = res[e][0];
+                o.st_dp[pos] = res[e][1];
+                o.st_r2[pos] = res[e][2];
+            }
+        }
+        if (tid == 0) tile_done(o, ta, tb, n_chunk_rows, quarters);
+    };
+
+    if constexpr (!LOOP) {
+        const uint32_t tile = tiles[blockIdx.x >> 2], q = blockIdx.x & 3;
+        if (tile != kNoTile) compute_item(tile, 0xFu << (4 * q), 1u << q);  // kNoTile: padding of an XCD-ordered list
+    } else {
+        // the screen's items, heaviest bucket first; the first by workgroup id
+        // (rounds dealt in snake order, heavy beside light on a CU), the next
+        // from the work counter (zeroed by the screen); every entry and its
+        // tile checked before anything is read through them
+        __shared__ uint32_t s_next, s_pre[17];
+        cand_prefix(tile_buckets, s_pre);
+        const uint32_t nt = s_pre[16];
+        uint32_t first = blockIdx.x;
+        {
+            constexpr uint32_t R = WLD_REF_ITEML_WG;
+            const uint32_t m = gridDim.x / R, k = m ? blockIdx.x / m : R, j = blockIdx.x - (k < R ? k * m : 0u);
+            if (k < R) first = (k & 1) ? (k + 1) * m - 1 - j : k * m + j;
+        }
+        for (uint32_t bi = first; bi < nt;) {
+            const uint32_t e = cand_entry_checked(o, s_pre, bucket_cap, bi);
+            const uint32_t tile = e != ~0u ? tiles[e] : kNoTile;
+            const uint32_t bits = e != ~0u ? tile_bits[e] : 0u;
+            uint32_t owned = 0;
+            for (uint32_t q = 0; q < 4; ++q) owned |= ((bits >> (4 * q)) & 0xFu) ? 1u << q : 0u;
+            if (tile_in_range(tile, L) && bits && __popc(bits) <= 4)
+                compute_item(tile, bits, owned);
+            else if (e != ~0u && threadIdx.x == 0)
+                report_guard(o, kGuardTile);
+            if (threadIdx.x == 0) s_next = gridDim.x + atomicAdd(tile_work, 1u);
+            __syncthreads();  // (also: the next item's compaction reuses the LDS)
+            bi = s_next;
+            __syncthreads();
+        }
+        scan_tail(sa, nt, false, first);
+    }
+}
+
 // One class chain of lib.rs's four sums (lib.rs:416-480) over positions
 // [q0, q1) of the lane-class layout, in element order: adds of selected
 // weights, lib.rs's select + add.  A 16-position group holds element 4j + g at
@@ -804,9 +1012,11 @@ void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
             else launch_v<true, false, true, true, false>(v, grid, flush, cs, o, dn, s);
         } else if (v.tile_count) {
             if (v.safe) launch_v<false, true, false, true, true>(v, grid, flush, cs, o, dn, s);
-            else if (v.rb_items)  // 16-row-block items, one sub-block per wave, six workgroups per CU
-                launch_v<false, false, true, true, true, 1>(v, std::min<uint32_t>(4 * v.n_tiles, kRefItemGrid), flush,
-                                                             cs, o, dn, s);
+            else if (v.rb_items)  // items of <= 4 sub-blocks, one per wave, no LDS staging
+                hipLaunchKernelGGL(ref_item_kernel<true>, dim3(std::min<uint32_t>(4 * v.n_tiles, kRefItemGrid)),
+                                   dim3(256), 0, s, v.codes, v.w, v.site_ok, v.tiles, v.n_tiles, v.tile_bits,
+                                   v.tile_work, v.tile_buckets, v.bucket_cap, v.L, v.NP, cs, v.ref_tail_n,
+                                   v.n_chunk_rows, v.thr, o, v.scan);
             else launch_v<false, false, true, true, true>(v, grid, flush, cs, o, dn, s);
         } else {
             // every tile of the run: with fewer tiles than four rounds of
@@ -814,7 +1024,9 @@ void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
             // four 16-row blocks are separate work items (f32 MFMA path)
             if (v.safe) launch_v<false, true, false, true, false>(v, grid, flush, cs, o, dn, s);
             else if (WLD_REF_ITEMS && v.n_tiles <= 4 * kRefCandidateGrid)
-                launch_v<false, false, true, true, false, 1>(v, grid, flush, cs, o, dn, s, 4);
+                hipLaunchKernelGGL(ref_item_kernel<false>, dim3(4 * grid), dim3(256), 0, s, v.codes, v.w, v.site_ok,
+                                   v.tiles, v.n_tiles, nullptr, nullptr, nullptr, 0u, v.L, v.NP, cs, v.ref_tail_n,
+                                   v.n_chunk_rows, v.thr, o, ScanArgs{});
             else launch_v<false, false, true, true, false>(v, grid, flush, cs, o, dn, s);
         }
         return;
