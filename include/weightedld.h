@@ -213,7 +213,9 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *                      MFMA (128 sequences per instruction, twice the i8
  *                      rate) when the weights are nonnegative, at most 16,384
  *                      sequences, and their fp6 rounding leaves a residual
- *                      within twice the i8 top digit's; 0: the i8 screen;
+ *                      within 2% of the sums or twice the i8 top digit's, at
+ *                      thresholds above any at which it left more than a
+ *                      quarter of the tiles as candidates; 0: the i8 screen;
  *                      2: fp6 whenever it applies.  Same rows (a screen only
  *                      decides which tiles are computed).
  *   WLD_OPT_FUSED_SCAN 1 (default): after a screen, the run's chunk scan runs

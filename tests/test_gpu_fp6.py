@@ -105,6 +105,27 @@ def test_fp6_exact_mode_rows(W):
         _bits_equal(a.rows(), _store_dict(b.rows()))
 
 
+def test_fp6_handover_to_i8(W):
+    """Auto policy: at a threshold where the fp6 screen leaves more than a
+    quarter of the tiles as candidates, the next pass (and any at a lower
+    threshold) screens on i8; higher thresholds stay on fp6.  Rows equal the
+    oracle's throughout."""
+    import bench
+    buf = bench.synth(2048, 2000)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    c = W.Context(0)
+    c.load(buf, w)
+    seen = []
+    for thr in (0.002, 0.002, 0.001, 0.05):
+        c.run(thr)
+        st = c.stats()
+        seen.append((thr, st["screened"], st["screen_fp6"], st["candidate_tiles"], st["tiles"]))
+        _bits_equal(c.rows(), O.all_pairs(buf, w, np.float32(thr)))
+    assert seen[0][1] == 1 and seen[0][2] == 1 and seen[0][3] * 4 > seen[0][4], seen
+    assert seen[1][2] == 0 and seen[2][2] == 0 and seen[3][1:3] == (1, 1), seen
+    c.close()
+
+
 def test_fp6_default_on_bench_data_and_ineligible_weights(W):
     """Auto: the bench's Henikoff weights (nearly equal) take the fp6 screen;
     mixed-sign weights never do (its bound assumes nonnegative cells)."""

@@ -333,6 +333,7 @@ def test_ref_screen_policy(W):
     # pairs; then the full f32 kernel.  Rows bit-identical to the oracle at
     # every step of the policy.
     ctx = W.Context(0, W.KERNEL_AUTO)
+    ctx.set_option("screen_fp6", 0)  # the i8 tiers (test_gpu_fp6.py: the fp6 screen's handover)
     buf = synth(2000, 2000, 23)
     w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
     ctx.load(buf, w)

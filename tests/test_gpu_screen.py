@@ -265,6 +265,7 @@ def test_screen_auto_policy(W, ctxs):
     w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
     ctx.load(buf, w)
     assert ctx.get_option("screen") == 1
+    ctx.set_option("screen_fp6", 0)  # the i8 tiers' policy (test_gpu_fp6.py: the fp6 screen's handover)
     seen = []
     for thr in (0.002, 0.002, 0.001, 0.05, 0.001, 0.003):
         ctx.run(thr)
@@ -282,6 +283,7 @@ def test_screen_auto_policy(W, ctxs):
     ctx.set_option("screen", 0)
     rows0 = (ctx.run(0.001), ctx.rows())
     ctx.set_option("screen", 1)
+    ctx.set_option("screen_fp6", 1)
     assert rows2[2] == 1 and rows2[0] == rows0[0]
     _same_rows(rows2[1], rows0[1])
 

@@ -113,6 +113,9 @@ struct wld_ctx {
     // auto: the largest threshold at which the screen left > half the tiles,
     // and at which the two-plane screen left > a fifth
     float screen_bad_thr = -1.0f;
+    // auto: the largest threshold at which the fp6 screen left more than a
+    // quarter of the tiles (there and below, the i8 screen's tighter bound)
+    float fp6_bad_thr = -1.0f;
     float screen2_bad_thr = -1.0f;
     // auto, lib.rs's order: the largest threshold at which the exact candidate
     // pairs were more than a tenth of all pairs (then the full f32 kernel)
@@ -303,7 +306,7 @@ int fp6_prepare(wld_ctx *c) {
     c->f6.a6 = ptr<uint8_t>(c->f6a);
     c->f6.b4 = ptr<uint8_t>(c->f6b);
     c->fp6_ok = true;
-    c->fp6_better = c->fp6_rel <= 2.0 * c->i8_rel;
+    c->fp6_better = c->fp6_rel <= std::max(2.0 * c->i8_rel, 0.02);
     return WLD_OK;
 }
 
@@ -312,7 +315,7 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     const size_t L = c->L, N = c->N;
     // a new data set: the auto screen policy (thresholds learned on the last
     // one) starts over; the reference-order layout is rebuilt when needed
-    c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = -1.0f;
+    c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = c->fp6_bad_thr = -1.0f;
     c->have_ref = false;
     c->LP = round_up(std::max<size_t>(L, 1), kChunk);
     c->NP = round_up(std::max<size_t>(N, 1), kSeqPad);
@@ -664,7 +667,8 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         c->screened2 = m.screen && m.screen2;
         for (int t = 0; t < 3; ++t) m.resid[t] = c->wst.resid[t];
         // the one-plane screen on fp6 x fp4 MFMA where the load allows it
-        m.fp6 = c->fp6_ok && (c->opt_fp6 == 2 || (c->opt_fp6 == 1 && c->fp6_better)) ? &c->f6 : nullptr;
+        m.fp6 = c->fp6_ok && (c->opt_fp6 == 2 || (c->opt_fp6 == 1 && c->fp6_better && thr > c->fp6_bad_thr))
+                    ? &c->f6 : nullptr;
         for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
         m.cand_list = ptr<uint32_t>(c->cand);
         // this pass's candidate set (the scan zeroes the other one, enqueue_pass)
@@ -792,7 +796,7 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
         case WLD_OPT_SCREEN:
             if (value < 0 || value > 4) return fail(WLD_E_ARG, "WLD_OPT_SCREEN takes 0 to 4");
             c->opt_screen = (int)value;
-            c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = -1.0f;
+            c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = c->fp6_bad_thr = -1.0f;
             break;
         case WLD_OPT_TILE_ORDER:
             c->opt_tile_rows = value != 0;
@@ -808,7 +812,7 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
         case WLD_OPT_VALU_PLAIN: c->opt_valu_plain = value != 0; break;
         case WLD_OPT_REF_SUMS:
             c->opt_ref_sums = value != 0;
-            c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = -1.0f;  // the policy's break-even differs
+            c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = c->fp6_bad_thr = -1.0f;  // the policy's break-even differs
             break;
         case WLD_OPT_STAGING_ROWS:
             if (value < 1) return fail(WLD_E_ARG, "WLD_OPT_STAGING_ROWS must be >= 1");
@@ -822,7 +826,7 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
         case WLD_OPT_SCREEN_FP6:
             if (value < 0 || value > 2) return fail(WLD_E_ARG, "WLD_OPT_SCREEN_FP6 takes 0 to 2");
             c->opt_fp6 = (int)value;
-            c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = -1.0f;  // another screen's break-even
+            c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = c->fp6_bad_thr = -1.0f;  // another screen's break-even
             break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }
@@ -1296,8 +1300,13 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     // time at BASELINE config 4, archive/profiles_r01_r03/r02s2/) leaves more than a fifth
     // goes to the full kernel (the exact mode; lib.rs's order takes the two-
     // plane screen only when asked, WLD_OPT_SCREEN 3)
-    if (c->screened && !c->ref_pairs_pass && !c->screened2 && h[2] * 2 > c->n_tiles)
+    // ... the fp6 screen first hands over to the i8 one (a tighter bound at
+    // twice the cost) once it leaves more than a quarter of the tiles
+    if (c->fp6_pass && h[2] * 4 > c->n_tiles) {
+        c->fp6_bad_thr = std::max(c->fp6_bad_thr, r.thr);
+    } else if (c->screened && !c->ref_pairs_pass && !c->screened2 && h[2] * 2 > c->n_tiles) {
         c->screen_bad_thr = std::max(c->screen_bad_thr, r.thr);
+    }
     if (c->screened && c->screened2 && h[2] * 5 > c->n_tiles) c->screen2_bad_thr = std::max(c->screen2_bad_thr, r.thr);
     // exact candidate pairs, each summed alone in lib.rs's order (~1 ms per
     // million at C4 size): past a tenth of all pairs the full f32 kernel

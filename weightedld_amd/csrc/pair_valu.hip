@@ -63,6 +63,11 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 // ty + 16i), so the epilogue and compaction only change how a row slot maps
 // to a.  The VALU's code extraction then overlaps the matrix pipe instead of
 // competing with the FMAs for VALU issue.
+// the reference-order item kernel: ref_item_kernel (1) or the LDS-staged
+// one-slot pair_valu_kernel (0; A/B builds)
+#ifndef WLD_REF_ITEM_KERNEL
+#define WLD_REF_ITEM_KERNEL 1
+#endif
 #ifndef WLD_VALU_MF_WG
 #define WLD_VALU_MF_WG 2  // MF: 164 VGPRs would fit 3 per CU; measured equal
 #endif
@@ -652,8 +657,12 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const uint32_t xa = A[grp] >> (8 * e), xb = B[grp] >> (8 * e);
+#ifndef WLD_DIAG_NOSEL
                         const float u = (xa & kCodeIn) ? we[e] : 0.0f, v = (xa & kCodeMaj) ? we[e] : 0.0f;
                         const float fi = (float)(xb & 1u), fm = (float)((xb >> 1) & 1u);
+#else  // diagnostic (wrong sums): the operands without their selects and converts
+                        const float u = we[e], v = __uint_as_float(xa), fi = __uint_as_float(xb), fm = we[e];
+#endif
                         acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fi, acc[0], 0, 0, 0);
                         acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fi, acc[1], 0, 0, 0);
                         acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fm, acc[2], 0, 0, 0);
@@ -1012,6 +1021,9 @@ void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
             else launch_v<true, false, true, true, false>(v, grid, flush, cs, o, dn, s);
         } else if (v.tile_count) {
             if (v.safe) launch_v<false, true, false, true, true>(v, grid, flush, cs, o, dn, s);
+            else if (v.rb_items && !WLD_REF_ITEM_KERNEL)
+                launch_v<false, false, true, true, true, 1>(v, std::min<uint32_t>(4 * v.n_tiles, 1280u), flush, cs, o,
+                                                             dn, s);
             else if (v.rb_items)  // items of <= 4 sub-blocks, one per wave, no LDS staging
                 hipLaunchKernelGGL(ref_item_kernel<true>, dim3(std::min<uint32_t>(4 * v.n_tiles, kRefItemGrid)),
                                    dim3(256), 0, s, v.codes, v.w, v.site_ok, v.tiles, v.n_tiles, v.tile_bits,
@@ -1023,6 +1035,8 @@ void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
             // resident workgroups (BASELINE config 2: 528 tiles), each tile's
             // four 16-row blocks are separate work items (f32 MFMA path)
             if (v.safe) launch_v<false, true, false, true, false>(v, grid, flush, cs, o, dn, s);
+            else if (WLD_REF_ITEMS && !WLD_REF_ITEM_KERNEL && v.n_tiles <= 4 * kRefCandidateGrid)
+                launch_v<false, false, true, true, false, 1>(v, grid, flush, cs, o, dn, s, 4);
             else if (WLD_REF_ITEMS && v.n_tiles <= 4 * kRefCandidateGrid)
                 hipLaunchKernelGGL(ref_item_kernel<false>, dim3(4 * grid), dim3(256), 0, s, v.codes, v.w, v.site_ok,
                                    v.tiles, v.n_tiles, nullptr, nullptr, nullptr, 0u, v.L, v.NP, cs, v.ref_tail_n,
