@@ -40,6 +40,9 @@ CONFIGS = {
 }
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 I8_MFMA_PEAK_TOPS = 5000.0  # dense i8 MFMA = 2x bf16 dense 2.5 PF (MI355X_MICROARCH.md Matrix cores)
+# dense fp6/fp4 block-scaled MFMA (v_mfma_scale_f32_16x16x128_f8f6f4 with e2m3 x
+# e2m1 operands: 4x bf16 per clock, MI355X_MICROARCH.md Matrix cores FP6 row)
+FP6_MFMA_PEAK_TFLOPS = 10000.0
 F32_VALU_PEAK_TFLOPS = 157.3  # FP32 vector peak (spec) = f32-input MFMA peak
 
 
@@ -517,6 +520,7 @@ def main():
     # 0 none, 1 i8 one-plane screen, 3 two-plane screen, 4 exact candidate pairs
     screen_kind = ctx.stats()["screened"]
     screened = bool(screen_kind)
+    fp6 = screen_kind == 1 and bool(ctx.stats()["screen_fp6"])  # the one-plane screen on fp6 x fp4 MFMA
     n_tiles = ctx.stats()["tiles"]
     # the same steps without the screen (every tile, every plane; same rows),
     # reported alongside: a few sequential runs after the timed region
@@ -594,11 +598,14 @@ def main():
     # without a screen in front (thresholds <= 0, --no-screen)
     f32_path = kern_name == "valu" or (args.ref_sums and not screened)
     if not f32_path:
-        # the dominant kernel's peak: dense i8 MFMA (no sparsity)
-        peak, unit = I8_MFMA_PEAK_TOPS, "TFLOP/s"
+        # the dominant kernel's peak: dense i8 MFMA, or dense fp6 MFMA for the
+        # fp6 screen (no sparsity in either)
+        peak, unit = (FP6_MFMA_PEAK_TFLOPS if fp6 else I8_MFMA_PEAK_TOPS), "TFLOP/s"
         dom_ms = screen_ms if screened else kernel_ms
         achieved = alg_ops / (dom_ms * 1e-3) / 1e12
-        if screen_kind == 4:
+        if fp6:
+            kname = "pair_fp6_screen_kernel<fp6 x fp4 16x16x128>"
+        elif screen_kind == 4:
             kname = "pair_mfma_kernel<candidate pairs, %d planes>" % min(planes, 2)
         elif screened:
             kname = "pair_mfma_kernel<screen,%d plane%s>" % ((2, "s") if screen_kind == 3 else (1, ""))
@@ -612,7 +619,8 @@ def main():
         ex_planes = (2 if screen_kind == 3 else 1) if screened and screen_kind != 4 else \
             min(planes, 2) if screen_kind == 4 else planes
         roof["executed_frac"] = shard_pairs * 8.0 * ex_planes * N / (dom_ms * 1e-3) / 1e12 / peak
-        roof["executed_work"] = "%d i8 digit plane(s) x 8*N ops per pair" % ex_planes
+        roof["executed_work"] = ("fp6 weights x fp4 codes, 8*N ops per pair" if fp6 else
+                                 "%d i8 digit plane(s) x 8*N ops per pair" % ex_planes)
         # against the i8 peak as well (the integer kernels' roofline)
         roof["frac_of_i8_peak"] = achieved / I8_MFMA_PEAK_TOPS
     else:
@@ -636,7 +644,7 @@ def main():
         cand_ops = n_cand * 4096 * 8.0 * N
         if screen_kind == 4:  # the per-pair kernel's algorithmic work: 8N per candidate pair
             cand_ops = float(np.mean(cpairs)) * 8.0 * N
-        roof["screen"] = {"kind": {3: "i8 two-plane", 4: "candidate pairs (i8 pass on the top two digit planes, rigorous bound)"}.get(screen_kind, "i8"),
+        roof["screen"] = {"kind": "fp6 x fp4" if fp6 else {3: "i8 two-plane", 4: "candidate pairs (i8 pass on the top two digit planes, rigorous bound)"}.get(screen_kind, "i8"),
                           "tiles": n_tiles,
                           "candidate_tiles": n_cand, "candidate_fraction": n_cand / max(n_tiles, 1),
                           "screen_ms": screen_ms, "candidate_launch_ms": cand_ms,
@@ -655,7 +663,7 @@ def main():
                           "unscreened_frac": alg_ops / (unscreened_ms * 1e-3) / 1e12 / roof["peak"]}
     # PMC traffic (profiles/traffic.json) was measured on the default C4 line's
     # dominant kernel (the one-plane i8 screen); other lines report null
-    tr = load_traffic(args.config + ("-unweighted" if args.unweighted else ""), kern_name)
+    tr = load_traffic(args.config + ("-unweighted" if args.unweighted else ""), "fp6" if fp6 else kern_name)
     same_kernel = (screen_kind == 1 and args.thr is None and not args.wide_weights
                    and not (args.rehearse_dist and args.rehearse_shard > 1))
     roof["traffic"] = tr.get("hbm_bytes_per_launch") if tr and same_kernel else None
@@ -666,6 +674,13 @@ def main():
         dtype = ("i8 MFMA on the top %d digit plane(s) of %s (i32 sums), rigorous r2 bound with lib.rs's rounding; "
                  "the %.0f candidate pairs: f32 sums in lib.rs's order, f32 epilogue" % (
                      min(planes, 2), fixed, float(np.mean(cpairs))))
+    elif kern_name == "mfma" and fp6:
+        dtype = ("fp6 (e2m3) weights x fp4 (e2m1) codes on block-scaled MFMA, screen (f32 sums, exact on the rounded "
+                 "weights; rigorous f32 r2 bound over every pair); candidate tiles (%.0f of %d): %s" % (
+                     float(np.mean(cand)), n_tiles,
+                     "f32 sums in lib.rs's order on f32 MFMA, f32 epilogue" if args.ref_sums else
+                     "%d i8 digit plane%s of %s, exact i32 sums, f32 epilogue" % (planes, "s" if planes > 1 else "",
+                                                                                  fixed)))
     elif kern_name == "mfma" and screened:
         dtype = ("i8 MFMA screen on the top weight digit%s (i32 sums, rigorous f32/f64 r2 bound over every pair); "
                  "candidate tiles (%.0f of %d): %s" % (

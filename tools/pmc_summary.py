@@ -9,7 +9,7 @@ import sys
 for f in sorted(glob.glob(sys.argv[1] + "/**/*_counter_collection.csv", recursive=True)):
   by_kernel = collections.defaultdict(lambda: (collections.defaultdict(list), {}))
   for r in csv.DictReader(open(f)):
-    if not any(k in r["Kernel_Name"] for k in ("pair_mfma", "pair_valu")):
+    if not any(k in r["Kernel_Name"] for k in ("pair_mfma", "pair_valu", "pair_fp6", "ref_item")):
         continue
     agg, dur = by_kernel[r["Kernel_Name"].split("(")[0]]
     agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
