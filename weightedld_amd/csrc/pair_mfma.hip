@@ -881,81 +881,111 @@ struct AccF6 {
     }
 };
 
-__global__ __launch_bounds__(256, 4) void pair_fp6_screen_kernel(const uint8_t *__restrict__ a6,
+// TPW tiles per workgroup (workgroup b: list entries 8 (TPW (b >> 3) + j) +
+// (b & 7), consecutive entries of its XCD's queue in the XCD-ordered list):
+// the next tile's first stage is issued during this tile's last stage, so its
+// DMA lands while this tile's epilogue runs (1: one tile per workgroup).
+#ifndef WLD_FP6_TPW
+#define WLD_FP6_TPW 1
+#endif
+#ifndef WLD_FP6_WG
+#define WLD_FP6_WG 4  // workgroups per CU
+#endif
+__global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const uint8_t *__restrict__ a6,
                                                                   const uint8_t *__restrict__ b4,
                                                                   const uint64_t *__restrict__ ok_bits,
-                                                                  const uint32_t *__restrict__ tiles, uint32_t NK,
-                                                                  uint32_t L, uint32_t n_chunk_rows, float thr,
-                                                                  OrderArgs o, ScreenArgs sc) {
+                                                                  const uint32_t *__restrict__ tiles, uint32_t n_tiles,
+                                                                  uint32_t NK, uint32_t L, uint32_t n_chunk_rows,
+                                                                  float thr, OrderArgs o, ScreenArgs sc) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6Stage];
     __shared__ unsigned long long sBits[kTile];
     __shared__ uint32_t sRowBase[kTile];
     if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
-    const uint32_t tile = tiles[blockIdx.x];
-    if (tile == kNoTile) return;  // padding of an XCD-ordered list (whole workgroup)
-    const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint8_t *srcA = a6 + (size_t)(4 * ta + wave) * NK * kF6ABytes;  // wave-uniform
-    const uint8_t *srcB = b4 + (size_t)(4 * tb + wave) * NK * kF6BBytes;
     const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
-    auto issue = [&](uint32_t kb, uint32_t buf) {
+    // the j-th tile of this workgroup (kNoTile: padding of an XCD-ordered list, or past the end)
+    auto tile_at = [&](uint32_t j) -> uint32_t {
+        const uint32_t i = 8 * (WLD_FP6_TPW * (blockIdx.x >> 3) + j) + (blockIdx.x & 7);
+        return i < n_tiles ? tiles[i] : kNoTile;
+    };
+    // this wave's DMA sources for a tile: A of row block 4 ta + wave, B of column block 4 tb + wave
+    auto src_a = [&](uint32_t tile) { return a6 + (size_t)(4 * (tile >> 16) + wave) * NK * kF6ABytes; };
+    auto src_b = [&](uint32_t tile) { return b4 + (size_t)(4 * (tile & 0xFFFFu) + wave) * NK * kF6BBytes; };
+    auto issue = [&](const uint8_t *sA, const uint8_t *sB, uint32_t kb, uint32_t buf) {
         const uint32_t gb = lds + buf * kF6Stage;
-        const uint8_t *a = srcA + (size_t)kb * kF6ABytes;
+        const uint8_t *a = sA + (size_t)kb * kF6ABytes;
         glds16_s(a, lane16, gb + wave * kF6ABytes);
         glds16_s(a + 1024, lane16, gb + wave * kF6ABytes + 1024);
         glds16_s(a + 2048, lane16, gb + wave * kF6ABytes + 2048);
-        glds16_s(srcB + (size_t)kb * kF6BBytes, lane16, gb + 4 * kF6ABytes + wave * kF6BBytes);
+        glds16_s(sB + (size_t)kb * kF6BBytes, lane16, gb + 4 * kF6ABytes + wave * kF6BBytes);
     };
-    issue(0, 0);
-    const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
-    AccF6 acc;
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int x = 0; x < 2; ++x)
-#pragma unroll
-            for (int y = 0; y < 2; ++y) acc.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+    uint32_t j = 0, tile = tile_at(0);
+    while (tile == kNoTile && ++j < WLD_FP6_TPW) tile = tile_at(j);
+    if (tile == kNoTile) return;  // (uniform: the whole workgroup)
+    const uint8_t *sA = src_a(tile), *sB = src_b(tile);
+    issue(sA, sB, 0, 0);
     uint32_t buf = 0;
-    for (uint32_t kb = 0; kb < NK; ++kb) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this stage landed
-        __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
-        asm volatile("" ::: "memory");
-        if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
-        const uint8_t *g = smem + buf * kF6Stage;
-        const uint8_t *pa = g + wave * kF6ABytes + lane * 24;
-        const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
-                    i2 = *reinterpret_cast<const uint2 *>(pa + 16);
-        const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536), m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
-                    m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
-        const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
-        const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
+    for (;;) {
+        // the next tile of this workgroup (its first stage is issued in this one's last)
+        uint32_t jn = j + 1, next = kNoTile;
+        while (jn < WLD_FP6_TPW && (next = tile_at(jn)) == kNoTile) ++jn;
+        const uint8_t *nA = next != kNoTile ? src_a(next) : sA, *nB = next != kNoTile ? src_b(next) : sB;
+        const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
+        const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
+        AccF6 acc;
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const uint4 r = *reinterpret_cast<const uint4 *>(g + 4 * kF6ABytes + n * kF6BBytes + lane * 16);
-            constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
-            const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
-            const v8i bmin = {(int)r.x & kMinor, (int)r.y & kMinor, (int)r.z & kMinor, (int)r.w & kMinor, 0, 0, 0, 0};
-            acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, braw, acc.v[n][0][0], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-            acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc.v[n][0][1], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-            acc.v[n][1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, braw, acc.v[n][1][0], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-            acc.v[n][1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, bmin, acc.v[n][1][1], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y) acc.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+        for (uint32_t kb = 0; kb < NK; ++kb) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this stage landed
+            __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
+            asm volatile("" ::: "memory");
+            if (kb + 1 < NK) issue(sA, sB, kb + 1, buf ^ 1);
+            else if (next != kNoTile) issue(nA, nB, 0, buf ^ 1);
+            const uint8_t *g = smem + buf * kF6Stage;
+            const uint8_t *pa = g + wave * kF6ABytes + lane * 24;
+            const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
+                        i2 = *reinterpret_cast<const uint2 *>(pa + 16);
+            const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536),
+                        m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
+                        m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
+            const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
+            const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const uint4 r = *reinterpret_cast<const uint4 *>(g + 4 * kF6ABytes + n * kF6BBytes + lane * 16);
+                constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
+                const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
+                const v8i bmin = {(int)r.x & kMinor, (int)r.y & kMinor, (int)r.z & kMinor, (int)r.w & kMinor,
+                                  0, 0, 0, 0};
+                acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, braw, acc.v[n][0][0], 2, 4, 0,
+                                                                                  0x7F7F7F7F, 0, 0x7F7F7F7F);
+                acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc.v[n][0][1], 2, 4, 0,
+                                                                                  0x7F7F7F7F, 0, 0x7F7F7F7F);
+                acc.v[n][1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, braw, acc.v[n][1][0], 2, 4, 0,
+                                                                                  0x7F7F7F7F, 0, 0x7F7F7F7F);
+                acc.v[n][1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, bmin, acc.v[n][1][1], 2, 4, 0,
+                                                                                  0x7F7F7F7F, 0, 0x7F7F7F7F);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
+            buf ^= 1;
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
-        buf ^= 1;
+        // (the f64 fallback of pair_cand: exact sums from X, Y; the launch uses
+        // the f32 test, sc.f32 == 2)
+        auto sum = [&](int x, int y, int i) -> double {
+            const float2 p = acc.raw(x, i);
+            return ((double)p.x + (y ? -(double)p.y : (double)p.y)) * 0.5;
+        };
+        const DenseArgs dn{nullptr, nullptr, nullptr, nullptr};
+        tile_epilogue<kModeScreen, AccF6>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, 0, o, dn, sc, sBits,
+                                          sRowBase);
+        if (next == kNoTile) break;
+        __syncthreads();  // (the epilogue's LDS state is reused by the next tile's)
+        tile = next, sA = nA, sB = nB, j = jn;
     }
-    // (the f64 fallback of pair_cand: exact sums from X, Y; the launch uses
-    // the f32 test, sc.f32 == 2)
-    auto sum = [&](int x, int y, int i) -> double {
-        const float2 p = acc.raw(x, i);
-        return ((double)p.x + (y ? -(double)p.y : (double)p.y)) * 0.5;
-    };
-    const DenseArgs dn{nullptr, nullptr, nullptr, nullptr};
-    tile_epilogue<kModeScreen, AccF6>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, 0, o, dn, sc, sBits,
-                                      sRowBase);
 }
 
 void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b4,
@@ -1194,8 +1224,11 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
         if ((double)sc.Rf < sc.R) sc.Rf = nextafterf(sc.Rf, INFINITY);
         sc.f32 = 2;
         screen_consts(m.fp6->Tg, 2.0f * sc.Rf, sc.E, sc.mloc);
-        hipLaunchKernelGGL(pair_fp6_screen_kernel, dim3(m.n_tiles), dim3(256), 0, s, m.fp6->a6, m.fp6->b4, ok_bits,
-                           m.tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
+        // WLD_FP6_TPW tiles per workgroup; the grid a multiple of 8 (each
+        // workgroup's tiles on its XCD's queue of the XCD-ordered list)
+        const uint32_t grid = (m.n_tiles + 8 * WLD_FP6_TPW - 1) / (8 * WLD_FP6_TPW) * 8;
+        hipLaunchKernelGGL(pair_fp6_screen_kernel, dim3(grid), dim3(256), 0, s, m.fp6->a6, m.fp6->b4, ok_bits,
+                           m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
         if (screen_done) (void)hipEventRecord(screen_done, s);
         launch_candidates(m, n, idx, ok_bits, o, dn, sc, s);
         return true;
