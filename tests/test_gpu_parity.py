@@ -393,6 +393,46 @@ def test_staging_overflow_regrows(W, ctxs, kern):
 
 
 @pytest.mark.parametrize("kern", KERNELS)
+def test_gather_behind_scan_sequences(W, ctxs, kern):
+    """After a run with rows the gather is enqueued behind the scan before the
+    host sees the row count (capi.hip enqueue_pass, WLD_SPEC_GATHER), with
+    outputs for 1.25x the last run's rows.  Every case of that guess: more rows
+    (gathered again into larger outputs), a staging overflow (the pass re-runs,
+    the gather with it), no rows, fewer rows, a shard, a site map — each run's
+    rows equal the oracle's."""
+    _ctx(ctxs, kern)
+    ctx = new_ctx(W, kern)
+    ctx.set_option("staging_rows", 100)
+    L, N = 700, 150
+    buf = synth(L, N, 6)
+    w = np.random.default_rng(3).random(N).astype(np.float32)
+    ctx.load(buf, w)
+    seq = [(0.5, None), (0.2, None), (0.0, None), (0.0, None), (1.01, None), (0.3, None), (0.0, (3, 1)), (0.1, None)]
+    for thr, shard in seq:
+        if shard:  # (n_shards, shard): the shard's rows are the full run's with a in its chunk rows
+            b, e = ctx.shard_chunk_rows(L, *shard)
+            n = ctx.run(thr, b, e)
+            full = O.all_pairs(buf, w, np.float32(thr))
+            sel = (full["site_a"] // 256 >= b) & (full["site_a"] // 256 < e)
+            ref = {k: np.asarray(full[k])[sel] for k in ("site_a", "site_b", "d", "d_prime", "r2")}
+            assert n == int(sel.sum()) > 0
+            compare_rows(ctx.rows(), ref, thr, buf=buf, w=w)
+            continue
+        n = ctx.run(thr)
+        ref = O.all_pairs(buf, w, np.float32(thr))
+        assert n == len(ref["site_a"]), (thr, n)
+        compare_rows(ctx.rows(), ref, thr, buf=buf, w=w)
+    keep = np.arange(L, dtype=np.uint64) * 3 + 7
+    ctx.load(buf, w, keep)
+    for thr in (0.2, 0.2, 0.0):
+        n = ctx.run(thr)
+        ref = O.all_pairs(buf, w, np.float32(thr), site_map=keep)
+        assert n == len(ref["site_a"])
+        compare_rows(ctx.rows(), ref, thr, buf=buf, w=w, site_map=keep)
+    ctx.close()
+
+
+@pytest.mark.parametrize("kern", KERNELS)
 @pytest.mark.parametrize("G", [2, 3, 4])
 def test_sharded_runs_concatenate_to_reference_order(ctxs, kern, G):
     ctx = _ctx(ctxs, kern)

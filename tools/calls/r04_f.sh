@@ -1,12 +1,15 @@
 #!/bin/bash
 # round-4 GPU call F: fp6 screen with optional several tiles per workgroup
-# (WLD_FP6_TPW) and 3 vs 4 waves (WLD_FP6_WG): fp6 tests on the default build,
-# C4 A/B of the variants, bench lines
+# (WLD_FP6_TPW) and 3 vs 4 waves (WLD_FP6_WG); the gather enqueued behind the
+# scan (WLD_SPEC_GATHER): tests, C4 and C2 A/B, bench lines
 out=gpurun_out/r04f; mkdir -p $out; export TMPDIR=/tmp
-tools/gpu_step.sh 600 $out/fp6_tests.txt python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu \
-  tests/test_gpu_fp6.py || exit $?
+tools/gpu_step.sh 600 $out/tests.txt python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu \
+  tests/test_gpu_fp6.py tests/test_gpu_parity.py -k "fp6 or gather_behind or staging or sharded or site_map" || exit $?
 tools/gpu_step.sh 400 $out/ab_c4.txt python tools/ab_builds.py --config c4 --reps 20 --rounds 3 \
   base=weightedld_amd/libweightedld.so tpw2=build/exp/tpw2/libweightedld.so tpw4=build/exp/tpw4/libweightedld.so \
   wg3=build/exp/wg3/libweightedld.so || exit $?
+tools/gpu_step.sh 300 $out/ab_c2.txt python tools/ab_builds.py --config c2 --reps 30 --rounds 3 \
+  spec=weightedld_amd/libweightedld.so nospec=build/exp/nospec/libweightedld.so || exit $?
 tools/gpu_step.sh 300 $out/bench_c4.log python bench.py --no-cpu-baseline || exit $?
+tools/gpu_step.sh 200 $out/bench_c2.log python bench.py --config c2 --no-cpu-baseline || exit $?
 echo done

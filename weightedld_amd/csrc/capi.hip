@@ -165,6 +165,12 @@ struct wld_ctx {
     bool screened = false;  // the last pass ran a screen
     bool screened2 = false; // ... on two digit planes
     uint64_t rows = 0;
+    // the gather goes into the stream behind the scan, before the host has
+    // seen the row count, when the previous run had rows (WLD_SPEC_GATHER):
+    // no host round trip between scan and gather; gather_cap: the output
+    // rows the enqueued gather may write (0: none enqueued)
+    bool spec_gather = false;
+    uint64_t gather_cap = 0;
     wld_run_stats stats{};
     // per-chunk progress (wld_run_host with a callback): the run's chunk
     // countdowns and log slot counter on the device, the log in mapped pinned
@@ -1052,6 +1058,16 @@ int wld_shard_chunks(size_t n_sites, int n_shards, int shard, uint32_t *begin, u
 }
 
 namespace {
+int ensure_outputs(wld_ctx *c, uint64_t rows) {
+    rows = std::max<uint64_t>(rows, 1);
+    WLD_TRY(ensure(c->out_a, rows * 4));
+    WLD_TRY(ensure(c->out_b, rows * 4));
+    WLD_TRY(ensure(c->out_d, rows * 4));
+    WLD_TRY(ensure(c->out_dp, rows * 4));
+    WLD_TRY(ensure(c->out_r2, rows * 4));
+    return WLD_OK;
+}
+
 int grow_staging(wld_ctx *c, uint64_t cap) {
     cap = std::max<uint64_t>(cap, 1);
     if (c->st_capacity >= cap) return WLD_OK;
@@ -1093,7 +1109,7 @@ int enqueue_pass(wld_ctx *c) {
     unsigned long long *cur = cn + kCandSet0 + kCandSetWords * c->cand_set;
     unsigned long long *nxt = cn + kCandSet0 + kCandSetWords * (c->cand_set ^ 1);
     ScanArgs sa{ptr<uint32_t>(c->chunk_total), r.lin_begin, lin_count, ptr<uint32_t>(c->chunk_base), cn + 1, cn,
-                c->d_hcnt, r.count_out, reinterpret_cast<unsigned *>(cur), reinterpret_cast<unsigned *>(nxt),
+                c->d_hcnt, r.count_out, cn + kCursorSeen, reinterpret_cast<unsigned *>(cur), reinterpret_cast<unsigned *>(nxt),
                 reinterpret_cast<unsigned *>(nxt + 1), reinterpret_cast<unsigned *>(cn + 2)};
     c->h_cnt[0] = c->h_cnt[1] = lin_count ? ~0ull : 0ull;
     c->h_cnt[2] = c->h_cnt[3] = 0;
@@ -1115,6 +1131,20 @@ int enqueue_pass(wld_ctx *c) {
         HIP_TRY(hipMemsetAsync(r.count_out, 0, sizeof(unsigned long long), c->stream));
     }
     HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+    c->gather_cap = 0;
+    if (WLD_SPEC_GATHER && c->spec_gather && lin_count) {
+        // outputs for a quarter more rows than the last run's (the scan's
+        // count decides; more than that and run_complete gathers again)
+        const uint64_t cap = std::min<uint64_t>(c->st_capacity, c->rows + c->rows / 4 + 4096);
+        WLD_TRY(ensure_outputs(c, cap));
+        launch_gather(o, ptr<uint32_t>(c->chunk_base), r.lin_begin, lin_count, chunk_rows_of(c->L), (uint32_t)c->L, 0,
+                      cn, c->out_a.bytes / 4, c->has_map ? ptr<uint32_t>(c->site_map) : nullptr,
+                      ptr<uint32_t>(c->out_a), ptr<uint32_t>(c->out_b), ptr<float>(c->out_d), ptr<float>(c->out_dp),
+                      ptr<float>(c->out_r2), c->stream);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->ev[5], c->stream));
+        c->gather_cap = c->out_a.bytes / 4;
+    }
     return WLD_OK;
 }
 
@@ -1242,8 +1272,8 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
         }
         // the pass's end, not the stream's: on a shared stream (wld_set_stream)
         // the next context's run may already be queued behind it
-        HIP_TRY(hipEventSynchronize(c->ev[4]));
-        WLD_TRY(check_guard(c, "pair phase"));
+        HIP_TRY(hipEventSynchronize(c->ev[c->gather_cap ? 5 : 4]));
+        WLD_TRY(check_guard(c, c->gather_cap ? "pair phase or reference-order gather" : "pair phase"));
         c->run_dirty = false;  // the pass completed: its scan cleaned the run state
         h[0] = __atomic_load_n(&c->h_cnt[0], __ATOMIC_ACQUIRE);
         h[1] = __atomic_load_n(&c->h_cnt[1], __ATOMIC_ACQUIRE);
@@ -1259,15 +1289,11 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     // chunk totals the rows kept)
     if (c->ref_pairs_pass ? h[0] < h[1] : h[0] != h[1])
         return fail(WLD_E_HIP, "internal: staging cursor %llu vs chunk total %llu", h[0], h[1]);
-    WLD_TRY(ensure(c->out_a, std::max<uint64_t>(rows, 1) * 4));
-    WLD_TRY(ensure(c->out_b, std::max<uint64_t>(rows, 1) * 4));
-    WLD_TRY(ensure(c->out_d, std::max<uint64_t>(rows, 1) * 4));
-    WLD_TRY(ensure(c->out_dp, std::max<uint64_t>(rows, 1) * 4));
-    WLD_TRY(ensure(c->out_r2, std::max<uint64_t>(rows, 1) * 4));
-    int order_end = 4;  // with no rows the order phase ends at the scan
-    if (rows && lin_count) {
+    int order_end = c->gather_cap ? 5 : 4;  // with no rows (and no gather enqueued) it ends at the scan
+    if (rows && lin_count && rows > c->gather_cap) {  // not gathered behind the scan
+        WLD_TRY(ensure_outputs(c, rows));
         launch_gather(order_args(c), ptr<uint32_t>(c->chunk_base), r.lin_begin, lin_count, n, (uint32_t)c->L, rows,
-                      c->has_map ? ptr<uint32_t>(c->site_map) : nullptr, ptr<uint32_t>(c->out_a),
+                      nullptr, rows, c->has_map ? ptr<uint32_t>(c->site_map) : nullptr, ptr<uint32_t>(c->out_a),
                       ptr<uint32_t>(c->out_b), ptr<float>(c->out_d), ptr<float>(c->out_dp), ptr<float>(c->out_r2),
                       c->stream);
         HIP_TRY(hipGetLastError());
@@ -1278,6 +1304,8 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     }
     c->rows = rows;
     c->have_rows = true;
+    c->spec_gather = rows > 0;
+    c->gather_cap = 0;
     c->stats.kernel = c->kernel;
     c->stats.pairs = r.pairs;
     c->stats.rows = rows;

@@ -78,6 +78,7 @@ struct ScanArgs {
     uint32_t lin_begin, count;
     uint32_t *chunk_base;
     unsigned long long *total, *cursor, *host_out, *count_out;
+    unsigned long long *cursor_seen;  // device word: the staging cursor before its reset (may be null)
     unsigned *cand_count;  // this pass's {candidate tiles, their candidate sub-blocks} (read)
     // the OTHER candidate set (the next pass's: {count, sub-blocks} and 16
     // bucket counts), zeroed here; this pass's set is never written by its
@@ -90,8 +91,9 @@ struct ScanArgs {
 
 // 64-bit words of a context's run counters (capi.hip enqueue_pass):
 // {cursor, total, {ticket, work}, set 0: {candidates, sub-blocks} + 16 bucket
-// counts (9 words), set 1: the same}
-constexpr uint32_t kCounterWords = 21;
+// counts (9 words), set 1: the same, the cursor the scan saw}
+constexpr uint32_t kCounterWords = 22;
+constexpr uint32_t kCursorSeen = 21;
 constexpr uint32_t kCandSetWords = 9;
 constexpr uint32_t kCandSet0 = 3;
 
@@ -199,6 +201,12 @@ constexpr uint32_t kRefItemGrid = 1024;
 #ifndef WLD_REF_ITEMS
 #define WLD_REF_ITEMS 1
 #endif
+// the reference-order gather enqueued behind the scan when the previous run
+// had rows (capi.hip enqueue_pass; 0: after the host has read the row count,
+// the round-3 order; A/B builds only)
+#ifndef WLD_SPEC_GATHER
+#define WLD_SPEC_GATHER 1
+#endif
 // ... and of ref_sums_kernel / ref_compact_kernel (low-register: eight per CU)
 constexpr uint32_t kRefRowsGrid = 2048;
 
@@ -269,10 +277,15 @@ void launch_progress_init(unsigned *chunk_left, uint32_t lin_begin, uint32_t cou
 void launch_run_init(unsigned long long *counters, uint32_t *chunk_total, uint32_t n_chunks, hipStream_t s);
 // the run's chunk scan as a launch of its own (ScanArgs; ticket unused)
 void launch_chunk_scan(const ScanArgs &a, hipStream_t s);
-// (rows: the run's row count, the bound of every destination)
+// (rows: the run's row count, the bound of every destination.  With state
+// (the run counters) set, the gather is enqueued before the host has seen the
+// scan: it reads the row total and the cursor the scan saw from the device and
+// writes nothing if the staging overflowed or the rows exceed out_cap — the
+// host then re-runs the pass or gathers again into larger buffers)
 void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,
-                   uint32_t n_chunk_rows, uint32_t L, uint64_t rows, const uint32_t *site_map, uint32_t *out_a,
-                   uint32_t *out_b, float *out_d, float *out_dp, float *out_r2, hipStream_t s);
+                   uint32_t n_chunk_rows, uint32_t L, uint64_t rows, const unsigned long long *state,
+                   uint64_t out_cap, const uint32_t *site_map, uint32_t *out_a, uint32_t *out_b, float *out_d,
+                   float *out_dp, float *out_r2, hipStream_t s);
 
 // Linear index of chunk (row, col) in the reference's triu_index order
 // (lib.rs:623-632): rows descend, so row r starts at (n-1-r)(n-r)/2.

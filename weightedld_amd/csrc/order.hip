@@ -55,6 +55,8 @@ constexpr uint32_t kGatherRows = 16;
 __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t *__restrict__ chunk_base,
                                                       uint32_t lin_begin, uint32_t count, uint32_t n_chunk_rows,
                                                       uint32_t L, uint64_t rows,
+                                                      const unsigned long long *__restrict__ state,
+                                                      uint64_t out_cap,
                                                       const uint32_t *__restrict__ site_map,
                                                       uint32_t *__restrict__ out_a, uint32_t *__restrict__ out_b,
                                                       float *__restrict__ out_d, float *__restrict__ out_dp,
@@ -63,6 +65,10 @@ __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t
     __shared__ uint32_t sOff[kGatherRows][kTilesPerChunk];
     __shared__ uint32_t sPre[kGatherRows][kTilesPerChunk];
     __shared__ uint32_t sWave[4];
+    if (state) {  // enqueued behind the scan, before the host has seen it
+        if (state[kCursorSeen] > o.st_capacity || state[1] > out_cap) return;  // (uniform) the host redoes it
+        rows = state[1];
+    }
     const uint32_t base = chunk_base[blockIdx.x];
     const uint64_t next = blockIdx.x + 1 < count ? chunk_base[blockIdx.x + 1] : rows;
     if (next == base) return;  // (uniform) no row in this chunk
@@ -167,11 +173,12 @@ void launch_chunk_scan(const ScanArgs &a, hipStream_t s) {
 }
 
 void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_begin, uint32_t count,
-                   uint32_t n_chunk_rows, uint32_t L, uint64_t rows, const uint32_t *site_map, uint32_t *out_a,
-                   uint32_t *out_b, float *out_d, float *out_dp, float *out_r2, hipStream_t s) {
+                   uint32_t n_chunk_rows, uint32_t L, uint64_t rows, const unsigned long long *state,
+                   uint64_t out_cap, const uint32_t *site_map, uint32_t *out_a, uint32_t *out_b, float *out_d,
+                   float *out_dp, float *out_r2, hipStream_t s) {
     if (!count) return;
     hipLaunchKernelGGL(gather_kernel, dim3(count, kChunk / kGatherRows), dim3(256), 0, s, o, chunk_base, lin_begin,
-                       count, n_chunk_rows, L, rows, site_map, out_a, out_b, out_d, out_dp, out_r2);
+                       count, n_chunk_rows, L, rows, state, out_cap, site_map, out_a, out_b, out_d, out_dp, out_r2);
 }
 
 }  // namespace wld

@@ -259,6 +259,7 @@ __device__ inline void chunk_scan_block(const ScanArgs &a) {
         if (a.count_out) *a.count_out = run;  // e.g. the caller's tensor for the RCCL count exchange
         const unsigned long long cur = __hip_atomic_load(a.cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *a.cursor = 0;
+        if (a.cursor_seen) *a.cursor_seen = cur;
         unsigned cand = 0, blocks = 0;
         if (a.cand_count) {
             cand = ld32(a.cand_count);
