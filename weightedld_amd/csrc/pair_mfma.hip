@@ -891,13 +891,20 @@ struct AccF6 {
 #ifndef WLD_FP6_WG
 #define WLD_FP6_WG 4  // workgroups per CU
 #endif
+// stage buffers: 2 (one stage in flight while one is read) or 3 (two in
+// flight, a counted vmcnt: LDS-DMA completes in issue order; three
+// workgroups per CU fit 3 x 16 KB each)
+#ifndef WLD_FP6_NBUF
+#define WLD_FP6_NBUF 2
+#endif
+static_assert(WLD_FP6_NBUF == 2 || (WLD_FP6_NBUF == 3 && WLD_FP6_TPW == 1), "fp6 stage ring");
 __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const uint8_t *__restrict__ a6,
                                                                   const uint8_t *__restrict__ b4,
                                                                   const uint64_t *__restrict__ ok_bits,
                                                                   const uint32_t *__restrict__ tiles, uint32_t n_tiles,
                                                                   uint32_t NK, uint32_t L, uint32_t n_chunk_rows,
                                                                   float thr, OrderArgs o, ScreenArgs sc) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6Stage];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[WLD_FP6_NBUF * kF6Stage];
     __shared__ unsigned long long sBits[kTile];
     __shared__ uint32_t sRowBase[kTile];
     if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
@@ -924,6 +931,7 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     if (tile == kNoTile) return;  // (uniform: the whole workgroup)
     const uint8_t *sA = src_a(tile), *sB = src_b(tile);
     issue(sA, sB, 0, 0);
+    if (WLD_FP6_NBUF == 3 && NK > 1) issue(sA, sB, 1, 1);
     uint32_t buf = 0;
     for (;;) {
         // the next tile of this workgroup (its first stage is issued in this one's last)
@@ -940,11 +948,19 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
 #pragma unroll
                 for (int y = 0; y < 2; ++y) acc.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
         for (uint32_t kb = 0; kb < NK; ++kb) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this stage landed
-            __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
+            // this wave's copies of this stage landed (with three buffers the
+            // next stage's four may still be in flight) ...
+            if (WLD_FP6_NBUF == 3 && kb + 1 < NK) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // ... and every other wave's; the buffer read last stage is free
             asm volatile("" ::: "memory");
-            if (kb + 1 < NK) issue(sA, sB, kb + 1, buf ^ 1);
-            else if (next != kNoTile) issue(nA, nB, 0, buf ^ 1);
+            if (WLD_FP6_NBUF == 3) {
+                if (kb + 2 < NK) issue(sA, sB, kb + 2, buf == 0 ? 2 : buf - 1);
+            } else if (kb + 1 < NK) {
+                issue(sA, sB, kb + 1, buf ^ 1);
+            } else if (next != kNoTile) {
+                issue(nA, nB, 0, buf ^ 1);
+            }
             const uint8_t *g = smem + buf * kF6Stage;
             const uint8_t *pa = g + wave * kF6ABytes + lane * 24;
             const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
@@ -971,7 +987,7 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
                                                                                   0x7F7F7F7F, 0, 0x7F7F7F7F);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
-            buf ^= 1;
+            buf = buf + 1 == WLD_FP6_NBUF ? 0 : buf + 1;
         }
         // (the f64 fallback of pair_cand: exact sums from X, Y; the launch uses
         // the f32 test, sc.f32 == 2)
