@@ -416,7 +416,9 @@ typedef struct {
                                   could not reject (16 x candidate_tiles unless screened); with
                                   WLD_OPT_REF_SUMS only these are computed */
     uint64_t candidate_pairs; /* screened == 4: the pairs summed one by one in lib.rs's order */
-    int screen_fp6;          /* screened == 1 on fp6 x fp4 block-scaled MFMA (WLD_OPT_SCREEN_FP6), not i8 */
+    int screen_fp6;          /* screened == 1 on fp6 x fp4 block-scaled MFMA (WLD_OPT_SCREEN_FP6), not i8;
+                                2: the fp6 screen gave the pass up (more than a sixteenth of the tiles were
+                                candidates) and it re-ran on the i8 screen */
 } wld_run_stats;
 int wld_last_stats(wld_ctx *ctx, wld_run_stats *out);
 

@@ -106,10 +106,11 @@ def test_fp6_exact_mode_rows(W):
 
 
 def test_fp6_handover_to_i8(W):
-    """Auto policy: at a threshold where the fp6 screen leaves more than a
-    quarter of the tiles as candidates, the next pass (and any at a lower
-    threshold) screens on i8; higher thresholds stay on fp6.  Rows equal the
-    oracle's throughout."""
+    """Auto policy: at a threshold where the fp6 screen reaches a sixteenth of
+    the tiles as candidates it gives the pass up and the pass re-runs on the i8
+    screen (screen_fp6 2); that threshold and any lower one screen on i8 from
+    then on; higher thresholds stay on fp6.  Rows equal the oracle's
+    throughout."""
     import bench
     buf = bench.synth(2048, 2000)
     w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
@@ -121,8 +122,54 @@ def test_fp6_handover_to_i8(W):
         st = c.stats()
         seen.append((thr, st["screened"], st["screen_fp6"], st["candidate_tiles"], st["tiles"]))
         _bits_equal(c.rows(), O.all_pairs(buf, w, np.float32(thr)))
-    assert seen[0][1] == 1 and seen[0][2] == 1 and seen[0][3] * 4 > seen[0][4], seen
+    assert seen[0][2] == 2, seen
     assert seen[1][2] == 0 and seen[2][2] == 0 and seen[3][1:3] == (1, 1), seen
+    c.close()
+
+
+def test_fp6_abandoned_pass_on_ld_blocks(W):
+    """Linkage blocks: nearly every tile holds a pair the fp6 bound (1.4%
+    residual on these weights) cannot reject.  Auto: the first pass gives up
+    after a sixteenth of the tiles and re-runs on i8 inside the same call;
+    rows equal the oracle's.  With per-chunk progress, or a caller's count
+    word (the N>1 step's collective reads it), the pass is never given up:
+    the fp6 screen completes, its candidates are computed, and the next pass
+    hands over by the candidate count."""
+    import bench
+    import torch
+    L, N, thr = 4096, 2000, 0.05
+    buf = bench.ld_blocks(L, N, seed=7)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ref = O.all_pairs(buf, w, np.float32(thr))
+    assert len(ref["site_a"]) > 1000
+    c = W.Context(0)
+    c.load(buf, w)
+    c.run(thr)
+    st = c.stats()
+    assert st["screen_fp6"] == 2 and st["screened"] in (1, 3, 4), st
+    _bits_equal(c.rows(), ref)
+    c.run(thr)
+    assert c.stats()["screen_fp6"] == 0
+    _bits_equal(c.rows(), ref)
+    # progress: no give-up
+    c.load(buf, w)
+    calls = []
+    store = c.run_host(thr, calls.append)
+    st = c.stats()
+    assert st["screen_fp6"] == 1 and st["candidate_tiles"] * 16 > st["tiles"], st
+    assert calls and calls[0] == 0
+    _bits_equal(store, ref)
+    c.run(thr)
+    assert c.stats()["screen_fp6"] == 0
+    # a caller's count word: no give-up either
+    c.load(buf, w)
+    cnt = torch.full((1,), -1, dtype=torch.int64, device="cuda:0")
+    c.run_chunks_async(thr, 0, 0, cnt.data_ptr())
+    n = c.run_wait()
+    torch.cuda.synchronize()
+    assert n == int(cnt.item()) == len(ref["site_a"])
+    assert c.stats()["screen_fp6"] == 1
+    _bits_equal(c.rows(), ref)
     c.close()
 
 

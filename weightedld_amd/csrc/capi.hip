@@ -114,7 +114,7 @@ struct wld_ctx {
     // and at which the two-plane screen left > a fifth
     float screen_bad_thr = -1.0f;
     // auto: the largest threshold at which the fp6 screen left more than a
-    // quarter of the tiles (there and below, the i8 screen's tighter bound)
+    // sixteenth of the tiles (there and below, the i8 screen's tighter bound)
     float fp6_bad_thr = -1.0f;
     float screen2_bad_thr = -1.0f;
     // auto, lib.rs's order: the largest threshold at which the exact candidate
@@ -675,6 +675,13 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         // the one-plane screen on fp6 x fp4 MFMA where the load allows it
         m.fp6 = c->fp6_ok && (c->opt_fp6 == 2 || (c->opt_fp6 == 1 && c->fp6_better && thr > c->fp6_bad_thr))
                     ? &c->f6 : nullptr;
+        // auto: past a sixteenth of the tiles as candidates the fp6 screen
+        // gives the pass up and run_complete re-runs it on the i8 screen (not
+        // with per-chunk progress, which a re-run does not report again, nor
+        // with a caller's count word, which a collective may read before the
+        // re-run rewrites it)
+        m.fp6_bail = c->opt_fp6 == 1 && !c->prog_pass && !c->pend.count_out ? std::max<uint32_t>(c->n_tiles / 16, 1)
+                                                                                : 0;
         for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
         m.cand_list = ptr<uint32_t>(c->cand);
         // this pass's candidate set (the scan zeroes the other one, enqueue_pass)
@@ -1265,7 +1272,8 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     const uint32_t n = chunk_rows_of(c->L);
     const uint32_t lin_count = r.lin_end - r.lin_begin;
     unsigned long long h[4] = {0, 0, 0, 0};
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    bool regrown = false, abandoned = false;
+    for (;;) {
         if (c->prog_pass) {
             c->prog_pass = false;  // a re-run after a staging overflow does not report again
             WLD_TRY(drain_progress(c, r.lin_begin, lin_count));
@@ -1279,8 +1287,18 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
         h[1] = __atomic_load_n(&c->h_cnt[1], __ATOMIC_ACQUIRE);
         h[2] = __atomic_load_n(&c->h_cnt[2], __ATOMIC_ACQUIRE);
         h[3] = __atomic_load_n(&c->h_cnt[3], __ATOMIC_ACQUIRE);
+        if (h[2] & kAbandonBit) {
+            // the fp6 screen gave the pass up: this threshold (and any lower
+            // one) screens on i8 from now on, this pass included
+            if (abandoned) return fail(WLD_E_HIP, "internal: a re-run pass was abandoned again");
+            abandoned = true;
+            c->fp6_bad_thr = std::max(c->fp6_bad_thr, r.thr);
+            WLD_TRY(enqueue_pass(c));
+            continue;
+        }
         if (h[0] <= c->st_capacity) break;
-        if (attempt == 1) return fail(WLD_E_HIP, "internal: staging overflow after resize");
+        if (regrown) return fail(WLD_E_HIP, "internal: staging overflow after resize");
+        regrown = true;
         WLD_TRY(grow_staging(c, h[0]));
         WLD_TRY(enqueue_pass(c));
     }
@@ -1315,7 +1333,7 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     c->stats.pair_kernel_launches = c->n_tiles ? (c->ref_pairs_pass ? 3 : c->screened ? 2 : 1) : 0;
     c->stats.tiles = c->n_tiles;
     c->stats.screened = c->ref_pairs_pass ? 4 : c->screened ? (c->screened2 ? 3 : 1) : 0;
-    c->stats.screen_fp6 = c->fp6_pass ? 1 : 0;
+    c->stats.screen_fp6 = c->fp6_pass ? 1 : abandoned ? 2 : 0;
     c->stats.candidate_pairs = c->ref_pairs_pass ? h[0] : 0;
     // auto: a threshold at which even the i8 screen leaves more than half the
     // tiles is not screened from now on (nor any lower one): the screen costs a
@@ -1329,8 +1347,9 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     // goes to the full kernel (the exact mode; lib.rs's order takes the two-
     // plane screen only when asked, WLD_OPT_SCREEN 3)
     // ... the fp6 screen first hands over to the i8 one (a tighter bound at
-    // twice the cost) once it leaves more than a quarter of the tiles
-    if (c->fp6_pass && h[2] * 4 > c->n_tiles) {
+    // twice the cost) once it leaves more than a sixteenth of the tiles (or,
+    // in auto, gives the pass up on reaching that many: the loop above)
+    if (c->fp6_pass && h[2] * 16 > c->n_tiles) {
         c->fp6_bad_thr = std::max(c->fp6_bad_thr, r.thr);
     } else if (c->screened && !c->ref_pairs_pass && !c->screened2 && h[2] * 2 > c->n_tiles) {
         c->screen_bad_thr = std::max(c->screen_bad_thr, r.thr);

@@ -94,6 +94,12 @@ struct ScanArgs {
 // counts (9 words), set 1: the same, the cursor the scan saw}
 constexpr uint32_t kCounterWords = 22;
 constexpr uint32_t kCursorSeen = 21;
+// set on a pass's candidate count and on its bucket 0 by a screen that gave
+// up (the fp6 screen past ScreenArgs::bail candidates): the candidate launch
+// then computes nothing, the scan reports the count with the bit to the host
+// (which re-runs the pass on the i8 screen) and a cursor the gather enqueued
+// behind it refuses
+constexpr unsigned kAbandonBit = 0x80000000u;
 constexpr uint32_t kCandSetWords = 9;
 constexpr uint32_t kCandSet0 = 3;
 
@@ -261,6 +267,8 @@ struct MfmaLaunch {
     ScanArgs scan;
     // the one-plane screen on fp6 x fp4 MFMA instead of i8 (null: the i8 screen)
     const Fp6Screen *fp6;
+    // ... gives up past this many candidate tiles (0: never; kAbandonBit)
+    uint32_t fp6_bail;
 };
 // Enqueues the MFMA pair kernel(s) of one pass; returns true when a screen
 // (one- or two-plane) ran (then screen_done, if given, is recorded between

@@ -259,12 +259,13 @@ __device__ inline void chunk_scan_block(const ScanArgs &a) {
         if (a.count_out) *a.count_out = run;  // e.g. the caller's tensor for the RCCL count exchange
         const unsigned long long cur = __hip_atomic_load(a.cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *a.cursor = 0;
-        if (a.cursor_seen) *a.cursor_seen = cur;
         unsigned cand = 0, blocks = 0;
         if (a.cand_count) {
             cand = ld32(a.cand_count);
             blocks = ld32(a.cand_count + 1);
         }
+        // (an abandoned pass's rows are not gathered: the host re-runs it)
+        if (a.cursor_seen) *a.cursor_seen = (cand & kAbandonBit) ? ~0ull : cur;
         // the next pass's candidate set starts at 0 (nothing in this launch
         // reads or writes it)
         if (a.cand_reset) a.cand_reset[0] = a.cand_reset[1] = 0;
@@ -304,12 +305,14 @@ __device__ inline void chunk_scan_block(const ScanArgs &a) {
 // light tail goes to whichever finish first); entry (b, k) at b cap + k of the
 // tile and bit arrays.  The launch maps its u-th tile through the buckets'
 // prefix sums, which cand_prefix puts in s_pre[17] (every thread calls it).
+// An abandoned screen (kAbandonBit on bucket 0) leaves no candidate.
 __device__ inline void cand_prefix(const unsigned *buckets, uint32_t *s_pre) {
     if (threadIdx.x == 0) {
+        const bool abandoned = buckets[0] & kAbandonBit;
         uint32_t run = 0;
         for (int b = 0; b < 16; ++b) {
             s_pre[b] = run;
-            run += buckets[b];
+            run += abandoned ? 0u : buckets[b];
         }
         s_pre[16] = run;
     }

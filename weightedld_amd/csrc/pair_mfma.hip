@@ -397,6 +397,10 @@ struct ScreenArgs {
     // without a candidate get their zero counts here
     int rb_items;
     ScanArgs scan;          // screen and candidate launches: the fused chunk scan (scan_tail)
+    // the fp6 screen: a workgroup that finds more than bail candidate tiles
+    // listed gives the pass up (kAbandonBit) instead of computing its tile
+    // (0: never)
+    uint32_t bail;
 };
 
 // Reference epilogue of one pair from its exact sums (fixed-point units):
@@ -780,7 +784,7 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
     } else {
         // the first tile by workgroup id, the next ones from the work counter
         __shared__ uint32_t s_next, s_pre[17];
-        const uint32_t nt = *tile_count;
+        const uint32_t nt = (*tile_count & kAbandonBit) ? 0u : *tile_count;
         if (blockIdx.x < nt) cand_prefix(sc.cand_buckets, s_pre);  // (a workgroup without a tile skips it)
         for (uint32_t bi = blockIdx.x; bi < nt;) {
             // the thread id laundered per tile: nothing lane-derived is hoisted
@@ -907,9 +911,16 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     __shared__ __attribute__((aligned(16))) uint8_t smem[WLD_FP6_NBUF * kF6Stage];
     __shared__ unsigned long long sBits[kTile];
     __shared__ uint32_t sRowBase[kTile];
+    __shared__ uint32_t sBail;
     if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
+    // read by thread 0 while the tile's first stage is in flight, published by
+    // the first stage barrier: one decision for the whole workgroup
+    auto bail_check = [&] {
+        if (tid == 0)
+            sBail = sc.bail && __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > sc.bail;
+    };
     // the j-th tile of this workgroup (kNoTile: padding of an XCD-ordered list, or past the end)
     auto tile_at = [&](uint32_t j) -> uint32_t {
         const uint32_t i = 8 * (WLD_FP6_TPW * (blockIdx.x >> 3) + j) + (blockIdx.x & 7);
@@ -932,6 +943,7 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     const uint8_t *sA = src_a(tile), *sB = src_b(tile);
     issue(sA, sB, 0, 0);
     if (WLD_FP6_NBUF == 3 && NK > 1) issue(sA, sB, 1, 1);
+    bail_check();
     uint32_t buf = 0;
     for (;;) {
         // the next tile of this workgroup (its first stage is issued in this one's last)
@@ -954,6 +966,14 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();  // ... and every other wave's; the buffer read last stage is free
             asm volatile("" ::: "memory");
+            if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
+                if (tid == 0) {
+                    atomicOr(sc.cand_count, kAbandonBit);
+                    atomicOr(sc.cand_buckets, kAbandonBit);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                return;
+            }
             if (WLD_FP6_NBUF == 3) {
                 if (kb + 2 < NK) issue(sA, sB, kb + 2, buf == 0 ? 2 : buf - 1);
             } else if (kb + 1 < NK) {
@@ -1001,6 +1021,7 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
         if (next == kNoTile) break;
         __syncthreads();  // (the epilogue's LDS state is reused by the next tile's)
         tile = next, sA = nA, sB = nB, j = jn;
+        bail_check();
     }
 }
 
@@ -1239,6 +1260,7 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
         sc.Rf = (float)sc.R;
         if ((double)sc.Rf < sc.R) sc.Rf = nextafterf(sc.Rf, INFINITY);
         sc.f32 = 2;
+        sc.bail = m.fp6_bail;
         screen_consts(m.fp6->Tg, 2.0f * sc.Rf, sc.E, sc.mloc);
         // WLD_FP6_TPW tiles per workgroup; the grid a multiple of 8 (each
         // workgroup's tiles on its XCD's queue of the XCD-ordered list)

@@ -514,7 +514,7 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_
         // as many as the buckets count; each owns its row block's segments
         __shared__ uint32_t s_next, s_pre[17];
         if constexpr (NS == 1) cand_prefix(tile_buckets, s_pre);
-        const uint32_t nt = NS == 1 ? s_pre[16] : *tile_count;
+        const uint32_t nt = NS == 1 ? s_pre[16] : (*tile_count & kAbandonBit) ? 0u : *tile_count;
 #ifndef WLD_CAND_MIX
 #define WLD_CAND_MIX 1
 #endif
