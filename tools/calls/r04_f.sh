@@ -12,4 +12,5 @@ tools/gpu_step.sh 300 $out/ab_c2.txt python tools/ab_builds.py --config c2 --rep
   spec=weightedld_amd/libweightedld.so nospec=build/exp/nospec/libweightedld.so || exit $?
 tools/gpu_step.sh 300 $out/bench_c4.log python bench.py --no-cpu-baseline || exit $?
 tools/gpu_step.sh 200 $out/bench_c2.log python bench.py --config c2 --no-cpu-baseline || exit $?
+tools/gpu_step.sh 200 $out/bench_ldb.log python bench.py --data ldblocks --no-cpu-baseline || exit $?
 echo done
