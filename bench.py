@@ -630,7 +630,10 @@ def main():
         roof = {"bound": "mfma", "achieved": achieved, "peak": F32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / F32_VALU_PEAK_TFLOPS, "path": "f32 MFMA 16x16x4",
                 "work": "algorithmic: 8*N f32 flops per site pair",
-                "kernel": "pair_valu_kernel<%s>" % ("lib.rs order" if args.ref_sums else "two-level sums"),
+                # (lib.rs's order on up to 4 x 768 tiles: 16-row items, one
+                # sub-block per wave, capi.hip / pair_valu.hip ref_item_kernel)
+                "kernel": ("ref_item_kernel<lib.rs order, 16-row items>" if args.ref_sums and n_tiles <= 4 * 768
+                           else "pair_valu_kernel<%s>" % ("lib.rs order" if args.ref_sums else "two-level sums")),
                 "kernel_ms": kernel_ms}
     roof["pair_phase_ms"] = kernel_ms
     roof["pair_phase_frac"] = alg_ops / (kernel_ms * 1e-3) / 1e12 / roof["peak"]
@@ -649,7 +652,7 @@ def main():
                           "candidate_tiles": n_cand, "candidate_fraction": n_cand / max(n_tiles, 1),
                           "screen_ms": screen_ms, "candidate_launch_ms": cand_ms,
                           "candidate_kernel": ("ref_rows_kernel<lib.rs order, one pair per thread>" if screen_kind == 4
-                                               else "pair_valu_kernel<ref order, f32 MFMA>" if args.ref_sums else
+                                               else "ref_item_kernel<lib.rs order, f32 MFMA, 16-row items>" if args.ref_sums else
                                                "pair_mfma_kernel<prefilter, %d planes>" % planes),
                           "candidate_pairs": float(np.mean(cpairs)) if screen_kind == 4 else None,
                           "candidate_frac": (cand_ops / (cand_ms * 1e-3) / 1e12 / cand_peak) if cand_ms > 0.02 else None,
