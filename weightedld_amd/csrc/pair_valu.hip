@@ -640,6 +640,25 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                     cw[grp] = *reinterpret_cast<const float4 *>(wg + k0 + 16 * grp);
                 }
             };
+            // the scalar tail's codes and weights (positions 8 cls .. 8 cls + 7),
+            // all loaded at once after the last stage (one round trip, not one
+            // per position), into the stage prefetch registers: ca[e] / cb[e] =
+            // a row e's bytes 0-3 / 4-7, cw[0], cw[1] = the weights, cw[2].x /
+            // .y = the b row's bytes
+            auto fetch_tail = [&] {
+                const size_t p0 = 8 * (size_t)cls;
+                const uint2 b8 = *reinterpret_cast<const uint2 *>(rcodes + (size_t)(b0 + 16 * un + r) * NPr + p0);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint2 a8 =
+                        *reinterpret_cast<const uint2 *>(rcodes + (size_t)(a0 + 16 * ui + 4 * g + e) * NPr + p0);
+                    ca[e] = a8.x, cb[e] = a8.y;
+                }
+                cw[0] = *reinterpret_cast<const float4 *>(rw + p0);
+                cw[1] = *reinterpret_cast<const float4 *>(rw + p0 + 4);
+                cw[2].x = __uint_as_float(b8.x);
+                cw[2].y = __uint_as_float(b8.y);
+            };
             if (n_st) fetch(0);
             v4f acc[4];
             for (uint32_t st = 0; st < n_st; ++st) {
@@ -676,22 +695,32 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
 #pragma unroll
                         for (int q = 0; q < 4; ++q) tot[e][q] += acc[q][e];
             }
-            (void)cls;
             // the scalar tail (lib.rs:461-480), onto the horizontal sums in order
+            // (ref_tail_n <= 7, uniform)
+            // (one position per step: the byte queues shift down by 8 bits, the
+            // weights by one register)
+            if (ref_tail_n) fetch_tail();
+            float4 wlo = cw[0], whi = cw[1];
+            uint32_t qb0 = __float_as_uint(cw[2].x), qb1 = __float_as_uint(cw[2].y);
+#pragma unroll 1
             for (uint32_t t = 0; t < ref_tail_n; ++t) {
-                const uint32_t p = 8 * cls + t;
-                const float we = rw[p];
-                const uint32_t xb = rcodes[(size_t)(b0 + 16 * un + r) * NPr + p];
-                const float fi = (float)(xb & 1u), fm = (float)(xb >> 1);
+                const float we = wlo.x;
+                const float fi = (float)(qb0 & 1u), fm = (float)((qb0 >> 1) & 1u);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const uint32_t xa = rcodes[(size_t)(a0 + 16 * ui + 4 * g + e) * NPr + p];
+                    const uint32_t xa = ca[e];
                     const float u = (xa & kCodeIn) ? we : 0.0f, v = (xa & kCodeMaj) ? we : 0.0f;
                     tot[e][0] = __builtin_fmaf(u, fi, tot[e][0]);
                     tot[e][1] = __builtin_fmaf(v, fi, tot[e][1]);
                     tot[e][2] = __builtin_fmaf(u, fm, tot[e][2]);
                     tot[e][3] = __builtin_fmaf(v, fm, tot[e][3]);
+                    ca[e] = (ca[e] >> 8) | (cb[e] << 24);
+                    cb[e] >>= 8;
                 }
+                qb0 = (qb0 >> 8) | (qb1 << 24);
+                qb1 >>= 8;
+                wlo = make_float4(wlo.y, wlo.z, wlo.w, whi.x);
+                whi = make_float4(whi.y, whi.z, whi.w, 0.0f);
             }
         }
         // ---- epilogue (lib.rs:482-520, 660) --------------------------------
@@ -757,7 +786,10 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
 
     if constexpr (!LOOP) {
         const uint32_t tile = tiles[blockIdx.x >> 2], q = blockIdx.x & 3;
-        if (tile != kNoTile) compute_item(tile, 0xFu << (4 * q), 1u << q);  // kNoTile: padding of an XCD-ordered list
+        // a diagonal tile's sub-blocks left of row block q's diagonal one hold
+        // only pairs a > b: not computed (their waves idle to the epilogue)
+        const uint32_t cols = (tile >> 16) == (tile & 0xFFFFu) ? 0xFu & ~((1u << q) - 1u) : 0xFu;
+        if (tile != kNoTile) compute_item(tile, cols << (4 * q), 1u << q);  // kNoTile: padding of an XCD-ordered list
     } else {
         // the screen's items, heaviest bucket first; the first by workgroup id
         // (rounds dealt in snake order, heavy beside light on a CU), the next
