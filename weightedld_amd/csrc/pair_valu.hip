@@ -421,7 +421,9 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_
                 res[i][j][0] = d;
                 res[i][j][1] = dp;
                 res[i][j][2] = r2;
-                const bool valid = a < b && b < L && site_ok[a] && site_ok[b];
+                // (every load issued, no short-circuit: a, b < LP; the compiler
+                // batches them instead of one round trip per pair)
+                const bool valid = (a < b) & (b < L) & ((site_ok[a] & site_ok[b]) != 0);
                 if constexpr (DENSE) {
                     if (a < b && b < L) {
                         const size_t k = (size_t)a * L + b;
@@ -625,6 +627,13 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
         for (int e = 0; e < 4; ++e)
 #pragma unroll
             for (int q = 0; q < 4; ++q) tot[e][q] = 0.0f;
+        // the epilogue's site flags, loaded now (one dword: the lane's four a
+        // rows; one byte: its b column), not behind the sums
+        uint32_t okA4 = 0, okB = 0;
+        if (has) {
+            okA4 = *reinterpret_cast<const uint32_t *>(site_ok + a0 + 16 * ui + 4 * g);
+            okB = site_ok[b0 + 16 * un + r];
+        }
         if (has) {
             const uint8_t *rowA = rcodes + (size_t)(a0 + 16 * ui + r) * NPr + 4 * g;
             const uint8_t *rowB = rcodes + (size_t)(b0 + 16 * un + r) * NPr + 4 * g;
@@ -734,7 +743,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
             res[e][0] = d;
             res[e][1] = dp;
             res[e][2] = r2;
-            if (has && a < b && b < L && site_ok[a] && site_ok[b] && r2 > thr) passmask |= 1u << e;
+            if (has && a < b && b < L && ((okA4 >> (8 * e)) & 0xFFu) && okB && r2 > thr) passmask |= 1u << e;
         }
         // ---- compaction: the tile's 64x64 pass bits, rows in b order ---------
         const bool own_row = tid < kTile && ((owned >> (tid >> 4)) & 1u);
