@@ -627,13 +627,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
         for (int e = 0; e < 4; ++e)
 #pragma unroll
             for (int q = 0; q < 4; ++q) tot[e][q] = 0.0f;
-        // the epilogue's site flags, loaded now (one dword: the lane's four a
-        // rows; one byte: its b column), not behind the sums
-        uint32_t okA4 = 0, okB = 0;
-        if (has) {
-            okA4 = *reinterpret_cast<const uint32_t *>(site_ok + a0 + 16 * ui + 4 * g);
-            okB = site_ok[b0 + 16 * un + r];
-        }
+        uint32_t okA4 = 0, okB = 0;  // the epilogue's site flags
         if (has) {
             const uint8_t *rowA = rcodes + (size_t)(a0 + 16 * ui + r) * NPr + 4 * g;
             const uint8_t *rowB = rcodes + (size_t)(b0 + 16 * un + r) * NPr + 4 * g;
@@ -708,6 +702,11 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
             // (ref_tail_n <= 7, uniform)
             // (one position per step: the byte queues shift down by 8 bits, the
             // weights by one register)
+            // the epilogue's site flags (one dword: the lane's four a rows; one
+            // byte: its b column) in the same round trip as the tail, not one
+            // load per pair behind the sums
+            okA4 = *reinterpret_cast<const uint32_t *>(site_ok + a0 + 16 * ui + 4 * g);
+            okB = site_ok[b0 + 16 * un + r];
             if (ref_tail_n) fetch_tail();
             float4 wlo = cw[0], whi = cw[1];
             uint32_t qb0 = __float_as_uint(cw[2].x), qb1 = __float_as_uint(cw[2].y);
