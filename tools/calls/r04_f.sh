@@ -10,7 +10,8 @@ tools/gpu_step.sh 400 $out/ab_c4.txt python tools/ab_builds.py --config c4 --rep
   base=weightedld_amd/libweightedld.so tpw2=build/exp/tpw2/libweightedld.so tpw4=build/exp/tpw4/libweightedld.so \
   wg3=build/exp/wg3/libweightedld.so nbuf3=build/exp/nbuf3/libweightedld.so || exit $?
 tools/gpu_step.sh 300 $out/ab_c2.txt python tools/ab_builds.py --config c2 --reps 30 --rounds 3 \
-  spec=weightedld_amd/libweightedld.so nospec=build/exp/nospec/libweightedld.so tailold=build/exp/tailold/libweightedld.so || exit $?
+  spec=weightedld_amd/libweightedld.so nospec=build/exp/nospec/libweightedld.so tailold=build/exp/tailold/libweightedld.so \
+  noepi=build/exp/noepi/libweightedld.so noload=build/exp/noload/libweightedld.so nosel=build/exp/nosel/libweightedld.so || exit $?
 tools/gpu_step.sh 300 $out/bench_c4.log python bench.py --no-cpu-baseline || exit $?
 tools/gpu_step.sh 200 $out/bench_c2.log python bench.py --config c2 --no-cpu-baseline || exit $?
 tools/gpu_step.sh 200 $out/bench_ldb.log python bench.py --data ldblocks --no-cpu-baseline || exit $?

@@ -636,6 +636,9 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
             uint32_t ca[4], cb[4];
             float4 cw[4];
             auto fetch = [&](uint32_t k0) {
+#ifdef WLD_DIAG_NOLOAD  // diagnostic (wrong sums): every stage re-reads stage 0 (L1-resident)
+                k0 = 0;
+#endif
 #pragma unroll
                 for (int grp = 0; grp < 4; ++grp) {
                     ca[grp] = *reinterpret_cast<const uint32_t *>(rowA + k0 + 16 * grp);
@@ -742,7 +745,11 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
             res[e][0] = d;
             res[e][1] = dp;
             res[e][2] = r2;
+#ifndef WLD_DIAG_NOEPI
             if (has && a < b && b < L && ((okA4 >> (8 * e)) & 0xFFu) && okB && r2 > thr) passmask |= 1u << e;
+#else  // diagnostic (no rows): the sums kept live, nothing passes, no compaction
+            if (r2 == 12345.0f && okB) passmask |= 1u << e;
+#endif
         }
         // ---- compaction: the tile's 64x64 pass bits, rows in b order ---------
         const bool own_row = tid < kTile && ((owned >> (tid >> 4)) & 1u);
