@@ -930,6 +930,9 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     auto src_a = [&](uint32_t tile) { return a6 + (size_t)(4 * (tile >> 16) + wave) * NK * kF6ABytes; };
     auto src_b = [&](uint32_t tile) { return b4 + (size_t)(4 * (tile & 0xFFFFu) + wave) * NK * kF6BBytes; };
     auto issue = [&](const uint8_t *sA, const uint8_t *sB, uint32_t kb, uint32_t buf) {
+#ifdef WLD_DIAG_FP6_NODMA  // diagnostic (wrong sums): stages past the first two reuse their buffers' data
+        if (kb >= 2) return;
+#endif
         const uint32_t gb = lds + buf * kF6Stage;
         const uint8_t *a = sA + (size_t)kb * kF6ABytes;
         glds16_s(a, lane16, gb + wave * kF6ABytes);
