@@ -509,18 +509,28 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
                 const uint32_t nb = (uint32_t)__popc(bits);  // nb >= 1
                 atomicAdd(sc.cand_count, 1u);
                 atomicAdd(sc.cand_count + 1, nb);  // sub-blocks to compute (stats)
+                // (a list entry: a slot of its bucket; none once the pass is
+                // given up, whose mark sits in bucket 0's count)
+                auto slot = [&](uint32_t bucket) -> uint32_t {
+                    const uint32_t k = atomicAdd(&sc.cand_buckets[bucket], 1u);
+                    return (k & kAbandonBit) || k >= sc.cand_cap ? ~0u : bucket * sc.cand_cap + k;
+                };
                 if (!sc.rb_items) {
-                    const uint32_t e = (16u - nb) * sc.cand_cap + atomicAdd(&sc.cand_buckets[16u - nb], 1u);
-                    sc.cand_list[e] = (ta << 16) | tb;
-                    sc.cand_bits[e] = bits;
+                    const uint32_t e = slot(16u - nb);
+                    if (e != ~0u) {
+                        sc.cand_list[e] = (ta << 16) | tb;
+                        sc.cand_bits[e] = bits;
+                    }
                 } else {
                     // the tile's 16-row blocks in order, packed greedily into
                     // items of at most four computed sub-blocks (one per wave)
                     uint32_t empty = 0, cur = 0, cur_k = 0;
                     auto emit = [&]() {
-                        const uint32_t e = (4u - cur_k) * sc.cand_cap + atomicAdd(&sc.cand_buckets[4u - cur_k], 1u);
-                        sc.cand_list[e] = (ta << 16) | tb;
-                        sc.cand_bits[e] = cur;
+                        const uint32_t e = slot(4u - cur_k);
+                        if (e != ~0u) {
+                            sc.cand_list[e] = (ta << 16) | tb;
+                            sc.cand_bits[e] = cur;
+                        }
                     };
                     for (uint32_t q = 0; q < 4; ++q) {
                         const uint32_t rb = (bits >> (4 * q)) & 0xFu, k = (uint32_t)__popc(rb);
