@@ -13,6 +13,10 @@ tools/gpu_step.sh 200 $out/bench_shard4.log python bench.py --rehearse-dist --re
 tools/gpu_step.sh 200 $out/bench_gpus2.log python bench.py --gpus 2 --collectives gloo --check-steps 2 --no-cpu-baseline || exit $?
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_c4 -o c4 -- \
   python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline > $out/prof_c4.log 2>&1 || { echo "prof failed"; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_ldb -o ldb -- \
+  python3 bench.py --data ldblocks --steps 30 --warmup 5 --no-cpu-baseline > $out/prof_ldb.log 2>&1 || { echo "prof ldb failed"; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_c2 -o c2 -- \
+  python3 bench.py --config c2 --steps 100 --warmup 10 --no-cpu-baseline > $out/prof_c2.log 2>&1 || { echo "prof c2 failed"; exit 1; }
 bargs="--steps 5 --warmup 2 --settle-s 0 --no-cpu-baseline"
 timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
   SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --output-format csv -d $out/pmc_sq -o sq -- \
