@@ -11,7 +11,10 @@ tools/gpu_step.sh 400 $out/ab_c4.txt python tools/ab_builds.py --config c4 --rep
   wg3=build/exp/wg3/libweightedld.so nbuf3=build/exp/nbuf3/libweightedld.so nodma=build/exp/nodma/libweightedld.so || exit $?
 tools/gpu_step.sh 300 $out/ab_c2.txt python tools/ab_builds.py --config c2 --reps 30 --rounds 3 \
   spec=weightedld_amd/libweightedld.so nospec=build/exp/nospec/libweightedld.so tailold=build/exp/tailold/libweightedld.so \
-  noepi=build/exp/noepi/libweightedld.so noload=build/exp/noload/libweightedld.so nosel=build/exp/nosel/libweightedld.so || exit $?
+  noepi=build/exp/noepi/libweightedld.so noload=build/exp/noload/libweightedld.so nosel=build/exp/nosel/libweightedld.so \
+  cvt=build/exp/cvt/libweightedld.so || exit $?
+WLD_AB_DATA=ldblocks tools/gpu_step.sh 300 $out/ab_ldb.txt python tools/ab_builds.py --config c4 --reps 10 --rounds 3 \
+  base=weightedld_amd/libweightedld.so cvt=build/exp/cvt/libweightedld.so || exit $?
 tools/gpu_step.sh 300 $out/bench_c4.log python bench.py --no-cpu-baseline || exit $?
 tools/gpu_step.sh 200 $out/bench_c2.log python bench.py --config c2 --no-cpu-baseline || exit $?
 tools/gpu_step.sh 200 $out/bench_ldb.log python bench.py --data ldblocks --no-cpu-baseline || exit $?

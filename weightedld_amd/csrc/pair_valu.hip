@@ -594,6 +594,23 @@ __global__ __launch_bounds__(256) void ref_layout_kernel(const uint8_t *__restri
 // LOOP: the candidate launch over the screen's item list (buckets, work
 // counter, fused chunk scan); else the full run's tiles in four 16-row items
 // each (workgroup 4t + q: tile t's row block q).
+// the item kernel's operands: byte converts of masked code dwords (1) or
+// per-element selects (0)
+#ifndef WLD_ITEM_CVT
+#define WLD_ITEM_CVT 0
+#endif
+// byte e of x as a float (v_cvt_f32_ubyte<e>: no shift or mask first; e a
+// constant after unrolling)
+__device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
+    float r;
+    switch (e) {
+    case 0: asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(r) : "v"(x)); break;
+    case 1: asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(x)); break;
+    case 2: asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(r) : "v"(x)); break;
+    default: asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(r) : "v"(x)); break;
+    }
+    return r;
+}
 #ifndef WLD_REF_ITEM_WG
 #define WLD_REF_ITEM_WG 5  // workgroups per CU, full runs (<= 102 VGPRs, no spill)
 #endif
@@ -679,10 +696,22 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
 #pragma unroll
                 for (int grp = 0; grp < 4; ++grp) {
                     const float we[4] = {Wt[grp].x, Wt[grp].y, Wt[grp].z, Wt[grp].w};
+#if WLD_ITEM_CVT
+                    // the four elements' in / major bits as bytes 0/1 (one mask
+                    // per dword), each turned into 0.0/1.0 by a byte convert
+                    const uint32_t ai = A[grp] & 0x01010101u, am = (A[grp] >> 1) & 0x01010101u;
+                    const uint32_t bi = B[grp] & 0x01010101u, bm = (B[grp] >> 1) & 0x01010101u;
+#endif
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const uint32_t xa = A[grp] >> (8 * e), xb = B[grp] >> (8 * e);
-#ifndef WLD_DIAG_NOSEL
+#if WLD_ITEM_CVT && !defined(WLD_DIAG_NOSEL)
+                        // w x 1.0 or w x 0.0: exact; a -0.0 term (negative w
+                        // masked) adds nothing to a chain that starts at +0.0
+                        const float u = we[e] * cvt_ubyte(ai, e), v = we[e] * cvt_ubyte(am, e);
+                        const float fi = cvt_ubyte(bi, e), fm = cvt_ubyte(bm, e);
+                        (void)xa, (void)xb;
+#elif !defined(WLD_DIAG_NOSEL)
                         const float u = (xa & kCodeIn) ? we[e] : 0.0f, v = (xa & kCodeMaj) ? we[e] : 0.0f;
                         const float fi = (float)(xb & 1u), fm = (float)((xb >> 1) & 1u);
 #else  // diagnostic (wrong sums): the operands without their selects and converts
