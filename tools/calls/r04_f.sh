@@ -5,7 +5,8 @@
 # bench lines
 out=gpurun_out/r04f; mkdir -p $out; export TMPDIR=/tmp
 tools/gpu_step.sh 600 $out/tests.txt python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu \
-  tests/test_gpu_fp6.py tests/test_gpu_refsums.py tests/test_gpu_parity.py -k "fp6 or gather_behind or staging or sharded or site_map or ref" || exit $?
+  tests/test_gpu_fp6.py tests/test_gpu_refsums.py tests/test_gpu_parity.py \
+  -k "fp6 or gather_behind or staging_overflow or ref_rows_bit_exact or ref_dense" || exit $?
 tools/gpu_step.sh 400 $out/ab_c4.txt python tools/ab_builds.py --config c4 --reps 20 --rounds 3 \
   base=weightedld_amd/libweightedld.so tpw2=build/exp/tpw2/libweightedld.so tpw4=build/exp/tpw4/libweightedld.so \
   wg3=build/exp/wg3/libweightedld.so nbuf3=build/exp/nbuf3/libweightedld.so nodma=build/exp/nodma/libweightedld.so || exit $?
