@@ -4,6 +4,7 @@
 # scan (WLD_SPEC_GATHER); the item kernel's tail loads: tests, C4 and C2 A/B,
 # bench lines
 out=gpurun_out/r04f; mkdir -p $out; export TMPDIR=/tmp
+tools/gpu_step.sh 60 $out/fp6_32_probe.txt tools/probes/fp6_32_probe || exit $?
 tools/gpu_step.sh 600 $out/tests.txt python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu \
   tests/test_gpu_fp6.py tests/test_gpu_refsums.py tests/test_gpu_parity.py \
   -k "fp6 or gather_behind or staging_overflow or ref_rows_bit_exact or ref_dense" || exit $?
