@@ -10,7 +10,7 @@ tools/gpu_step.sh 600 $out/tests.txt python -u -m pytest -v --timeout 300 --time
   -k "fp6 or gather_behind or staging_overflow or ref_rows_bit_exact or ref_dense" || exit $?
 tools/gpu_step.sh 400 $out/ab_c4.txt python tools/ab_builds.py --config c4 --reps 20 --rounds 3 \
   base=weightedld_amd/libweightedld.so tpw2=build/exp/tpw2/libweightedld.so tpw4=build/exp/tpw4/libweightedld.so \
-  wg3=build/exp/wg3/libweightedld.so nbuf3=build/exp/nbuf3/libweightedld.so nodma=build/exp/nodma/libweightedld.so || exit $?
+  wg3=build/exp/wg3/libweightedld.so nbuf3=build/exp/nbuf3/libweightedld.so nodma=build/exp/nodma/libweightedld.so fp632=build/exp/fp632/libweightedld.so || exit $?
 tools/gpu_step.sh 300 $out/ab_c2.txt python tools/ab_builds.py --config c2 --reps 30 --rounds 3 \
   spec=weightedld_amd/libweightedld.so nospec=build/exp/nospec/libweightedld.so tailold=build/exp/tailold/libweightedld.so \
   noepi=build/exp/noepi/libweightedld.so noload=build/exp/noload/libweightedld.so nosel=build/exp/nosel/libweightedld.so \
