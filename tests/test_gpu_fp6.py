@@ -108,9 +108,9 @@ def test_fp6_exact_mode_rows(W):
 def test_fp6_handover_to_i8(W):
     """Auto policy: at a threshold where the fp6 screen reaches a sixteenth of
     the tiles as candidates it gives the pass up and the pass re-runs on the i8
-    screen (screen_fp6 2); that threshold and any lower one screen on i8 from
-    then on; higher thresholds stay on fp6.  Rows equal the oracle's
-    throughout."""
+    screen (screen_fp6 2), or (one round of tiles) completes; that threshold
+    and any lower one screen on i8 from then on; higher thresholds stay on
+    fp6.  Rows equal the oracle's throughout."""
     import bench
     buf = bench.synth(2048, 2000)
     w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
@@ -122,7 +122,10 @@ def test_fp6_handover_to_i8(W):
         st = c.stats()
         seen.append((thr, st["screened"], st["screen_fp6"], st["candidate_tiles"], st["tiles"]))
         _bits_equal(c.rows(), O.all_pairs(buf, w, np.float32(thr)))
-    assert seen[0][2] == 2, seen
+    # (a grid of one round of workgroups cannot give up: every workgroup has
+    # read the count before the first candidate lands; the pass then
+    # completes and hands over by its count)
+    assert seen[0][2] == 2 or (seen[0][2] == 1 and seen[0][3] * 16 > seen[0][4]), seen
     assert seen[1][2] == 0 and seen[2][2] == 0 and seen[3][1:3] == (1, 1), seen
     c.close()
 

@@ -407,16 +407,20 @@ def test_gather_behind_scan_sequences(W, ctxs, kern):
     buf = synth(L, N, 6)
     w = np.random.default_rng(3).random(N).astype(np.float32)
     ctx.load(buf, w)
-    seq = [(0.5, None), (0.2, None), (0.0, None), (0.0, None), (1.01, None), (0.3, None), (0.0, (3, 1)), (0.1, None)]
+    seq = [(0.5, None), (0.2, None), (0.0, None), (0.0, None), (1.01, None), (0.3, None), (0.0, (3,)), (0.1, None)]
     for thr, shard in seq:
-        if shard:  # (n_shards, shard): the shard's rows are the full run's with a in its chunk rows
-            b, e = ctx.shard_chunk_rows(L, *shard)
-            n = ctx.run(thr, b, e)
+        if shard:  # every shard of an n-way split: the full run's rows with a in its chunk rows
             full = O.all_pairs(buf, w, np.float32(thr))
-            sel = (full["site_a"] // 256 >= b) & (full["site_a"] // 256 < e)
-            ref = {k: np.asarray(full[k])[sel] for k in ("site_a", "site_b", "d", "d_prime", "r2")}
-            assert n == int(sel.sum()) > 0
-            compare_rows(ctx.rows(), ref, thr, buf=buf, w=w)
+            total = 0
+            for k in range(shard[0]):
+                b, e = ctx.shard_chunk_rows(L, shard[0], k)
+                n = ctx.run(thr, b, e)
+                sel = (full["site_a"] // 256 >= b) & (full["site_a"] // 256 < e)
+                ref = {f: np.asarray(full[f])[sel] for f in ("site_a", "site_b", "d", "d_prime", "r2")}
+                assert n == int(sel.sum())
+                compare_rows(ctx.rows(), ref, thr, buf=buf, w=w)
+                total += n
+            assert total == len(full["site_a"]) > 0
             continue
         n = ctx.run(thr)
         ref = O.all_pairs(buf, w, np.float32(thr))

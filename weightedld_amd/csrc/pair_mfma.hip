@@ -895,54 +895,30 @@ struct AccF6 {
     }
 };
 
-// TPW tiles per workgroup (workgroup b: list entries 8 (TPW (b >> 3) + j) +
-// (b & 7), consecutive entries of its XCD's queue in the XCD-ordered list):
-// the next tile's first stage is issued during this tile's last stage, so its
-// DMA lands while this tile's epilogue runs (1: one tile per workgroup).
-#ifndef WLD_FP6_TPW
-#define WLD_FP6_TPW 1
-#endif
 #ifndef WLD_FP6_WG
 #define WLD_FP6_WG 4  // workgroups per CU
 #endif
-// stage buffers: 2 (one stage in flight while one is read) or 3 (two in
-// flight, a counted vmcnt: LDS-DMA completes in issue order; three
-// workgroups per CU fit 3 x 16 KB each)
-#ifndef WLD_FP6_NBUF
-#define WLD_FP6_NBUF 2
-#endif
-static_assert(WLD_FP6_NBUF == 2 || (WLD_FP6_NBUF == 3 && WLD_FP6_TPW == 1), "fp6 stage ring");
 __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const uint8_t *__restrict__ a6,
                                                                   const uint8_t *__restrict__ b4,
                                                                   const uint64_t *__restrict__ ok_bits,
                                                                   const uint32_t *__restrict__ tiles, uint32_t n_tiles,
                                                                   uint32_t NK, uint32_t L, uint32_t n_chunk_rows,
                                                                   float thr, OrderArgs o, ScreenArgs sc) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[WLD_FP6_NBUF * kF6Stage];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6Stage];
     __shared__ unsigned long long sBits[kTile];
     __shared__ uint32_t sRowBase[kTile];
     __shared__ uint32_t sBail;
     if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
-    // read by thread 0 while the tile's first stage is in flight, published by
-    // the first stage barrier: one decision for the whole workgroup
-    auto bail_check = [&] {
-        if (tid == 0)
-            sBail = sc.bail && __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > sc.bail;
-    };
-    // the j-th tile of this workgroup (kNoTile: padding of an XCD-ordered list, or past the end)
-    auto tile_at = [&](uint32_t j) -> uint32_t {
-        const uint32_t i = 8 * (WLD_FP6_TPW * (blockIdx.x >> 3) + j) + (blockIdx.x & 7);
-        return i < n_tiles ? tiles[i] : kNoTile;
-    };
-    // this wave's DMA sources for a tile: A of row block 4 ta + wave, B of column block 4 tb + wave
-    auto src_a = [&](uint32_t tile) { return a6 + (size_t)(4 * (tile >> 16) + wave) * NK * kF6ABytes; };
-    auto src_b = [&](uint32_t tile) { return b4 + (size_t)(4 * (tile & 0xFFFFu) + wave) * NK * kF6BBytes; };
-    auto issue = [&](const uint8_t *sA, const uint8_t *sB, uint32_t kb, uint32_t buf) {
-#ifdef WLD_DIAG_FP6_NODMA  // diagnostic (wrong sums): stages past the first two reuse their buffers' data
-        if (kb >= 2) return;
-#endif
+    // (kNoTile: padding of an XCD-ordered list, or past the end of the grid)
+    const uint32_t tile = blockIdx.x < n_tiles ? tiles[blockIdx.x] : kNoTile;
+    if (tile == kNoTile) return;  // (uniform: the whole workgroup)
+    const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
+    // this wave's DMA sources: A of row block 4 ta + wave, B of column block 4 tb + wave
+    const uint8_t *sA = a6 + (size_t)(4 * ta + wave) * NK * kF6ABytes;
+    const uint8_t *sB = b4 + (size_t)(4 * tb + wave) * NK * kF6BBytes;
+    auto issue = [&](uint32_t kb, uint32_t buf) {
         const uint32_t gb = lds + buf * kF6Stage;
         const uint8_t *a = sA + (size_t)kb * kF6ABytes;
         glds16_s(a, lane16, gb + wave * kF6ABytes);
@@ -950,167 +926,25 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
         glds16_s(a + 2048, lane16, gb + wave * kF6ABytes + 2048);
         glds16_s(sB + (size_t)kb * kF6BBytes, lane16, gb + 4 * kF6ABytes + wave * kF6BBytes);
     };
-    uint32_t j = 0, tile = tile_at(0);
-    while (tile == kNoTile && ++j < WLD_FP6_TPW) tile = tile_at(j);
-    if (tile == kNoTile) return;  // (uniform: the whole workgroup)
-    const uint8_t *sA = src_a(tile), *sB = src_b(tile);
-    issue(sA, sB, 0, 0);
-    if (WLD_FP6_NBUF == 3 && NK > 1) issue(sA, sB, 1, 1);
-    bail_check();
-    uint32_t buf = 0;
-    for (;;) {
-        // the next tile of this workgroup (its first stage is issued in this one's last)
-        uint32_t jn = j + 1, next = kNoTile;
-        while (jn < WLD_FP6_TPW && (next = tile_at(jn)) == kNoTile) ++jn;
-        const uint8_t *nA = next != kNoTile ? src_a(next) : sA, *nB = next != kNoTile ? src_b(next) : sB;
-        const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
-        const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
-        AccF6 acc;
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-            for (int x = 0; x < 2; ++x)
-#pragma unroll
-                for (int y = 0; y < 2; ++y) acc.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-        for (uint32_t kb = 0; kb < NK; ++kb) {
-            // this wave's copies of this stage landed (with three buffers the
-            // next stage's four may still be in flight) ...
-            if (WLD_FP6_NBUF == 3 && kb + 1 < NK) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();  // ... and every other wave's; the buffer read last stage is free
-            asm volatile("" ::: "memory");
-            if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
-                if (tid == 0) {
-                    atomicOr(sc.cand_count, kAbandonBit);
-                    atomicOr(sc.cand_buckets, kAbandonBit);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                return;
-            }
-            if (WLD_FP6_NBUF == 3) {
-                if (kb + 2 < NK) issue(sA, sB, kb + 2, buf == 0 ? 2 : buf - 1);
-            } else if (kb + 1 < NK) {
-                issue(sA, sB, kb + 1, buf ^ 1);
-            } else if (next != kNoTile) {
-                issue(nA, nB, 0, buf ^ 1);
-            }
-            const uint8_t *g = smem + buf * kF6Stage;
-            const uint8_t *pa = g + wave * kF6ABytes + lane * 24;
-            const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
-                        i2 = *reinterpret_cast<const uint2 *>(pa + 16);
-            const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536),
-                        m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
-                        m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
-            const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
-            const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
-#pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                const uint4 r = *reinterpret_cast<const uint4 *>(g + 4 * kF6ABytes + n * kF6BBytes + lane * 16);
-                constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
-                const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
-                const v8i bmin = {(int)r.x & kMinor, (int)r.y & kMinor, (int)r.z & kMinor, (int)r.w & kMinor,
-                                  0, 0, 0, 0};
-                acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, braw, acc.v[n][0][0], 2, 4, 0,
-                                                                                  0x7F7F7F7F, 0, 0x7F7F7F7F);
-                acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc.v[n][0][1], 2, 4, 0,
-                                                                                  0x7F7F7F7F, 0, 0x7F7F7F7F);
-                acc.v[n][1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, braw, acc.v[n][1][0], 2, 4, 0,
-                                                                                  0x7F7F7F7F, 0, 0x7F7F7F7F);
-                acc.v[n][1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, bmin, acc.v[n][1][1], 2, 4, 0,
-                                                                                  0x7F7F7F7F, 0, 0x7F7F7F7F);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
-            buf = buf + 1 == WLD_FP6_NBUF ? 0 : buf + 1;
-        }
-        // (the f64 fallback of pair_cand: exact sums from X, Y; the launch uses
-        // the f32 test, sc.f32 == 2)
-        auto sum = [&](int x, int y, int i) -> double {
-            const float2 p = acc.raw(x, i);
-            return ((double)p.x + (y ? -(double)p.y : (double)p.y)) * 0.5;
-        };
-        const DenseArgs dn{nullptr, nullptr, nullptr, nullptr};
-        tile_epilogue<kModeScreen, AccF6>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, 0, o, dn, sc, sBits,
-                                          sRowBase);
-        if (next == kNoTile) break;
-        __syncthreads();  // (the epilogue's LDS state is reused by the next tile's)
-        tile = next, sA = nA, sB = nB, j = jn;
-        bail_check();
-    }
-}
-
-// The fp6 screen on the 32x32x64 form (WLD_FP6_32, A/B builds): wave w owns
-// a rows 32 (w & 1).. against b columns 32 (w >> 1)..; per 128 sequences 8
-// MFMAs of twice the work of the 16x16x128 form, which hold the SIMD's vector
-// issue for the same cycles each: half the issue per flop.  Same operand
-// copies and LDS-DMA as pair_fp6_screen_kernel; in the stage, a row group's A
-// block sits at 3200 G (the odd groups 32 banks over, so a wave's two groups
-// read conflict-free).  Lane l of a 32x32x64 operand holds row (col) l & 31,
-// sequences 64 h + 32 (l >> 5) + j: the 16x16 copy's lane (l & 15) + 16 (2 h +
-// (l >> 5)) of 16-group (l & 31) >> 4.
-#ifndef WLD_FP6_32
-#define WLD_FP6_32 0
-#endif
-typedef float v16f __attribute__((ext_vector_type(16)));
-struct AccF6x32 {
-    static constexpr int kPlanes = 1;
-    static constexpr int kPairs = 16;
-    v16f v[2][2];  // [channel_a in / major][X / Y]
-    __device__ __forceinline__ float2 raw(int x, int i) const { return make_float2(v[x][0][i], v[x][1][i]); }
-    // C/D: col = lane & 31, row = 8 (i >> 2) + 4 (lane >> 5) + (i & 3) (tools/probes/fp6_32_probe.hip)
-    static __device__ __forceinline__ uint32_t a_local(int i, uint32_t wave, uint32_t lane) {
-        return 32 * (wave & 1) + 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3);
-    }
-    static __device__ __forceinline__ uint32_t b_local(int i, uint32_t wave, uint32_t lane) {
-        return 32 * (wave >> 1) + (lane & 31);
-    }
-};
-constexpr int kF6AStride32 = 3200, kF6Stage32 = 4 * kF6AStride32 + 4 * kF6BBytes;
-__global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen32_kernel(
-    const uint8_t *__restrict__ a6, const uint8_t *__restrict__ b4, const uint64_t *__restrict__ ok_bits,
-    const uint32_t *__restrict__ tiles, uint32_t n_tiles, uint32_t NK, uint32_t L, uint32_t n_chunk_rows, float thr,
-    OrderArgs o, ScreenArgs sc) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6Stage32];
-    __shared__ unsigned long long sBits[kTile];
-    __shared__ uint32_t sRowBase[kTile];
-    __shared__ uint32_t sBail;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
-    const uint32_t i = 8 * (blockIdx.x >> 3) + (blockIdx.x & 7);
-    const uint32_t tile = i < n_tiles ? tiles[i] : kNoTile;
-    if (tile == kNoTile) return;  // (uniform)
-    const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
-    const uint8_t *sA = a6 + (size_t)(4 * ta + wave) * NK * kF6ABytes;
-    const uint8_t *sB = b4 + (size_t)(4 * tb + wave) * NK * kF6BBytes;
-    auto issue = [&](uint32_t kb, uint32_t buf) {
-        const uint32_t gb = lds + buf * kF6Stage32;
-        const uint8_t *a = sA + (size_t)kb * kF6ABytes;
-        glds16_s(a, lane16, gb + wave * kF6AStride32);
-        glds16_s(a + 1024, lane16, gb + wave * kF6AStride32 + 1024);
-        glds16_s(a + 2048, lane16, gb + wave * kF6AStride32 + 2048);
-        glds16_s(sB + (size_t)kb * kF6BBytes, lane16, gb + 4 * kF6AStride32 + wave * kF6BBytes);
-    };
     issue(0, 0);
+    // the give-up test: read by thread 0 while the first stage is in flight,
+    // published by the first stage barrier (one decision for the workgroup)
     if (tid == 0)
         sBail = sc.bail && __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > sc.bail;
     const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
-    // this lane's operand offsets in a stage (k-half h adds 32 (2 h) lanes' worth)
-    const uint32_t r = lane & 31, gl = lane >> 5;
-    const uint32_t aoff = (2 * (wave & 1) + (r >> 4)) * kF6AStride32 + ((r & 15) + 16 * gl) * 24;
-    const uint32_t boff = 4 * kF6AStride32 + (2 * (wave >> 1) + (r >> 4)) * kF6BBytes + ((r & 15) + 16 * gl) * 16;
-    AccF6x32 acc;
+    AccF6 acc;
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+    for (int n = 0; n < 4; ++n)
 #pragma unroll
-        for (int y = 0; y < 2; ++y)
+        for (int x = 0; x < 2; ++x)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) acc.v[x][y][e] = 0.0f;
+            for (int y = 0; y < 2; ++y) acc.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
     uint32_t buf = 0;
     for (uint32_t kb = 0; kb < NK; ++kb) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this stage landed
         __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
         asm volatile("" ::: "memory");
-        if (kb == 0 && sBail) {  // (uniform) give the pass up
+        if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
             if (tid == 0) {
                 atomicOr(sc.cand_count, kAbandonBit);
                 atomicOr(sc.cand_buckets, kAbandonBit);
@@ -1119,40 +953,41 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen32_kernel(
             return;
         }
         if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
-        const uint8_t *g = smem + buf * kF6Stage32;
+        const uint8_t *g = smem + buf * kF6Stage;
+        const uint8_t *pa = g + wave * kF6ABytes + lane * 24;
+        const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
+                    i2 = *reinterpret_cast<const uint2 *>(pa + 16);
+        const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536), m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
+                    m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
+        const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
+        const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint8_t *pa = g + aoff + h * (32 * 24);
-            const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
-                        i2 = *reinterpret_cast<const uint2 *>(pa + 16);
-            const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536),
-                        m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
-                        m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
-            const uint4 rb = *reinterpret_cast<const uint4 *>(g + boff + h * (32 * 16));
-            const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
-            const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
+        for (int n = 0; n < 4; ++n) {
+            const uint4 r = *reinterpret_cast<const uint4 *>(g + 4 * kF6ABytes + n * kF6BBytes + lane * 16);
             constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
-            const v8i braw = {(int)rb.x, (int)rb.y, (int)rb.z, (int)rb.w, 0, 0, 0, 0};
-            const v8i bmin = {(int)rb.x & kMinor, (int)rb.y & kMinor, (int)rb.z & kMinor, (int)rb.w & kMinor, 0, 0, 0, 0};
-            acc.v[0][0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ai, braw, acc.v[0][0], 2, 4, 0, 0x7F7F7F7F, 0,
-                                                                          0x7F7F7F7F);
-            acc.v[0][1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ai, bmin, acc.v[0][1], 2, 4, 0, 0x7F7F7F7F, 0,
-                                                                          0x7F7F7F7F);
-            acc.v[1][0] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(am, braw, acc.v[1][0], 2, 4, 0, 0x7F7F7F7F, 0,
-                                                                          0x7F7F7F7F);
-            acc.v[1][1] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(am, bmin, acc.v[1][1], 2, 4, 0, 0x7F7F7F7F, 0,
-                                                                          0x7F7F7F7F);
+            const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
+            const v8i bmin = {(int)r.x & kMinor, (int)r.y & kMinor, (int)r.z & kMinor, (int)r.w & kMinor, 0, 0, 0, 0};
+            acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, braw, acc.v[n][0][0], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+            acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc.v[n][0][1], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+            acc.v[n][1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, braw, acc.v[n][1][0], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+            acc.v[n][1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, bmin, acc.v[n][1][1], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
         buf ^= 1;
     }
+    // (the f64 fallback of pair_cand: exact sums from X, Y; the launch uses
+    // the f32 test, sc.f32 == 2)
     auto sum = [&](int x, int y, int i) -> double {
         const float2 p = acc.raw(x, i);
         return ((double)p.x + (y ? -(double)p.y : (double)p.y)) * 0.5;
     };
     const DenseArgs dn{nullptr, nullptr, nullptr, nullptr};
-    tile_epilogue<kModeScreen, AccF6x32>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, 0, o, dn, sc, sBits,
-                                         sRowBase);
+    tile_epilogue<kModeScreen, AccF6>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, 0, o, dn, sc, sBits,
+                                      sRowBase);
 }
 
 void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b4,
@@ -1392,15 +1227,9 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
         sc.f32 = 2;
         sc.bail = m.fp6_bail;
         screen_consts(m.fp6->Tg, 2.0f * sc.Rf, sc.E, sc.mloc);
-        // WLD_FP6_TPW tiles per workgroup; the grid a multiple of 8 (each
-        // workgroup's tiles on its XCD's queue of the XCD-ordered list)
-        const uint32_t grid = (m.n_tiles + 8 * WLD_FP6_TPW - 1) / (8 * WLD_FP6_TPW) * 8;
-        if (WLD_FP6_32)
-            hipLaunchKernelGGL(pair_fp6_screen32_kernel, dim3((m.n_tiles + 7) / 8 * 8), dim3(256), 0, s, m.fp6->a6,
-                               m.fp6->b4, ok_bits, m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
-        else
-            hipLaunchKernelGGL(pair_fp6_screen_kernel, dim3(grid), dim3(256), 0, s, m.fp6->a6, m.fp6->b4, ok_bits,
-                               m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
+        // (one tile per workgroup, the XCD-ordered list)
+        hipLaunchKernelGGL(pair_fp6_screen_kernel, dim3(m.n_tiles), dim3(256), 0, s, m.fp6->a6, m.fp6->b4, ok_bits,
+                           m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
         if (screen_done) (void)hipEventRecord(screen_done, s);
         launch_candidates(m, n, idx, ok_bits, o, dn, sc, s);
         return true;

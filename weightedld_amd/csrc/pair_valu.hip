@@ -595,19 +595,35 @@ __global__ __launch_bounds__(256) void ref_layout_kernel(const uint8_t *__restri
 // counter, fused chunk scan); else the full run's tiles in four 16-row items
 // each (workgroup 4t + q: tile t's row block q).
 // the item kernel's operands: byte converts of masked code dwords (1) or
-// per-element selects (0)
+// per-element selects (0, A/B builds)
 #ifndef WLD_ITEM_CVT
-#define WLD_ITEM_CVT 0
+#define WLD_ITEM_CVT 1
 #endif
-// byte e of x as a float (v_cvt_f32_ubyte<e>: no shift or mask first; e a
-// constant after unrolling)
+// byte e of x as a float by v_cvt_f32_ubyte<e> (no shift or mask first; the
+// compiler's own lowering extracts the byte first).  Inline asm is invisible
+// to the hazard recognizer as a VALU write: a result that an MFMA reads
+// directly needs the VALU -> MFMA wait states inside the statement (NOP = 1);
+// one that a VALU op consumes first (the weight products) does not.
+template <int NOP>
 __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
     float r;
     switch (e) {
-    case 0: asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(r) : "v"(x)); break;
-    case 1: asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(x)); break;
-    case 2: asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(r) : "v"(x)); break;
-    default: asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(r) : "v"(x)); break;
+    case 0:
+        if (NOP) asm("v_cvt_f32_ubyte0 %0, %1\n\ts_nop 1" : "=v"(r) : "v"(x));
+        else asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(r) : "v"(x));
+        break;
+    case 1:
+        if (NOP) asm("v_cvt_f32_ubyte1 %0, %1\n\ts_nop 1" : "=v"(r) : "v"(x));
+        else asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(x));
+        break;
+    case 2:
+        if (NOP) asm("v_cvt_f32_ubyte2 %0, %1\n\ts_nop 1" : "=v"(r) : "v"(x));
+        else asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(r) : "v"(x));
+        break;
+    default:
+        if (NOP) asm("v_cvt_f32_ubyte3 %0, %1\n\ts_nop 1" : "=v"(r) : "v"(x));
+        else asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(r) : "v"(x));
+        break;
     }
     return r;
 }
@@ -653,9 +669,6 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
             uint32_t ca[4], cb[4];
             float4 cw[4];
             auto fetch = [&](uint32_t k0) {
-#ifdef WLD_DIAG_NOLOAD  // diagnostic (wrong sums): every stage re-reads stage 0 (L1-resident)
-                k0 = 0;
-#endif
 #pragma unroll
                 for (int grp = 0; grp < 4; ++grp) {
                     ca[grp] = *reinterpret_cast<const uint32_t *>(rowA + k0 + 16 * grp);
@@ -708,8 +721,8 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
 #if WLD_ITEM_CVT && !defined(WLD_DIAG_NOSEL)
                         // w x 1.0 or w x 0.0: exact; a -0.0 term (negative w
                         // masked) adds nothing to a chain that starts at +0.0
-                        const float u = we[e] * cvt_ubyte(ai, e), v = we[e] * cvt_ubyte(am, e);
-                        const float fi = cvt_ubyte(bi, e), fm = cvt_ubyte(bm, e);
+                        const float u = we[e] * cvt_ubyte<0>(ai, e), v = we[e] * cvt_ubyte<0>(am, e);
+                        const float fi = cvt_ubyte<1>(bi, e), fm = cvt_ubyte<1>(bm, e);
                         (void)xa, (void)xb;
 #elif !defined(WLD_DIAG_NOSEL)
                         const float u = (xa & kCodeIn) ? we[e] : 0.0f, v = (xa & kCodeMaj) ? we[e] : 0.0f;
@@ -774,11 +787,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
             res[e][0] = d;
             res[e][1] = dp;
             res[e][2] = r2;
-#ifndef WLD_DIAG_NOEPI
             if (has && a < b && b < L && ((okA4 >> (8 * e)) & 0xFFu) && okB && r2 > thr) passmask |= 1u << e;
-#else  // diagnostic (no rows): the sums kept live, nothing passes, no compaction
-            if (r2 == 12345.0f && okB) passmask |= 1u << e;
-#endif
         }
         // ---- compaction: the tile's 64x64 pass bits, rows in b order ---------
         const bool own_row = tid < kTile && ((owned >> (tid >> 4)) & 1u);
