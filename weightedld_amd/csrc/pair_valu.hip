@@ -697,8 +697,9 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
             };
             if (n_st) fetch(0);
             v4f acc[4];
+            uint32_t in_cls = 0;  // this stage's index in its class (no modulo in the loop)
             for (uint32_t st = 0; st < n_st; ++st) {
-                if (st % ref_cs == 0)
+                if (in_cls == 0)
 #pragma unroll
                     for (int q = 0; q < 4; ++q) acc[q] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
                 uint32_t A[4], B[4];
@@ -737,11 +738,13 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                     }
                 }
                 // end of a class: its chain joins the ordered horizontal sum
-                if ((st + 1) % ref_cs == 0)
+                if (++in_cls == ref_cs) {
+                    in_cls = 0;
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
 #pragma unroll
                         for (int q = 0; q < 4; ++q) tot[e][q] += acc[q][e];
+                }
             }
             // the scalar tail (lib.rs:461-480), onto the horizontal sums in order
             // (ref_tail_n <= 7, uniform)
