@@ -444,6 +444,10 @@ def main():
         _, rows = shard_step(thr, cb, ce)
         return int(rows.shape[1]) if rows is not None else 0
 
+    # WLD_PIPE_DRAIN_ROWS=0: keep steps in flight after a step with rows too
+    # (its gather is queued behind its scan on the device)
+    drain_rows = os.environ.get("WLD_PIPE_DRAIN_ROWS", "1") != "0"
+
     def run_steps(k):
         if ctxs1 is not None:
             # N=1 pipelined: step i on context i % D (D-buffered rows), up to
@@ -456,8 +460,8 @@ def main():
             pend, r = collections.deque(), 0
             for i in range(k):
                 c = ctxs1[i % len(ctxs1)]
-                if len(pend) == len(ctxs1) or (r > 0 and pend):
-                    while pend and (len(pend) == len(ctxs1) or r > 0):
+                if len(pend) == len(ctxs1) or (drain_rows and r > 0 and pend):
+                    while pend and (len(pend) == len(ctxs1) or (drain_rows and r > 0)):
                         r = pend.popleft().run_wait()
                 if pend and serialize in ("pair", "stream"):
                     c.run_after(pend[-1])  # this pair kernel queued behind the previous one (device wait)

@@ -9,4 +9,8 @@ tools/gpu_step.sh 300 $out/ab_c2.txt python tools/ab_builds.py --config c2 --rep
   cvt=weightedld_amd/libweightedld.so nocvt=build/exp/nocvt/libweightedld.so || exit $?
 WLD_AB_DATA=ldblocks tools/gpu_step.sh 300 $out/ab_ldb.txt python tools/ab_builds.py --config c4 --reps 10 --rounds 3 \
   cvt=weightedld_amd/libweightedld.so nocvt=build/exp/nocvt/libweightedld.so || exit $?
+tools/gpu_step.sh 200 $out/bench_c2_drain.log python bench.py --config c2 --no-cpu-baseline || exit $?
+WLD_PIPE_DRAIN_ROWS=0 tools/gpu_step.sh 200 $out/bench_c2_nodrain.log python bench.py --config c2 --no-cpu-baseline || exit $?
+tools/gpu_step.sh 200 $out/bench_ldb_drain.log python bench.py --data ldblocks --no-cpu-baseline || exit $?
+WLD_PIPE_DRAIN_ROWS=0 tools/gpu_step.sh 200 $out/bench_ldb_nodrain.log python bench.py --data ldblocks --no-cpu-baseline || exit $?
 echo done
