@@ -444,9 +444,11 @@ def main():
         _, rows = shard_step(thr, cb, ce)
         return int(rows.shape[1]) if rows is not None else 0
 
-    # WLD_PIPE_DRAIN_ROWS=0: keep steps in flight after a step with rows too
-    # (its gather is queued behind its scan on the device)
-    drain_rows = os.environ.get("WLD_PIPE_DRAIN_ROWS", "1") != "0"
+    # steps stay in flight after a step with rows too: its gather is queued
+    # behind its scan on the device (C2 0.157 -> 0.135 ms/step, LD blocks
+    # 1.350 -> 1.305, profiles/r04g/); WLD_PIPE_DRAIN_ROWS=1 drains the
+    # pipeline after such a step first (rounds 1-3)
+    drain_rows = os.environ.get("WLD_PIPE_DRAIN_ROWS", "0") != "0"
 
     def run_steps(k):
         if ctxs1 is not None:
@@ -454,9 +456,7 @@ def main():
             # D - 1 steps in flight; the host completes the oldest step
             # (wld_run_wait) while the newer ones run.  Step i's screen may
             # start while step i-1's runs (WLD_PIPE_SERIALIZE=pair: queued
-            # behind it with wld_run_after); after a step with rows the
-            # pipeline drains first, so row assembly does not compete with
-            # the next kernels.
+            # behind it with wld_run_after).
             pend, r = collections.deque(), 0
             for i in range(k):
                 c = ctxs1[i % len(ctxs1)]
