@@ -12,7 +12,6 @@ descending rank order.
 """
 import collections
 import contextlib
-import os
 
 import numpy as np
 
@@ -162,14 +161,6 @@ class ShardStep:
         self.stream = (torch.cuda.ExternalStream(ctx.stream_ptr(), device=device) if device.type == "cuda"
                        else _HostStream())
         self.rows_seen = False  # some rank had rows in the last finished step
-        # the gathered counts go to pinned host memory by an async copy queued
-        # behind the all_gather; finish() waits on its event and reads them
-        # (no synchronous device-to-host read per step: the host's share of a
-        # short step, e.g. one of eight shards of config 4)
-        self.pinned = (device.type == "cuda" and not self.host and os.environ.get("WLD_DIST_PINNED", "1") != "0")
-        if self.pinned:
-            self.cnts_host = torch.empty(world, dtype=torch.int64, pin_memory=True)
-            self.cnts_evt = torch.cuda.Event()
 
     def enqueue(self, thr, chunk_begin, chunk_end, kernel_done=None):
         """The pair kernel, its row count and the count all_gather, on the
@@ -185,9 +176,6 @@ class ShardStep:
                 kernel_done.record(self.stream)
             if not self.host:
                 dist.all_gather_into_tensor(g.cnts, g.cnt, group=g.group)
-                if self.pinned:
-                    self.cnts_host.copy_(g.cnts, non_blocking=True)
-                    self.cnts_evt.record(self.stream)
 
     def finish(self):
         """Completes an enqueued step: (rows on this rank, gathered rows on rank 0 / None)."""
@@ -199,12 +187,8 @@ class ShardStep:
             with _stream_scope(self.stream):
                 g.cnt.fill_(int(self.cnt_dev.item()))  # host wait for this step's count
             dist.all_gather_into_tensor(g.cnts, g.cnt, group=g.group)
-        if self.pinned:
-            self.cnts_evt.synchronize()  # the step's one host wait when no rank has rows
-            counts = self.cnts_host.tolist()
-        else:
-            with _stream_scope(self.stream):
-                counts = g.cnts.tolist()  # the step's one host wait when no rank has rows
+        with _stream_scope(self.stream):
+            counts = g.cnts.tolist()  # the step's one host wait when no rank has rows
         self.rows_seen = max(counts) > 0
         n = self.ctx.run_wait()  # returns at once: the stream is idle
         if max(counts) == 0:
