@@ -928,9 +928,18 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     };
     issue(0, 0);
     // the give-up test: read by thread 0 while the first stage is in flight,
-    // published by the first stage barrier (one decision for the workgroup)
-    if (tid == 0)
-        sBail = sc.bail && __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > sc.bail;
+    // published by the first stage barrier (one decision for the workgroup):
+    // 0 go on, 1 give up and mark the set, 2 give up (already marked: the
+    // mark is two atomics on one word each; tens of thousands of workgroups
+    // repeating them serialise for milliseconds)
+    if (tid == 0) {
+        uint32_t v = 0;
+        if (sc.bail) {
+            const unsigned cc = __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v = cc > sc.bail ? ((cc & kAbandonBit) ? 2u : 1u) : 0u;
+        }
+        sBail = v;
+    }
     const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
     AccF6 acc;
 #pragma unroll
@@ -945,7 +954,7 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
         __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
         asm volatile("" ::: "memory");
         if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
-            if (tid == 0) {
+            if (tid == 0 && sBail == 1) {
                 atomicOr(sc.cand_count, kAbandonBit);
                 atomicOr(sc.cand_buckets, kAbandonBit);
             }
