@@ -6,4 +6,7 @@ tools/gpu_step.sh 400 $out/fp6_tests.txt python -u -m pytest -v --timeout 300 --
   tests/test_gpu_fp6.py || exit $?
 tools/gpu_step.sh 200 $out/abandon_timing.txt python tools/fp6_abandon_timing.py || exit $?
 tools/gpu_step.sh 200 $out/bench_ldb.log python bench.py --data ldblocks --no-cpu-baseline || exit $?
+for d in 3 4 6; do
+  tools/gpu_step.sh 200 $out/shard8_depth$d.log python bench.py --rehearse-dist --rehearse-shard 8 --pipe-depth $d --no-cpu-baseline || exit $?
+done
 echo done
