@@ -385,6 +385,10 @@ def main():
         if args.tile_rows:
             c.set_option("tile_order", 1)
         c.set_option("ref_sums", 0 if args.exact_sums else 1)
+        # WLD_BENCH_OPTS="name=v;name=v": library options for A/B lines (never the headline's)
+        for kv in filter(None, os.environ.get("WLD_BENCH_OPTS", "").split(";")):
+            k, v = kv.split("=")
+            c.set_option(k.strip(), int(v))
         c.load_device(d_buf.data_ptr(), L, N, d_w.data_ptr())
         return c
 
@@ -721,6 +725,7 @@ def main():
             "Henikoff, every 10th x 2^-8 (--wide-weights)" if args.wide_weights else "Henikoff"),
         "config": {"workload": desc, "n_seqs": N, "n_sites": L, "r2_threshold": thr, "pairs": total_pairs,
                    "rows_passing": rows, "kernel": kern_name, "mfma_planes": planes,
+                   "library_options": os.environ.get("WLD_BENCH_OPTS") or "defaults",
                    "launch": ("bench.py spawned %d ranks" % world if os.environ.get("WLD_BENCH_SPAWNED") else
                               "external launcher (WORLD_SIZE=%d)" % world if "WORLD_SIZE" in os.environ else
                               "single process"),

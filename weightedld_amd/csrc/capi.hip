@@ -618,7 +618,8 @@ double ref_extra_residual(const wld_ctx *c) {
 // With scan given, a screen fuses the run's chunk scan into its last
 // workgroup or the candidate launch's (then the caller launches no scan).
 int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *dense, bool *screened = nullptr,
-                 const ScanArgs *scan = nullptr) {
+                 const ScanArgs *scan = nullptr, bool *scan_fused = nullptr) {
+    bool fused = false;  // the run's chunk scan ran inside a launch (the caller launches none)
     const uint32_t n = chunk_rows_of(c->L);
     bool sc = false;
     c->fp6_pass = false;
@@ -636,8 +637,10 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
     // every tile on the reference-order f32 kernel
     const bool ref_screen = c->opt_ref_sums && c->kernel == WLD_KERNEL_MFMA && !dense && c->use_frag &&
                             c->opt_prefilter && thr > 0.0f && c->opt_screen != 0;
+    // (a full run on the item kernel fuses the scan into its last workgroup)
+    if (scan && !dense) rv.scan = *scan;
     if (c->opt_ref_sums && !ref_screen) {
-        launch_pair_valu(rv, o, dense, c->stream);
+        fused = launch_pair_valu(rv, o, dense, c->stream);
     } else if (c->kernel == WLD_KERNEL_MFMA) {
         MfmaLaunch m{};
         m.codes = ptr<uint8_t>(c->codes);
@@ -705,9 +708,10 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
             }
         }
         if (ref_screen && !m.screen && !m.ref_rows) {
-            launch_pair_valu(rv, o, nullptr, c->stream);  // the policy sends this threshold to the full kernel
+            fused = launch_pair_valu(rv, o, nullptr, c->stream);  // the policy sends this threshold to the full kernel
         } else {
             sc = launch_pair_mfma(m, o, dense, c->stream, c->ev[6]);
+            fused = sc && scan && !dense;  // (a screen's candidate launch, or the candidate pairs' compaction)
             c->fp6_pass = sc && m.fp6 && !m.screen2 && !m.ref_rows;  // (launch_pair_mfma's one-plane screen branch)
         }
     } else {
@@ -718,6 +722,7 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
     }
     HIP_TRY(hipGetLastError());
     if (screened) *screened = sc;
+    if (scan_fused) *scan_fused = fused;
     return WLD_OK;
 }
 
@@ -1127,10 +1132,12 @@ int enqueue_pass(wld_ctx *c) {
     // chunks (C4: 3,160, ~10 us in one 256-thread workgroup); a larger range
     // (C5: 19,306 chunks, ~70 us fused) gets the 1024-thread scan kernel
     const bool fuse_scan = c->opt_fused_scan && lin_count && lin_count <= 4096;
-    if (c->n_tiles) WLD_TRY(launch_pairs(c, r.thr, o, nullptr, &c->screened, fuse_scan ? &sa : nullptr));
+    bool scan_fused = false;
+    if (c->n_tiles)
+        WLD_TRY(launch_pairs(c, r.thr, o, nullptr, &c->screened, fuse_scan ? &sa : nullptr, &scan_fused));
     if (lin_count) c->cand_set ^= 1;  // this pass's scan (fused or below) zeroes the other set
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
-    if (lin_count && !(c->screened && fuse_scan)) {  // else the candidate launch's last workgroup ran it
+    if (lin_count && !scan_fused) {  // else the last workgroup of the pair launch ran it
         sa.ticket = nullptr;
         launch_chunk_scan(sa, c->stream);
         HIP_TRY(hipGetLastError());

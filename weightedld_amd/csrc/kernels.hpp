@@ -151,7 +151,9 @@ struct ValuLaunch {
     // tiles (pair_mfma.hip ScreenArgs::rb_items), counted by the buckets
     bool rb_items;
 };
-void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
+// returns true when the run's chunk scan ran in the launch (v.scan given, the
+// item kernel of a full run); else the caller launches it
+bool launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *dense, hipStream_t s);
 // The candidate pairs a kModeRefPairs launch (pair_mfma.hip) staged: summed in
 // lib.rs's order one pair per thread from the lane-class layout
 // (ref_sums_kernel), then per tile slice the passing rows kept in place (in

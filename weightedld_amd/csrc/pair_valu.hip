@@ -846,6 +846,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
         // only pairs a > b: not computed (their waves idle to the epilogue)
         const uint32_t cols = (tile >> 16) == (tile & 0xFFFFu) ? 0xFu & ~((1u << q) - 1u) : 0xFu;
         if (tile != kNoTile) compute_item(tile, cols << (4 * q), 1u << q);  // kNoTile: padding of an XCD-ordered list
+        scan_tail(sa, gridDim.x);  // (every workgroup takes a ticket when the scan is fused)
     } else {
         // the screen's items, heaviest bucket first; the first by workgroup id
         // (rounds dealt in snake order, heavy beside light on a CU), the next
@@ -1094,12 +1095,12 @@ void launch_v(const ValuLaunch &v, uint32_t grid, uint32_t flush, uint32_t cs, c
 }
 }  // namespace
 
-void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
+bool launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *dense, hipStream_t s) {
     const DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
     const uint32_t flush = (uint32_t)std::max(1.0, std::floor(std::sqrt((double)v.NP) / 64.0 + 0.5));
     const uint32_t grid = v.tile_count ? std::min<uint32_t>(v.n_tiles, v.ref ? kRefCandidateGrid : kCandidateGrid)
                                        : v.n_tiles;
-    if (grid == 0) return;
+    if (grid == 0) return false;
     if (v.ref) {
         // the reference's f32 order: f32-input MFMA for finite weights, the
         // select loop otherwise (both sequential fmaf/add chains per block)
@@ -1125,13 +1126,16 @@ void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
             if (v.safe) launch_v<false, true, false, true, false>(v, grid, flush, cs, o, dn, s);
             else if (WLD_REF_ITEMS && !WLD_REF_ITEM_KERNEL && v.n_tiles <= 4 * kRefCandidateGrid)
                 launch_v<false, false, true, true, false, 1>(v, grid, flush, cs, o, dn, s, 4);
-            else if (WLD_REF_ITEMS && v.n_tiles <= 4 * kRefCandidateGrid)
+            else if (WLD_REF_ITEMS && v.n_tiles <= 4 * kRefCandidateGrid) {
+                // (the run's chunk scan in the last workgroup when given)
                 hipLaunchKernelGGL(ref_item_kernel<false>, dim3(4 * grid), dim3(256), 0, s, v.codes, v.w, v.site_ok,
                                    v.tiles, v.n_tiles, nullptr, nullptr, nullptr, 0u, v.L, v.NP, cs, v.ref_tail_n,
-                                   v.n_chunk_rows, v.thr, o, ScanArgs{});
+                                   v.n_chunk_rows, v.thr, o, v.scan);
+                return v.scan.ticket != nullptr;
+            }
             else launch_v<false, false, true, true, false>(v, grid, flush, cs, o, dn, s);
         }
-        return;
+        return false;
     }
     // finite weights: products and sums on the matrix cores (plain, option
     // WLD_OPT_VALU_PLAIN: the VALU loop, for A/B); non-finite weights keep the
@@ -1145,6 +1149,7 @@ void launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
         else if (v.plain) launch_v<false, false, false, false, false>(v, grid, flush, 1, o, dn, s);
         else launch_v<false, false, true, false, false>(v, grid, flush, 1, o, dn, s);
     }
+    return false;
 }
 
 }  // namespace wld
