@@ -718,18 +718,19 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
 #endif
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const uint32_t xa = A[grp] >> (8 * e), xb = B[grp] >> (8 * e);
 #if WLD_ITEM_CVT && !defined(WLD_DIAG_NOSEL)
                         // w x 1.0 or w x 0.0: exact; a -0.0 term (negative w
                         // masked) adds nothing to a chain that starts at +0.0
                         const float u = we[e] * cvt_ubyte<0>(ai, e), v = we[e] * cvt_ubyte<0>(am, e);
                         const float fi = cvt_ubyte<1>(bi, e), fm = cvt_ubyte<1>(bm, e);
-                        (void)xa, (void)xb;
-#elif !defined(WLD_DIAG_NOSEL)
+#else
+                        const uint32_t xa = A[grp] >> (8 * e), xb = B[grp] >> (8 * e);
+#ifndef WLD_DIAG_NOSEL
                         const float u = (xa & kCodeIn) ? we[e] : 0.0f, v = (xa & kCodeMaj) ? we[e] : 0.0f;
                         const float fi = (float)(xb & 1u), fm = (float)((xb >> 1) & 1u);
 #else  // diagnostic (wrong sums): the operands without their selects and converts
                         const float u = we[e], v = __uint_as_float(xa), fi = __uint_as_float(xb), fm = we[e];
+#endif
 #endif
                         acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fi, acc[0], 0, 0, 0);
                         acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fi, acc[1], 0, 0, 0);
