@@ -838,13 +838,9 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
 // wave LDS-DMAs its row block's A (3 KB) and its column block's B (1 KB)
 // into a double-buffered 16 KB stage; wave w computes a rows 16w.. against
 // the four column blocks (16 MFMAs per stage), then the screen epilogue.
-// WLD_FP6_BMIN (A/B builds): the B copy also holds the minor-bit plane (1 KB
-// after each 1 KB raw block), so no wave masks it (16 VALU per stage, repeated
-// by all four waves); 20 KB stages fit three workgroups per CU
-#ifndef WLD_FP6_BMIN
-#define WLD_FP6_BMIN 0
-#endif
-constexpr int kF6ABytes = 3072, kF6BBytes = WLD_FP6_BMIN ? 2048 : 1024, kF6Stage = 4 * kF6ABytes + 4 * kF6BBytes;
+constexpr int kF6ABytes = 3072, kF6BBytes = 1024;
+constexpr int kF6AStage = 4 * kF6ABytes;  // A bytes in an LDS stage
+constexpr int kF6Stage = kF6AStage + 4 * kF6BBytes;
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 
@@ -881,11 +877,7 @@ __global__ __launch_bounds__(256) void frag6_kernel(const uint8_t *__restrict__ 
     uint32_t *pm = pa + 1536 / 4;
     for (int d = 0; d < 6; ++d) pa[d] = ai[d], pm[d] = am[d];
     *reinterpret_cast<uint4 *>(b4 + (g16 * NK + kb) * (size_t)kF6BBytes + lane * 16) = make_uint4(b[0], b[1], b[2], b[3]);
-#if WLD_FP6_BMIN
-    constexpr uint32_t kMin = 0x22222222u;  // fp4 1.0 (minor) nibbles
-    *reinterpret_cast<uint4 *>(b4 + (g16 * NK + kb) * (size_t)kF6BBytes + 1024 + lane * 16) =
-        make_uint4(b[0] & kMin, b[1] & kMin, b[2] & kMin, b[3] & kMin);
-#endif
+
 }
 
 // the wave's 16 a rows x 64 b columns as f32 sums of fp6 x fp4 products:
@@ -935,10 +927,7 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
         glds16_s(a, lane16, gb + wave * kF6ABytes);
         glds16_s(a + 1024, lane16, gb + wave * kF6ABytes + 1024);
         glds16_s(a + 2048, lane16, gb + wave * kF6ABytes + 2048);
-        glds16_s(sB + (size_t)kb * kF6BBytes, lane16, gb + 4 * kF6ABytes + wave * kF6BBytes);
-#if WLD_FP6_BMIN
-        glds16_s(sB + (size_t)kb * kF6BBytes + 1024, lane16, gb + 4 * kF6ABytes + wave * kF6BBytes + 1024);
-#endif
+        glds16_s(sB + (size_t)kb * kF6BBytes, lane16, gb + kF6AStage + wave * kF6BBytes);
     };
     issue(0, 0);
     // the give-up test: read by thread 0 while the first stage is in flight,
@@ -962,39 +951,15 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
         for (int x = 0; x < 2; ++x)
 #pragma unroll
             for (int y = 0; y < 2; ++y) acc.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-    uint32_t buf = 0;
-    for (uint32_t kb = 0; kb < NK; ++kb) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this stage landed
-        __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
-        asm volatile("" ::: "memory");
-        if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
-            if (tid == 0 && sBail == 1) {
-                atomicOr(sc.cand_count, kAbandonBit);
-                atomicOr(sc.cand_buckets, kAbandonBit);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            return;
-        }
-        if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
+    // a stage's 16 MFMAs: A (in, major) against the four B blocks of LDS buffer buf
+    auto stage_mfma = [&](uint32_t buf, const v8i &ai, const v8i &am) {
         const uint8_t *g = smem + buf * kF6Stage;
-        const uint8_t *pa = g + wave * kF6ABytes + lane * 24;
-        const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
-                    i2 = *reinterpret_cast<const uint2 *>(pa + 16);
-        const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536), m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
-                    m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
-        const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
-        const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
-            const uint4 r = *reinterpret_cast<const uint4 *>(g + 4 * kF6ABytes + n * kF6BBytes + lane * 16);
-            const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
-#if WLD_FP6_BMIN
-            const uint4 rm = *reinterpret_cast<const uint4 *>(g + 4 * kF6ABytes + n * kF6BBytes + 1024 + lane * 16);
-            const v8i bmin = {(int)rm.x, (int)rm.y, (int)rm.z, (int)rm.w, 0, 0, 0, 0};
-#else
+            const uint4 r = *reinterpret_cast<const uint4 *>(g + kF6AStage + n * kF6BBytes + lane * 16);
             constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
+            const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
             const v8i bmin = {(int)r.x & kMinor, (int)r.y & kMinor, (int)r.z & kMinor, (int)r.w & kMinor, 0, 0, 0, 0};
-#endif
             acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, braw, acc.v[n][0][0], 2, 4, 0,
                                                                               0x7F7F7F7F, 0, 0x7F7F7F7F);
             acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc.v[n][0][1], 2, 4, 0,
@@ -1005,6 +970,35 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
                                                                               0x7F7F7F7F, 0, 0x7F7F7F7F);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
+    };
+    // the top of a stage: this wave's copies (and register loads) of it landed,
+    // then every other wave's (the barrier); false: the pass is given up
+    auto stage_top = [&](uint32_t kb) -> bool {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // the buffer read last stage is free from here
+        asm volatile("" ::: "memory");
+        if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
+            if (tid == 0 && sBail == 1) {
+                atomicOr(sc.cand_count, kAbandonBit);
+                atomicOr(sc.cand_buckets, kAbandonBit);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            return false;
+        }
+        return true;
+    };
+    uint32_t buf = 0;
+    for (uint32_t kb = 0; kb < NK; ++kb) {
+        if (!stage_top(kb)) return;
+        if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
+        const uint8_t *pa = smem + buf * kF6Stage + wave * kF6ABytes + lane * 24;
+        const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
+                    i2 = *reinterpret_cast<const uint2 *>(pa + 16);
+        const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536), m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
+                    m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
+        const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
+        const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
+        stage_mfma(buf, ai, am);
         buf ^= 1;
     }
     // (the f64 fallback of pair_cand: exact sums from X, Y; the launch uses
