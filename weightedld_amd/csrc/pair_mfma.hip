@@ -427,6 +427,65 @@ __device__ __forceinline__ bool pair_eval(double T, double SA, double SB, double
     return valid && r2 > thr;
 }
 
+// The screen's verdict on one tile, by its 256 threads (tid: the thread's
+// index in the tile's group): bits = the 16x16 sub-blocks that may hold a
+// passing pair (nonzero: a candidate, listed; zero: rejected, finished here)
+__device__ __forceinline__ void screen_verdict(uint32_t bits, uint32_t ta, uint32_t tb, uint32_t tid,
+                                               uint32_t n_chunk_rows, const OrderArgs &o, const ScreenArgs &sc) {
+    const uint32_t a0 = ta * kTile;
+    if (bits) {
+    if (tid == 0) {
+        const uint32_t nb = (uint32_t)__popc(bits);  // nb >= 1
+        atomicAdd(sc.cand_count, 1u);
+        atomicAdd(sc.cand_count + 1, nb);  // sub-blocks to compute (stats)
+        // (a list entry: a slot of its bucket; none once the pass is
+        // given up, whose mark sits in bucket 0's count)
+        auto slot = [&](uint32_t bucket) -> uint32_t {
+            const uint32_t k = atomicAdd(&sc.cand_buckets[bucket], 1u);
+            return (k & kAbandonBit) || k >= sc.cand_cap ? ~0u : bucket * sc.cand_cap + k;
+        };
+        if (!sc.rb_items) {
+            const uint32_t e = slot(16u - nb);
+            if (e != ~0u) {
+                sc.cand_list[e] = (ta << 16) | tb;
+                sc.cand_bits[e] = bits;
+            }
+        } else {
+            // the tile's 16-row blocks in order, packed greedily into
+            // items of at most four computed sub-blocks (one per wave)
+            uint32_t empty = 0, cur = 0, cur_k = 0;
+            auto emit = [&]() {
+                const uint32_t e = slot(4u - cur_k);
+                if (e != ~0u) {
+                    sc.cand_list[e] = (ta << 16) | tb;
+                    sc.cand_bits[e] = cur;
+                }
+            };
+            for (uint32_t q = 0; q < 4; ++q) {
+                const uint32_t rb = (bits >> (4 * q)) & 0xFu, k = (uint32_t)__popc(rb);
+                if (!k) {
+                    ++empty;
+                    continue;
+                }
+                if (cur_k + k > 4) {
+                    emit();
+                    cur = cur_k = 0;
+                }
+                cur |= rb << (4 * q);
+                cur_k += k;
+            }
+            if (cur_k) emit();
+            if (empty) tile_done(o, ta, tb, n_chunk_rows, empty);  // (quarters: no candidate there)
+        }
+    }
+    if (sc.rb_items && tid < kTile && !((bits >> (4 * (tid >> 4))) & 0xFu))
+        o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;  // a row block without a candidate: no rows
+    } else {
+        if (tid < kTile) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
+        if (tid == 0) tile_done(o, ta, tb, n_chunk_rows);  // rejected: finished here
+    }
+}
+
 // Epilogue of one 64x64 tile.  The lane holds 16 (a, b) pairs (Acc::a_local,
 // b_local).  kModeDense writes every pair's stats (tests); kModeAll and
 // kModePrefilter compact passing pairs through the tile's 64x64 pass-bit
@@ -504,56 +563,9 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
                 if (pair_cand(i)) m |= 1u << sub_block<Acc>(i, wave, lane);
             if (m) atomicOr(sMask, (unsigned long long)m);
             __syncthreads();
-            const uint32_t bits = (uint32_t)*sMask;
-            if (tid == 0) {
-                const uint32_t nb = (uint32_t)__popc(bits);  // nb >= 1
-                atomicAdd(sc.cand_count, 1u);
-                atomicAdd(sc.cand_count + 1, nb);  // sub-blocks to compute (stats)
-                // (a list entry: a slot of its bucket; none once the pass is
-                // given up, whose mark sits in bucket 0's count)
-                auto slot = [&](uint32_t bucket) -> uint32_t {
-                    const uint32_t k = atomicAdd(&sc.cand_buckets[bucket], 1u);
-                    return (k & kAbandonBit) || k >= sc.cand_cap ? ~0u : bucket * sc.cand_cap + k;
-                };
-                if (!sc.rb_items) {
-                    const uint32_t e = slot(16u - nb);
-                    if (e != ~0u) {
-                        sc.cand_list[e] = (ta << 16) | tb;
-                        sc.cand_bits[e] = bits;
-                    }
-                } else {
-                    // the tile's 16-row blocks in order, packed greedily into
-                    // items of at most four computed sub-blocks (one per wave)
-                    uint32_t empty = 0, cur = 0, cur_k = 0;
-                    auto emit = [&]() {
-                        const uint32_t e = slot(4u - cur_k);
-                        if (e != ~0u) {
-                            sc.cand_list[e] = (ta << 16) | tb;
-                            sc.cand_bits[e] = cur;
-                        }
-                    };
-                    for (uint32_t q = 0; q < 4; ++q) {
-                        const uint32_t rb = (bits >> (4 * q)) & 0xFu, k = (uint32_t)__popc(rb);
-                        if (!k) {
-                            ++empty;
-                            continue;
-                        }
-                        if (cur_k + k > 4) {
-                            emit();
-                            cur = cur_k = 0;
-                        }
-                        cur |= rb << (4 * q);
-                        cur_k += k;
-                    }
-                    if (cur_k) emit();
-                    if (empty) tile_done(o, ta, tb, n_chunk_rows, empty);  // (quarters: no candidate there)
-                }
-            }
-            if (sc.rb_items && tid < kTile && !((bits >> (4 * (tid >> 4))) & 0xFu))
-                o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;  // a row block without a candidate: no rows
+            screen_verdict((uint32_t)*sMask, ta, tb, tid, n_chunk_rows, o, sc);
         } else {
-            if (tid < kTile) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
-            if (tid == 0) tile_done(o, ta, tb, n_chunk_rows);  // rejected: finished here
+            screen_verdict(0u, ta, tb, tid, n_chunk_rows, o, sc);
         }
         return;
     }
@@ -1012,6 +1024,158 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
                                       sRowBase);
 }
 
+// The fp6 screen on two tiles of one tile row per workgroup: (ta, tb0) and
+// (ta, tb1) (tb1 = tb0 + 1; a lone tile: the second entry kNoTile).  Eight
+// waves share one A copy per stage: waves 0-3 copy A's four row blocks
+// (3 KB each), waves 4-7 B's column blocks of both tiles (1 KB each); half h
+// = wave / 4 computes tile h exactly as pair_fp6_screen_kernel's waves do.
+// A stage is 12 + 8 KB for 8192 pairs instead of 16 KB for 4096: the L2 ->
+// CU bytes per pair 4 -> 2.5 (the one-tile kernel moved ~52% of the L2's
+// bandwidth at C4, and more bytes per stage cost time there, Appendix A).
+constexpr int kF6Stage2 = kF6AStage + 8 * kF6BBytes;
+__global__ __launch_bounds__(512, 2) void pair_fp6_screen2_kernel(const uint8_t *__restrict__ a6,
+                                                                  const uint8_t *__restrict__ b4,
+                                                                  const uint64_t *__restrict__ ok_bits,
+                                                                  const uint32_t *__restrict__ tile_pairs,
+                                                                  uint32_t n_pairs, uint32_t NK, uint32_t L,
+                                                                  uint32_t n_chunk_rows, float thr, OrderArgs o,
+                                                                  ScreenArgs sc) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6Stage2];
+    __shared__ unsigned long long sMask[2];
+    __shared__ uint32_t sBail, sAny[2];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t h = wave >> 2, w4 = wave & 3, lt = tid & 255;  // tile half, wave and thread in it
+    const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
+    // (kNoTile: padding of an XCD-ordered list, or past the end of the grid)
+    const uint32_t t0 = blockIdx.x < n_pairs ? tile_pairs[2 * blockIdx.x] : kNoTile;
+    if (t0 == kNoTile) return;  // (uniform: the whole workgroup)
+    const uint32_t t1 = tile_pairs[2 * blockIdx.x + 1];
+    const bool two = t1 != kNoTile, live = h == 0 || two;  // (a lone tile's half 1 computes tile 0's B, unused)
+    const uint32_t ta = t0 >> 16, tb0 = t0 & 0xFFFFu, tb1 = two ? t1 & 0xFFFFu : tb0, tb = h ? tb1 : tb0;
+    // this wave's DMA sources: A of row block 4 ta + w4 (half 0) or B of
+    // column block w4 of both tiles (half 1)
+    const uint8_t *sA = a6 + (size_t)(4 * ta + w4) * NK * kF6ABytes;
+    const uint8_t *sB0 = b4 + (size_t)(4 * tb0 + w4) * NK * kF6BBytes;
+    const uint8_t *sB1 = b4 + (size_t)(4 * tb1 + w4) * NK * kF6BBytes;
+    auto issue = [&](uint32_t kb, uint32_t buf) {
+        const uint32_t gb = lds + buf * kF6Stage2;
+        if (h == 0) {
+            const uint8_t *a = sA + (size_t)kb * kF6ABytes;
+            glds16_s(a, lane16, gb + w4 * kF6ABytes);
+            glds16_s(a + 1024, lane16, gb + w4 * kF6ABytes + 1024);
+            glds16_s(a + 2048, lane16, gb + w4 * kF6ABytes + 2048);
+        } else {
+            glds16_s(sB0 + (size_t)kb * kF6BBytes, lane16, gb + kF6AStage + w4 * kF6BBytes);
+            glds16_s(sB1 + (size_t)kb * kF6BBytes, lane16, gb + kF6AStage + 4 * kF6BBytes + w4 * kF6BBytes);
+        }
+    };
+    issue(0, 0);
+    // the give-up test as in pair_fp6_screen_kernel; the verdict words
+    // zeroed (all published by the first stage barrier)
+    if (tid == 0) {
+        uint32_t v = 0;
+        if (sc.bail) {
+            const unsigned cc = __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v = cc > sc.bail ? ((cc & kAbandonBit) ? 2u : 1u) : 0u;
+        }
+        sBail = v;
+    }
+    if (tid < 2) {
+        sMask[tid] = 0ull;
+        sAny[tid] = 0u;
+    }
+    const uint64_t okA = ok_bits[ta], okB = live ? ok_bits[tb] : 0ull;
+    AccF6 acc;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) acc.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+    uint32_t buf = 0;
+    for (uint32_t kb = 0; kb < NK; ++kb) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this stage landed
+        __builtin_amdgcn_s_barrier();  // ... and every other wave's; the buffer read last stage is free
+        asm volatile("" ::: "memory");
+        if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
+            if (tid == 0 && sBail == 1) {
+                atomicOr(sc.cand_count, kAbandonBit);
+                atomicOr(sc.cand_buckets, kAbandonBit);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            return;
+        }
+        if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
+        const uint8_t *g = smem + buf * kF6Stage2;
+        const uint8_t *pa = g + w4 * kF6ABytes + lane * 24;
+        const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
+                    i2 = *reinterpret_cast<const uint2 *>(pa + 16);
+        const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536), m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
+                    m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
+        const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
+        const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const uint4 r = *reinterpret_cast<const uint4 *>(g + kF6AStage + (4 * h + n) * kF6BBytes + lane * 16);
+            constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
+            const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
+            const v8i bmin = {(int)r.x & kMinor, (int)r.y & kMinor, (int)r.z & kMinor, (int)r.w & kMinor, 0, 0, 0, 0};
+            acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, braw, acc.v[n][0][0], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+            acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc.v[n][0][1], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+            acc.v[n][1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, braw, acc.v[n][1][0], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+            acc.v[n][1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, bmin, acc.v[n][1][1], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
+        buf ^= 1;
+    }
+    // the screen epilogue of tile_epilogue (kModeScreen, f32 == 2) per half:
+    // a pair may pass unless the f32 bound rejects it; the halves' verdicts
+    // meet in LDS with barriers both halves pass
+    const uint32_t a0 = ta * kTile, b0 = tb * kTile;
+    const float thr_c = thr * (1.0f - 0x1p-7f), R2 = 2.0f * sc.Rf;
+    auto margin = [&](int i) {
+        const auto p0 = acc.raw(0, i), p1 = acc.raw(1, i);  // (X, Y) of channel_a in, major
+        float t2;
+        const float t1 =
+            r2_screen_terms_xy((float)p0.x, (float)p0.y, (float)p1.x, (float)p1.y, R2, thr_c, sc.E, sc.mloc, t2);
+        return max(__float_as_int(t1), __float_as_int(t2));
+    };
+    auto pair_cand = [&](int i) -> bool {
+        const uint32_t a_local = AccF6::a_local(i, w4, lane), b_local = AccF6::b_local(i, w4, lane);
+        return ((okB >> b_local) & 1) && a0 + a_local < b0 + b_local && ((okA >> a_local) & 1) && margin(i) > 0;
+    };
+    bool cand = false;
+    if (okA == ~0ull && okB == ~0ull && ta != tb) {
+        int worst = -1;
+#pragma unroll
+        for (int i = 0; i < AccF6::kPairs; ++i) worst = max(worst, margin(i));
+        cand = worst > 0;
+    } else {
+#pragma unroll
+        for (int i = 0; i < AccF6::kPairs; ++i)
+            if (!cand) cand = pair_cand(i);
+    }
+    if (__ballot(cand) != 0 && lane == 0) sAny[h] = 1u;
+    __syncthreads();
+    const uint32_t any0 = sAny[0], any1 = sAny[1];
+    if (any0 | any1) {  // (uniform)
+        if (h ? any1 : any0) {
+            unsigned m = 0;
+#pragma unroll
+            for (int i = 0; i < AccF6::kPairs; ++i)
+                if (pair_cand(i)) m |= 1u << sub_block<AccF6>(i, w4, lane);
+            if (m) atomicOr(&sMask[h], (unsigned long long)m);
+        }
+        __syncthreads();
+    }
+    if (live) screen_verdict((uint32_t)sMask[h], ta, tb, lt, n_chunk_rows, o, sc);
+}
+
 void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b4,
                   hipStream_t s) {
     const size_t n = LP / 16 * ((NP + 127) / 128) * 64;
@@ -1249,9 +1413,13 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
         sc.f32 = 2;
         sc.bail = m.fp6_bail;
         screen_consts(m.fp6->Tg, 2.0f * sc.Rf, sc.E, sc.mloc);
-        // (one tile per workgroup, the XCD-ordered list)
-        hipLaunchKernelGGL(pair_fp6_screen_kernel, dim3(m.n_tiles), dim3(256), 0, s, m.fp6->a6, m.fp6->b4, ok_bits,
-                           m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
+        if (m.tile_pairs)  // (two tiles of a row per workgroup, the XCD-ordered entries)
+            hipLaunchKernelGGL(pair_fp6_screen2_kernel, dim3(std::max<uint32_t>(m.n_tile_pairs, 1)), dim3(512), 0, s,
+                               m.fp6->a6, m.fp6->b4, ok_bits, m.tile_pairs, m.n_tile_pairs, m.fp6->NK, m.L,
+                               m.n_chunk_rows, m.thr, o, sc);
+        else  // (one tile per workgroup, the XCD-ordered list)
+            hipLaunchKernelGGL(pair_fp6_screen_kernel, dim3(m.n_tiles), dim3(256), 0, s, m.fp6->a6, m.fp6->b4, ok_bits,
+                               m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
         if (screen_done) (void)hipEventRecord(screen_done, s);
         launch_candidates(m, n, idx, ok_bits, o, dn, sc, s);
         return true;
