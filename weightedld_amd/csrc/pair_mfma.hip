@@ -913,6 +913,19 @@ struct AccF6 {
 #ifndef WLD_FP6_WG
 #define WLD_FP6_WG 4  // workgroups per CU
 #endif
+// A/B: the first round's workgroups of a CU start this many cycles apart
+// (by workgroup slot), so the four do not run their epilogues in lockstep
+#ifndef WLD_FP6_PIPE
+#define WLD_FP6_PIPE 0
+#endif
+#ifndef WLD_FP6_STAGGER
+#define WLD_FP6_STAGGER 0
+#endif
+// diagnostic builds (wrong results, timing only): 1 no epilogue, 2 also every
+// stage's copy from the first stage, 3 also no MFMA
+#ifndef WLD_FP6_DIAG
+#define WLD_FP6_DIAG 0
+#endif
 __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const uint8_t *__restrict__ a6,
                                                                   const uint8_t *__restrict__ b4,
                                                                   const uint64_t *__restrict__ ok_bits,
@@ -929,12 +942,18 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     // (kNoTile: padding of an XCD-ordered list, or past the end of the grid)
     const uint32_t tile = blockIdx.x < n_tiles ? tiles[blockIdx.x] : kNoTile;
     if (tile == kNoTile) return;  // (uniform: the whole workgroup)
+    if (WLD_FP6_STAGGER && blockIdx.x < 1024) {
+        uint32_t slot;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID, 16, 4)" : "=s"(slot));
+        for (uint32_t k = (slot & 3) * (WLD_FP6_STAGGER / 8128); k; --k) __builtin_amdgcn_s_sleep(127);
+    }
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
     // this wave's DMA sources: A of row block 4 ta + wave, B of column block 4 tb + wave
     const uint8_t *sA = a6 + (size_t)(4 * ta + wave) * NK * kF6ABytes;
     const uint8_t *sB = b4 + (size_t)(4 * tb + wave) * NK * kF6BBytes;
     auto issue = [&](uint32_t kb, uint32_t buf) {
         const uint32_t gb = lds + buf * kF6Stage;
+        if (WLD_FP6_DIAG >= 2) kb = 0;  // (diagnostic: every stage from the first, cache-resident)
         const uint8_t *a = sA + (size_t)kb * kF6ABytes;
         glds16_s(a, lane16, gb + wave * kF6ABytes);
         glds16_s(a + 1024, lane16, gb + wave * kF6ABytes + 1024);
@@ -972,6 +991,10 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
             constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
             const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
             const v8i bmin = {(int)r.x & kMinor, (int)r.y & kMinor, (int)r.z & kMinor, (int)r.w & kMinor, 0, 0, 0, 0};
+            if (WLD_FP6_DIAG == 3) {  // (diagnostic: no MFMA, the operands consumed)
+                acc.v[n][0][0][0] += (float)(ai[0] ^ am[5] ^ braw[n] ^ bmin[3]);
+                continue;
+            }
             acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, braw, acc.v[n][0][0], 2, 4, 0,
                                                                               0x7F7F7F7F, 0, 0x7F7F7F7F);
             acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc.v[n][0][1], 2, 4, 0,
@@ -1020,8 +1043,205 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
         return ((double)p.x + (y ? -(double)p.y : (double)p.y)) * 0.5;
     };
     const DenseArgs dn{nullptr, nullptr, nullptr, nullptr};
+    if (WLD_FP6_DIAG) {  // (diagnostic: no epilogue; the sums kept live, the tile rejected)
+        float t = 0.0f;
+#pragma unroll
+        for (int i = 0; i < AccF6::kPairs; ++i) t += acc.raw(0, i).x + acc.raw(1, i).y;
+        if (t == -1.0f) sBits[0] = 1;
+        screen_verdict(0u, ta, tb, tid, n_chunk_rows, o, sc);
+        return;
+    }
     tile_epilogue<kModeScreen, AccF6>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, 0, o, dn, sc, sBits,
                                       sRowBase);
+}
+
+// The fp6 screen with the epilogue in the MFMA shadow (WLD_FP6_PIPE): a
+// persistent workgroup takes list entries blockIdx.x, + gridDim.x, ... (the
+// same XCD queue) and evaluates tile j - 1's pairs while it accumulates tile
+// j: stage s of every eight runs the bound on pairs 2 (s mod 8) and + 1 of
+// the previous tile's sums (kept in a second accumulator set) between the
+// stage's MFMAs, and the copies run on across tiles (tile j + 1's first
+// stage behind tile j's last).  The one-tile kernel runs its epilogue after
+// its MFMAs, in lockstep with the other workgroups of its CU, and that phase
+// cost ~40% of its time at C4 (profiles/r04p: 0.77 -> 0.45 ms without it).
+constexpr uint32_t kF6PipeWgPerCu = 2, kF6PipeGrid = 256 * kF6PipeWgPerCu;
+__global__ __launch_bounds__(256, kF6PipeWgPerCu) void pair_fp6_pipe_kernel(const uint8_t *__restrict__ a6,
+                                                                            const uint8_t *__restrict__ b4,
+                                                                            const uint64_t *__restrict__ ok_bits,
+                                                                            const uint32_t *__restrict__ tiles,
+                                                                            uint32_t n_tiles, uint32_t NK, uint32_t L,
+                                                                            uint32_t n_chunk_rows, float thr,
+                                                                            OrderArgs o, ScreenArgs sc) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6Stage];
+    __shared__ unsigned long long sMask[2];
+    __shared__ uint32_t sBail;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
+    const uint32_t G = gridDim.x;
+    // (kNoTile: padding at the end of an XCD queue; nothing follows it there)
+    auto tile_at = [&](uint32_t j) -> uint32_t {
+        const uint32_t e = blockIdx.x + j * G;
+        return e < n_tiles ? tiles[e] : kNoTile;
+    };
+    uint32_t cur = tile_at(0);
+    if (cur == kNoTile) return;  // (uniform)
+    auto issue = [&](uint32_t tile, uint32_t kb, uint32_t buf) {
+        const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
+        const uint8_t *a = a6 + ((size_t)(4 * ta + wave) * NK + kb) * kF6ABytes;
+        const uint8_t *b = b4 + ((size_t)(4 * tb + wave) * NK + kb) * kF6BBytes;
+        const uint32_t gb = lds + buf * kF6Stage;
+        glds16_s(a, lane16, gb + wave * kF6ABytes);
+        glds16_s(a + 1024, lane16, gb + wave * kF6ABytes + 1024);
+        glds16_s(a + 2048, lane16, gb + wave * kF6ABytes + 2048);
+        glds16_s(b, lane16, gb + kF6AStage + wave * kF6BBytes);
+    };
+    if (tid == 0) sMask[0] = sMask[1] = 0ull;  // (published by the first stage barrier)
+    issue(cur, 0, 0);
+    const float thr_c = thr * (1.0f - 0x1p-7f), R2 = 2.0f * sc.Rf;
+    // the previous tile: its position and site flags (its sums: the other set)
+    uint32_t p_a0 = 0, p_b0 = 0, j = 0, buf = 0;
+    uint64_t p_okA = 0, p_okB = 0;
+    bool has_prev = false;
+    unsigned m = 0;  // this lane's sub-blocks of the previous tile holding a pair that may pass
+    // pairs 2p, 2p + 1 of the previous tile (tile_epilogue's kModeScreen test, f32 == 2)
+    // (kb: the sums pass through an empty asm that depends on the stage, so
+    // the bound is computed in the stage, between its MFMAs, not hoisted)
+    auto part = [&](const AccF6 &prev, int p, uint32_t kb) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int i = 2 * p + q;
+            const uint32_t al = AccF6::a_local(i, wave, lane), bl = AccF6::b_local(i, wave, lane);
+            auto p0 = prev.raw(0, i), p1 = prev.raw(1, i);
+            asm("" : "+v"(p0.x), "+v"(p0.y), "+v"(p1.x), "+v"(p1.y) : "s"(kb));
+            float t2;
+            const float t1 =
+                r2_screen_terms_xy((float)p0.x, (float)p0.y, (float)p1.x, (float)p1.y, R2, thr_c, sc.E, sc.mloc, t2);
+            const bool may = max(__float_as_int(t1), __float_as_int(t2)) > 0;
+            const bool valid = ((p_okB >> bl) & 1) && p_a0 + al < p_b0 + bl && ((p_okA >> al) & 1);
+            m |= (may && valid ? 1u : 0u) << sub_block<AccF6>(i, wave, lane);
+        }
+    };
+    auto stage_mfma = [&](AccF6 &acc, uint32_t b) {
+        const uint8_t *g = smem + b * kF6Stage;
+        const uint8_t *pa = g + wave * kF6ABytes + lane * 24;
+        const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
+                    i2 = *reinterpret_cast<const uint2 *>(pa + 16);
+        const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536), m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
+                    m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
+        const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
+        const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const uint4 r = *reinterpret_cast<const uint4 *>(g + kF6AStage + n * kF6BBytes + lane * 16);
+            constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
+            const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
+            const v8i bmin = {(int)r.x & kMinor, (int)r.y & kMinor, (int)r.z & kMinor, (int)r.w & kMinor, 0, 0, 0, 0};
+            acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, braw, acc.v[n][0][0], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+            acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc.v[n][0][1], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+            acc.v[n][1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, braw, acc.v[n][1][0], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+            acc.v[n][1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, bmin, acc.v[n][1][1], 2, 4, 0,
+                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
+        }
+    };
+    // the previous tile's verdict: its lanes' sub-blocks met in sMask[j & 1]
+    auto verdict = [&]() {
+        if (has_prev && m) atomicOr(&sMask[(j - 1) & 1], (unsigned long long)m);
+        __syncthreads();
+        if (has_prev)
+            screen_verdict((uint32_t)sMask[(j - 1) & 1], p_a0 / kTile, p_b0 / kTile, tid, n_chunk_rows, o, sc);
+    };
+    // tile j = cur into acc while tile j - 1 (sums in prev) is evaluated;
+    // false: the list ended (then acc holds the last tile) or the pass was given up
+    auto step = [&](AccF6 &acc, const AccF6 &prev, bool &given_up) -> bool {
+        const uint32_t next = tile_at(j + 1);
+        const uint32_t ta = cur >> 16, tb = cur & 0xFFFFu;
+        if (tid == 0) {  // the give-up test of pair_fp6_screen_kernel, per tile
+            uint32_t v = 0;
+            if (sc.bail) {
+                const unsigned cc = __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v = cc > sc.bail ? ((cc & kAbandonBit) ? 2u : 1u) : 0u;
+            }
+            sBail = v;
+        }
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y) acc.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+        m = 0;
+        for (uint32_t kb0 = 0; kb0 < NK; kb0 += 8) {
+#pragma unroll
+            for (int st = 0; st < 8; ++st) {
+                const uint32_t kb = kb0 + st;
+                if (kb < NK) {  // (uniform)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this stage landed
+                    __builtin_amdgcn_s_barrier();  // ... and every other wave's; the other buffer is free
+                    asm volatile("" ::: "memory");
+                    if (kb == 0) {
+                        if (sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
+                            if (tid == 0 && sBail == 1) {
+                                atomicOr(sc.cand_count, kAbandonBit);
+                                atomicOr(sc.cand_buckets, kAbandonBit);
+                            }
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                            given_up = true;
+                            return false;
+                        }
+                        if (tid == 0) sMask[j & 1] = 0ull;  // (tile j - 2's verdict has been read)
+                    }
+                    if (kb + 1 < NK)
+                        issue(cur, kb + 1, buf ^ 1);
+                    else if (next != kNoTile)
+                        issue(next, 0, buf ^ 1);
+                    stage_mfma(acc, buf);
+                    part(prev, st, kb);  // (again in later groups of eight: the same bits)
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done
+                    buf ^= 1;
+                }
+            }
+        }
+#pragma unroll
+        for (int st = 0; st < 8; ++st)
+            if ((uint32_t)st >= NK) part(prev, st, 0u);  // (fewer than eight stages)
+        verdict();
+        p_a0 = ta * kTile;
+        p_b0 = tb * kTile;
+        p_okA = ok_bits[ta];
+        p_okB = ok_bits[tb];
+        has_prev = true;
+        ++j;
+        cur = next;
+        return next != kNoTile;
+    };
+    // the last tile's sums, evaluated alone
+    auto drain = [&](const AccF6 &prev) {
+        m = 0;
+#pragma unroll
+        for (int st = 0; st < 8; ++st) part(prev, st, 0u);
+        verdict();
+    };
+    AccF6 accA, accB;
+    bool given_up = false;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) accB.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+    for (;;) {
+        const bool more = step(accA, accB, given_up);
+        if (given_up) break;
+        accB = accA;  // (tile j's sums become the previous tile's)
+        if (!more) {
+            drain(accB);
+            break;
+        }
+    }
 }
 
 // The fp6 screen on two tiles of one tile row per workgroup: (ta, tb0) and
@@ -1413,7 +1633,11 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
         sc.f32 = 2;
         sc.bail = m.fp6_bail;
         screen_consts(m.fp6->Tg, 2.0f * sc.Rf, sc.E, sc.mloc);
-        if (m.tile_pairs)  // (two tiles of a row per workgroup, the XCD-ordered entries)
+        if (WLD_FP6_PIPE)  // (persistent workgroups along the XCD-ordered list)
+            hipLaunchKernelGGL(pair_fp6_pipe_kernel, dim3(std::min<uint32_t>(m.n_tiles, kF6PipeGrid)), dim3(256), 0, s,
+                               m.fp6->a6, m.fp6->b4, ok_bits, m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows,
+                               m.thr, o, sc);
+        else if (m.tile_pairs)  // (two tiles of a row per workgroup, the XCD-ordered entries)
             hipLaunchKernelGGL(pair_fp6_screen2_kernel, dim3(std::max<uint32_t>(m.n_tile_pairs, 1)), dim3(512), 0, s,
                                m.fp6->a6, m.fp6->b4, ok_bits, m.tile_pairs, m.n_tile_pairs, m.fp6->NK, m.L,
                                m.n_chunk_rows, m.thr, o, sc);
