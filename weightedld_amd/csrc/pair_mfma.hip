@@ -918,6 +918,12 @@ struct AccF6 {
 #ifndef WLD_FP6_PIPE
 #define WLD_FP6_PIPE 0
 #endif
+#ifndef WLD_FP6_PK
+#define WLD_FP6_PK 0  // the pipe kernel's bound on packed f32 (two pairs per instruction)
+#endif
+#ifndef WLD_FP6_PIPE_SGB
+#define WLD_FP6_PIPE_SGB 0
+#endif
 #ifndef WLD_FP6_STAGGER
 #define WLD_FP6_STAGGER 0
 #endif
@@ -1108,18 +1114,25 @@ __global__ __launch_bounds__(256, kF6PipeWgPerCu) void pair_fp6_pipe_kernel(cons
     // (kb: the sums pass through an empty asm that depends on the stage, so
     // the bound is computed in the stage, between its MFMAs, not hoisted)
     auto part = [&](const AccF6 &prev, int p, uint32_t kb) {
+        auto u = prev.raw(0, 2 * p), v = prev.raw(1, 2 * p), x = prev.raw(0, 2 * p + 1), y = prev.raw(1, 2 * p + 1);
+        asm("" : "+v"(u.x), "+v"(u.y), "+v"(v.x), "+v"(v.y) : "s"(kb));
+        asm("" : "+v"(x.x), "+v"(x.y), "+v"(y.x), "+v"(y.y) : "s"(kb));
+        int2 mg;
+        if (WLD_FP6_PK)
+            mg = r2_screen_margin_xy2((wld_f2){u.x, x.x}, (wld_f2){u.y, x.y}, (wld_f2){v.x, y.x}, (wld_f2){v.y, y.y},
+                                      R2, thr_c, sc.E, sc.mloc);
+        else {
+            float t2a, t2b;
+            const float t1a = r2_screen_terms_xy(u.x, u.y, v.x, v.y, R2, thr_c, sc.E, sc.mloc, t2a);
+            const float t1b = r2_screen_terms_xy(x.x, x.y, y.x, y.y, R2, thr_c, sc.E, sc.mloc, t2b);
+            mg = make_int2(max(__float_as_int(t1a), __float_as_int(t2a)), max(__float_as_int(t1b), __float_as_int(t2b)));
+        }
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int i = 2 * p + q;
             const uint32_t al = AccF6::a_local(i, wave, lane), bl = AccF6::b_local(i, wave, lane);
-            auto p0 = prev.raw(0, i), p1 = prev.raw(1, i);
-            asm("" : "+v"(p0.x), "+v"(p0.y), "+v"(p1.x), "+v"(p1.y) : "s"(kb));
-            float t2;
-            const float t1 =
-                r2_screen_terms_xy((float)p0.x, (float)p0.y, (float)p1.x, (float)p1.y, R2, thr_c, sc.E, sc.mloc, t2);
-            const bool may = max(__float_as_int(t1), __float_as_int(t2)) > 0;
             const bool valid = ((p_okB >> bl) & 1) && p_a0 + al < p_b0 + bl && ((p_okA >> al) & 1);
-            m |= (may && valid ? 1u : 0u) << sub_block<AccF6>(i, wave, lane);
+            m |= ((q ? mg.y : mg.x) > 0 && valid ? 1u : 0u) << sub_block<AccF6>(i, wave, lane);
         }
     };
     auto stage_mfma = [&](AccF6 &acc, uint32_t b) {
@@ -1200,6 +1213,13 @@ __global__ __launch_bounds__(256, kF6PipeWgPerCu) void pair_fp6_pipe_kernel(cons
                         issue(next, 0, buf ^ 1);
                     stage_mfma(acc, buf);
                     part(prev, st, kb);  // (again in later groups of eight: the same bits)
+                    if (WLD_FP6_PIPE_SGB) {  // A/B: the bound's VALU placed between the MFMAs
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+                        }
+                    }
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done
                     buf ^= 1;
                 }
