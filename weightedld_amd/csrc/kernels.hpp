@@ -214,6 +214,11 @@ constexpr uint32_t kRefItemGrid = 1024;
 #ifndef WLD_FP6_PAIRS
 #define WLD_FP6_PAIRS 0
 #endif
+// the one-plane i8 screen with its epilogue in the MFMA shadow (persistent
+// workgroups, pair_i8_pipe_kernel)
+#ifndef WLD_I8_PIPE
+#define WLD_I8_PIPE 0
+#endif
 // the reference-order gather enqueued behind the scan when the previous run
 // had rows (capi.hip enqueue_pass; 0: after the host has read the row count,
 // the round-3 order; A/B builds only)
