@@ -844,7 +844,6 @@ __global__ __launch_bounds__(256, kI8PipeWgPerCu) void pair_i8_pipe_kernel(
     using Acc = Acc16<1, 4>;
     __shared__ __attribute__((aligned(16))) uint8_t smem[2 * KGB];
     __shared__ unsigned long long sMask[2];
-    __shared__ uint32_t sBail;
     if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t G = gridDim.x, NKB = NP / 32, n_groups = (NKB + KG - 1) / KG;
