@@ -214,6 +214,11 @@ constexpr uint32_t kRefItemGrid = 1024;
 #ifndef WLD_FP6_PAIRS
 #define WLD_FP6_PAIRS 0
 #endif
+// the screens' per-pair bound on full tiles two pairs per packed-f32
+// instruction (r2_screen_margin_xy2; the same bits as one pair at a time)
+#ifndef WLD_SCREEN_PK
+#define WLD_SCREEN_PK 0
+#endif
 // the one-plane i8 screen with its epilogue in the MFMA shadow (persistent
 // workgroups, pair_i8_pipe_kernel)
 #ifndef WLD_I8_PIPE

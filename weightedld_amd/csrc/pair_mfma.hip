@@ -544,8 +544,19 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
             // every pair valid (the tile touches neither the diagonal nor a
             // filtered/padding site)
             int worst = -1;
+            if (WLD_SCREEN_PK) {  // two pairs per packed-f32 instruction (the same bits)
 #pragma unroll
-            for (int i = 0; i < Acc::kPairs; ++i) worst = max(worst, margin(i));
+                for (int i = 0; i < Acc::kPairs; i += 2) {
+                    const auto u = acc.raw(0, i), v = acc.raw(1, i), x = acc.raw(0, i + 1), y = acc.raw(1, i + 1);
+                    const int2 mg = r2_screen_margin_xy2(
+                        (wld_f2){(float)u.x, (float)x.x}, (wld_f2){(float)u.y, (float)x.y},
+                        (wld_f2){(float)v.x, (float)y.x}, (wld_f2){(float)v.y, (float)y.y}, R2, thr_c, sc.E, sc.mloc);
+                    worst = max(worst, max(mg.x, mg.y));
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < Acc::kPairs; ++i) worst = max(worst, margin(i));
+            }
             cand = worst > 0;
         } else {
 #pragma unroll
