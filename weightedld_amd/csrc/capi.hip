@@ -156,8 +156,6 @@ struct wld_ctx {
 
     // run state
     DevBuf tiles, cand, seg_cnt, seg_off, chunk_total, chunk_base, counters;
-    DevBuf tile_pairs;     // the fp6 screen's two-tile entries (WLD_FP6_PAIRS)
-    uint32_t n_tile_pairs = 0;
     DevBuf st_a, st_b, st_d, st_dp, st_r2;
     DevBuf out_a, out_b, out_d, out_dp, out_r2;
     uint64_t st_capacity = 0;
@@ -546,35 +544,6 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
     }
     std::sort(t.begin(), t.end());
     const uint32_t kS = 24ull * kTile * c->NP <= (4ull << 20) ? 16u : 8u;
-    if (WLD_FP6_PAIRS) {
-        // the fp6 screen's entries: tiles (ta, 2j) and (ta, 2j + 1) together
-        // where both are in the list, the others alone; in the same launch
-        // order as the tiles (keyed by the first tile)
-        std::vector<uint32_t> first;
-        std::vector<uint64_t> pr;
-        for (size_t i = 0; i < t.size(); ++i) {
-            const bool two = (t[i] & 1u) == 0 && i + 1 < t.size() && t[i + 1] == t[i] + 1;
-            first.push_back(t[i]);
-            pr.push_back((uint64_t)t[i] | (uint64_t)(two ? t[i + 1] : kNoTile) << 32);
-            i += two;
-        }
-        if (!c->opt_tile_rows && first.size() >= 2048 && T_used < 65535) first = xcd_order(first, kS);
-        std::vector<uint32_t> flat;
-        flat.reserve(2 * first.size());
-        for (uint32_t f : first) {
-            uint32_t second = kNoTile;
-            if (f != kNoTile)
-                second = (uint32_t)(*std::lower_bound(pr.begin(), pr.end(), f,
-                                                      [](uint64_t e, uint32_t v) { return (uint32_t)e < v; }) >> 32);
-            flat.push_back(f);
-            flat.push_back(second);
-        }
-        c->n_tile_pairs = (uint32_t)first.size();
-        WLD_TRY(ensure(c->tile_pairs, std::max<size_t>(flat.size(), 2) * sizeof(uint32_t)));
-        if (!flat.empty())
-            HIP_TRY(hipMemcpyAsync(c->tile_pairs.p, flat.data(), flat.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
-                                   c->stream));
-    }
     // only with many rounds of resident tiles: whole super-blocks per XCD
     // leave up to one super-block of imbalance (C2's 528 tiles: +14%)
     if (!c->opt_tile_rows && t.size() >= 4096 && T_used < 65535) t = xcd_order(t, kS);
@@ -716,8 +685,6 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         // re-run rewrites it)
         m.fp6_bail = c->opt_fp6 == 1 && !c->prog_pass && !c->pend.count_out ? std::max<uint32_t>(c->n_tiles / 16, 1)
                                                                                 : 0;
-        m.tile_pairs = WLD_FP6_PAIRS ? ptr<uint32_t>(c->tile_pairs) : nullptr;
-        m.n_tile_pairs = c->n_tile_pairs;
         for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
         m.cand_list = ptr<uint32_t>(c->cand);
         // this pass's candidate set (the scan zeroes the other one, enqueue_pass)

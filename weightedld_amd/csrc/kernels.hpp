@@ -209,11 +209,6 @@ constexpr uint32_t kRefItemGrid = 1024;
 #ifndef WLD_REF_ITEMS
 #define WLD_REF_ITEMS 1
 #endif
-// the fp6 screen on two tiles of a tile row per 8-wave workgroup (one shared
-// A copy per stage)
-#ifndef WLD_FP6_PAIRS
-#define WLD_FP6_PAIRS 0
-#endif
 // the screens' per-pair bound on full tiles two pairs per packed-f32
 // instruction (r2_screen_margin_xy2; the same bits as one pair at a time)
 #ifndef WLD_SCREEN_PK
@@ -286,11 +281,6 @@ struct MfmaLaunch {
     const Fp6Screen *fp6;
     // ... gives up past this many candidate tiles (0: never; kAbandonBit)
     uint32_t fp6_bail;
-    // ... on two tiles of a tile row per workgroup (WLD_FP6_PAIRS): n_tile_pairs
-    // (first, second) tile entries, second kNoTile for a lone tile (null: one
-    // tile per workgroup from tiles)
-    const uint32_t *tile_pairs;
-    uint32_t n_tile_pairs;
 };
 // Enqueues the MFMA pair kernel(s) of one pass; returns true when a screen
 // (one- or two-plane) ran (then screen_done, if given, is recorded between

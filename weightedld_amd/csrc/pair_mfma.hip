@@ -841,9 +841,10 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
 }
 
 // The one-plane i8 screen (kModeScreen, NPL = 1, f32 == 2) with its epilogue
-// in the MFMA shadow (WLD_I8_PIPE), as pair_fp6_pipe_kernel: persistent
-// workgroups along the XCD-ordered list, tile j accumulated while tile j - 1's
-// pairs are bounded two per 64-sequence step (eight steps cover the tile), the
+// in the MFMA shadow (WLD_I8_PIPE; A/B): persistent workgroups along the
+// XCD-ordered list (entries blockIdx.x, + gridDim.x, ...: one XCD queue), tile
+// j accumulated while tile j - 1's pairs (sums in a second accumulator set)
+// are bounded two per 64-sequence step (eight steps cover the tile), the
 // copies running on across tiles.  Operands, layout and sums are those of
 // pair_mfma_kernel<kModeScreen, 1> (4-stage groups).
 constexpr uint32_t kI8PipeWgPerCu = 2, kI8PipeGrid = 256 * kI8PipeWgPerCu;
@@ -1066,20 +1067,6 @@ struct AccF6 {
 #ifndef WLD_FP6_WG
 #define WLD_FP6_WG 4  // workgroups per CU
 #endif
-// A/B: the first round's workgroups of a CU start this many cycles apart
-// (by workgroup slot), so the four do not run their epilogues in lockstep
-#ifndef WLD_FP6_PIPE
-#define WLD_FP6_PIPE 0
-#endif
-#ifndef WLD_FP6_PK
-#define WLD_FP6_PK 0  // the pipe kernel's bound on packed f32 (two pairs per instruction)
-#endif
-#ifndef WLD_FP6_PIPE_SGB
-#define WLD_FP6_PIPE_SGB 0
-#endif
-#ifndef WLD_FP6_STAGGER
-#define WLD_FP6_STAGGER 0
-#endif
 // diagnostic builds (wrong results, timing only): 1 no epilogue, 2 also every
 // stage's copy from the first stage, 3 also no MFMA
 #ifndef WLD_FP6_DIAG
@@ -1101,11 +1088,6 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     // (kNoTile: padding of an XCD-ordered list, or past the end of the grid)
     const uint32_t tile = blockIdx.x < n_tiles ? tiles[blockIdx.x] : kNoTile;
     if (tile == kNoTile) return;  // (uniform: the whole workgroup)
-    if (WLD_FP6_STAGGER && blockIdx.x < 1024) {
-        uint32_t slot;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID, 16, 4)" : "=s"(slot));
-        for (uint32_t k = (slot & 3) * (WLD_FP6_STAGGER / 8128); k; --k) __builtin_amdgcn_s_sleep(127);
-    }
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
     // this wave's DMA sources: A of row block 4 ta + wave, B of column block 4 tb + wave
     const uint8_t *sA = a6 + (size_t)(4 * ta + wave) * NK * kF6ABytes;
@@ -1212,361 +1194,6 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     }
     tile_epilogue<kModeScreen, AccF6>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, 0, o, dn, sc, sBits,
                                       sRowBase);
-}
-
-// The fp6 screen with the epilogue in the MFMA shadow (WLD_FP6_PIPE): a
-// persistent workgroup takes list entries blockIdx.x, + gridDim.x, ... (the
-// same XCD queue) and evaluates tile j - 1's pairs while it accumulates tile
-// j: stage s of every eight runs the bound on pairs 2 (s mod 8) and + 1 of
-// the previous tile's sums (kept in a second accumulator set) between the
-// stage's MFMAs, and the copies run on across tiles (tile j + 1's first
-// stage behind tile j's last).  The one-tile kernel runs its epilogue after
-// its MFMAs, in lockstep with the other workgroups of its CU, and that phase
-// cost ~40% of its time at C4 (profiles/r04p: 0.77 -> 0.45 ms without it).
-constexpr uint32_t kF6PipeWgPerCu = 2, kF6PipeGrid = 256 * kF6PipeWgPerCu;
-__global__ __launch_bounds__(256, kF6PipeWgPerCu) void pair_fp6_pipe_kernel(const uint8_t *__restrict__ a6,
-                                                                            const uint8_t *__restrict__ b4,
-                                                                            const uint64_t *__restrict__ ok_bits,
-                                                                            const uint32_t *__restrict__ tiles,
-                                                                            uint32_t n_tiles, uint32_t NK, uint32_t L,
-                                                                            uint32_t n_chunk_rows, float thr,
-                                                                            OrderArgs o, ScreenArgs sc) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6Stage];
-    __shared__ unsigned long long sMask[2];
-    __shared__ uint32_t sBail;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
-    const uint32_t G = gridDim.x;
-    // (kNoTile: padding at the end of an XCD queue; nothing follows it there)
-    auto tile_at = [&](uint32_t j) -> uint32_t {
-        const uint32_t e = blockIdx.x + j * G;
-        return e < n_tiles ? tiles[e] : kNoTile;
-    };
-    uint32_t cur = tile_at(0);
-    if (cur == kNoTile) return;  // (uniform)
-    auto issue = [&](uint32_t tile, uint32_t kb, uint32_t buf) {
-        const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
-        const uint8_t *a = a6 + ((size_t)(4 * ta + wave) * NK + kb) * kF6ABytes;
-        const uint8_t *b = b4 + ((size_t)(4 * tb + wave) * NK + kb) * kF6BBytes;
-        const uint32_t gb = lds + buf * kF6Stage;
-        glds16_s(a, lane16, gb + wave * kF6ABytes);
-        glds16_s(a + 1024, lane16, gb + wave * kF6ABytes + 1024);
-        glds16_s(a + 2048, lane16, gb + wave * kF6ABytes + 2048);
-        glds16_s(b, lane16, gb + kF6AStage + wave * kF6BBytes);
-    };
-    if (tid == 0) sMask[0] = sMask[1] = 0ull;  // (published by the first stage barrier)
-    issue(cur, 0, 0);
-    const float thr_c = thr * (1.0f - 0x1p-7f), R2 = 2.0f * sc.Rf;
-    // the previous tile: its position and site flags (its sums: the other set)
-    uint32_t p_a0 = 0, p_b0 = 0, j = 0, buf = 0;
-    uint64_t p_okA = 0, p_okB = 0;
-    bool has_prev = false;
-    unsigned m = 0;  // this lane's sub-blocks of the previous tile holding a pair that may pass
-    // pairs 2p, 2p + 1 of the previous tile (tile_epilogue's kModeScreen test, f32 == 2)
-    // (kb: the sums pass through an empty asm that depends on the stage, so
-    // the bound is computed in the stage, between its MFMAs, not hoisted)
-    auto part = [&](const AccF6 &prev, int p, uint32_t kb) {
-        auto u = prev.raw(0, 2 * p), v = prev.raw(1, 2 * p), x = prev.raw(0, 2 * p + 1), y = prev.raw(1, 2 * p + 1);
-        asm("" : "+v"(u.x), "+v"(u.y), "+v"(v.x), "+v"(v.y) : "s"(kb));
-        asm("" : "+v"(x.x), "+v"(x.y), "+v"(y.x), "+v"(y.y) : "s"(kb));
-        int2 mg;
-        if (WLD_FP6_PK)
-            mg = r2_screen_margin_xy2((wld_f2){u.x, x.x}, (wld_f2){u.y, x.y}, (wld_f2){v.x, y.x}, (wld_f2){v.y, y.y},
-                                      R2, thr_c, sc.E, sc.mloc);
-        else {
-            float t2a, t2b;
-            const float t1a = r2_screen_terms_xy(u.x, u.y, v.x, v.y, R2, thr_c, sc.E, sc.mloc, t2a);
-            const float t1b = r2_screen_terms_xy(x.x, x.y, y.x, y.y, R2, thr_c, sc.E, sc.mloc, t2b);
-            mg = make_int2(max(__float_as_int(t1a), __float_as_int(t2a)), max(__float_as_int(t1b), __float_as_int(t2b)));
-        }
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int i = 2 * p + q;
-            const uint32_t al = AccF6::a_local(i, wave, lane), bl = AccF6::b_local(i, wave, lane);
-            const bool valid = ((p_okB >> bl) & 1) && p_a0 + al < p_b0 + bl && ((p_okA >> al) & 1);
-            m |= ((q ? mg.y : mg.x) > 0 && valid ? 1u : 0u) << sub_block<AccF6>(i, wave, lane);
-        }
-    };
-    auto stage_mfma = [&](AccF6 &acc, uint32_t b) {
-        const uint8_t *g = smem + b * kF6Stage;
-        const uint8_t *pa = g + wave * kF6ABytes + lane * 24;
-        const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
-                    i2 = *reinterpret_cast<const uint2 *>(pa + 16);
-        const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536), m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
-                    m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
-        const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
-        const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const uint4 r = *reinterpret_cast<const uint4 *>(g + kF6AStage + n * kF6BBytes + lane * 16);
-            constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
-            const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
-            const v8i bmin = {(int)r.x & kMinor, (int)r.y & kMinor, (int)r.z & kMinor, (int)r.w & kMinor, 0, 0, 0, 0};
-            acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, braw, acc.v[n][0][0], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-            acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc.v[n][0][1], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-            acc.v[n][1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, braw, acc.v[n][1][0], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-            acc.v[n][1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, bmin, acc.v[n][1][1], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-        }
-    };
-    // the previous tile's verdict: its lanes' sub-blocks met in sMask[j & 1]
-    auto verdict = [&]() {
-        if (has_prev && m) atomicOr(&sMask[(j - 1) & 1], (unsigned long long)m);
-        __syncthreads();
-        if (has_prev)
-            screen_verdict((uint32_t)sMask[(j - 1) & 1], p_a0 / kTile, p_b0 / kTile, tid, n_chunk_rows, o, sc);
-    };
-    // tile j = cur into acc while tile j - 1 (sums in prev) is evaluated;
-    // false: the list ended (then acc holds the last tile) or the pass was given up
-    auto step = [&](AccF6 &acc, const AccF6 &prev, bool &given_up) -> bool {
-        const uint32_t next = tile_at(j + 1);
-        const uint32_t ta = cur >> 16, tb = cur & 0xFFFFu;
-        if (tid == 0) {  // the give-up test of pair_fp6_screen_kernel, per tile
-            uint32_t v = 0;
-            if (sc.bail) {
-                const unsigned cc = __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                v = cc > sc.bail ? ((cc & kAbandonBit) ? 2u : 1u) : 0u;
-            }
-            sBail = v;
-        }
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-            for (int x = 0; x < 2; ++x)
-#pragma unroll
-                for (int y = 0; y < 2; ++y) acc.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-        m = 0;
-        for (uint32_t kb0 = 0; kb0 < NK; kb0 += 8) {
-#pragma unroll
-            for (int st = 0; st < 8; ++st) {
-                const uint32_t kb = kb0 + st;
-                if (kb < NK) {  // (uniform)
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this stage landed
-                    __builtin_amdgcn_s_barrier();  // ... and every other wave's; the other buffer is free
-                    asm volatile("" ::: "memory");
-                    if (kb == 0) {
-                        if (sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
-                            if (tid == 0 && sBail == 1) {
-                                atomicOr(sc.cand_count, kAbandonBit);
-                                atomicOr(sc.cand_buckets, kAbandonBit);
-                            }
-                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                            given_up = true;
-                            return false;
-                        }
-                        if (tid == 0) sMask[j & 1] = 0ull;  // (tile j - 2's verdict has been read)
-                    }
-                    if (kb + 1 < NK)
-                        issue(cur, kb + 1, buf ^ 1);
-                    else if (next != kNoTile)
-                        issue(next, 0, buf ^ 1);
-                    stage_mfma(acc, buf);
-                    part(prev, st, kb);  // (again in later groups of eight: the same bits)
-                    if (WLD_FP6_PIPE_SGB) {  // A/B: the bound's VALU placed between the MFMAs
-#pragma unroll
-                        for (int k = 0; k < 16; ++k) {
-                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-                        }
-                    }
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done
-                    buf ^= 1;
-                }
-            }
-        }
-#pragma unroll
-        for (int st = 0; st < 8; ++st)
-            if ((uint32_t)st >= NK) part(prev, st, 0u);  // (fewer than eight stages)
-        verdict();
-        p_a0 = ta * kTile;
-        p_b0 = tb * kTile;
-        p_okA = ok_bits[ta];
-        p_okB = ok_bits[tb];
-        has_prev = true;
-        ++j;
-        cur = next;
-        return next != kNoTile;
-    };
-    // the last tile's sums, evaluated alone
-    auto drain = [&](const AccF6 &prev) {
-        m = 0;
-#pragma unroll
-        for (int st = 0; st < 8; ++st) part(prev, st, 0u);
-        verdict();
-    };
-    AccF6 accA, accB;
-    bool given_up = false;
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int x = 0; x < 2; ++x)
-#pragma unroll
-            for (int y = 0; y < 2; ++y) accB.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-    for (;;) {
-        const bool more = step(accA, accB, given_up);
-        if (given_up) break;
-        accB = accA;  // (tile j's sums become the previous tile's)
-        if (!more) {
-            drain(accB);
-            break;
-        }
-    }
-}
-
-// The fp6 screen on two tiles of one tile row per workgroup: (ta, tb0) and
-// (ta, tb1) (tb1 = tb0 + 1; a lone tile: the second entry kNoTile).  Eight
-// waves share one A copy per stage: waves 0-3 copy A's four row blocks
-// (3 KB each), waves 4-7 B's column blocks of both tiles (1 KB each); half h
-// = wave / 4 computes tile h exactly as pair_fp6_screen_kernel's waves do.
-// A stage is 12 + 8 KB for 8192 pairs instead of 16 KB for 4096: the L2 ->
-// CU bytes per pair 4 -> 2.5 (the one-tile kernel moved ~52% of the L2's
-// bandwidth at C4, and more bytes per stage cost time there, Appendix A).
-constexpr int kF6Stage2 = kF6AStage + 8 * kF6BBytes;
-__global__ __launch_bounds__(512, 2) void pair_fp6_screen2_kernel(const uint8_t *__restrict__ a6,
-                                                                  const uint8_t *__restrict__ b4,
-                                                                  const uint64_t *__restrict__ ok_bits,
-                                                                  const uint32_t *__restrict__ tile_pairs,
-                                                                  uint32_t n_pairs, uint32_t NK, uint32_t L,
-                                                                  uint32_t n_chunk_rows, float thr, OrderArgs o,
-                                                                  ScreenArgs sc) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6Stage2];
-    __shared__ unsigned long long sMask[2];
-    __shared__ uint32_t sBail, sAny[2];
-    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t h = wave >> 2, w4 = wave & 3, lt = tid & 255;  // tile half, wave and thread in it
-    const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
-    // (kNoTile: padding of an XCD-ordered list, or past the end of the grid)
-    const uint32_t t0 = blockIdx.x < n_pairs ? tile_pairs[2 * blockIdx.x] : kNoTile;
-    if (t0 == kNoTile) return;  // (uniform: the whole workgroup)
-    const uint32_t t1 = tile_pairs[2 * blockIdx.x + 1];
-    const bool two = t1 != kNoTile, live = h == 0 || two;  // (a lone tile's half 1 computes tile 0's B, unused)
-    const uint32_t ta = t0 >> 16, tb0 = t0 & 0xFFFFu, tb1 = two ? t1 & 0xFFFFu : tb0, tb = h ? tb1 : tb0;
-    // this wave's DMA sources: A of row block 4 ta + w4 (half 0) or B of
-    // column block w4 of both tiles (half 1)
-    const uint8_t *sA = a6 + (size_t)(4 * ta + w4) * NK * kF6ABytes;
-    const uint8_t *sB0 = b4 + (size_t)(4 * tb0 + w4) * NK * kF6BBytes;
-    const uint8_t *sB1 = b4 + (size_t)(4 * tb1 + w4) * NK * kF6BBytes;
-    auto issue = [&](uint32_t kb, uint32_t buf) {
-        const uint32_t gb = lds + buf * kF6Stage2;
-        if (h == 0) {
-            const uint8_t *a = sA + (size_t)kb * kF6ABytes;
-            glds16_s(a, lane16, gb + w4 * kF6ABytes);
-            glds16_s(a + 1024, lane16, gb + w4 * kF6ABytes + 1024);
-            glds16_s(a + 2048, lane16, gb + w4 * kF6ABytes + 2048);
-        } else {
-            glds16_s(sB0 + (size_t)kb * kF6BBytes, lane16, gb + kF6AStage + w4 * kF6BBytes);
-            glds16_s(sB1 + (size_t)kb * kF6BBytes, lane16, gb + kF6AStage + 4 * kF6BBytes + w4 * kF6BBytes);
-        }
-    };
-    issue(0, 0);
-    // the give-up test as in pair_fp6_screen_kernel; the verdict words
-    // zeroed (all published by the first stage barrier)
-    if (tid == 0) {
-        uint32_t v = 0;
-        if (sc.bail) {
-            const unsigned cc = __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v = cc > sc.bail ? ((cc & kAbandonBit) ? 2u : 1u) : 0u;
-        }
-        sBail = v;
-    }
-    if (tid < 2) {
-        sMask[tid] = 0ull;
-        sAny[tid] = 0u;
-    }
-    const uint64_t okA = ok_bits[ta], okB = live ? ok_bits[tb] : 0ull;
-    AccF6 acc;
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int x = 0; x < 2; ++x)
-#pragma unroll
-            for (int y = 0; y < 2; ++y) acc.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-    uint32_t buf = 0;
-    for (uint32_t kb = 0; kb < NK; ++kb) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of this stage landed
-        __builtin_amdgcn_s_barrier();  // ... and every other wave's; the buffer read last stage is free
-        asm volatile("" ::: "memory");
-        if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
-            if (tid == 0 && sBail == 1) {
-                atomicOr(sc.cand_count, kAbandonBit);
-                atomicOr(sc.cand_buckets, kAbandonBit);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            return;
-        }
-        if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
-        const uint8_t *g = smem + buf * kF6Stage2;
-        const uint8_t *pa = g + w4 * kF6ABytes + lane * 24;
-        const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
-                    i2 = *reinterpret_cast<const uint2 *>(pa + 16);
-        const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536), m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
-                    m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
-        const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
-        const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const uint4 r = *reinterpret_cast<const uint4 *>(g + kF6AStage + (4 * h + n) * kF6BBytes + lane * 16);
-            constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
-            const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
-            const v8i bmin = {(int)r.x & kMinor, (int)r.y & kMinor, (int)r.z & kMinor, (int)r.w & kMinor, 0, 0, 0, 0};
-            acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, braw, acc.v[n][0][0], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-            acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc.v[n][0][1], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-            acc.v[n][1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, braw, acc.v[n][1][0], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-            acc.v[n][1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, bmin, acc.v[n][1][1], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
-        buf ^= 1;
-    }
-    // the screen epilogue of tile_epilogue (kModeScreen, f32 == 2) per half:
-    // a pair may pass unless the f32 bound rejects it; the halves' verdicts
-    // meet in LDS with barriers both halves pass
-    const uint32_t a0 = ta * kTile, b0 = tb * kTile;
-    const float thr_c = thr * (1.0f - 0x1p-7f), R2 = 2.0f * sc.Rf;
-    auto margin = [&](int i) {
-        const auto p0 = acc.raw(0, i), p1 = acc.raw(1, i);  // (X, Y) of channel_a in, major
-        float t2;
-        const float t1 =
-            r2_screen_terms_xy((float)p0.x, (float)p0.y, (float)p1.x, (float)p1.y, R2, thr_c, sc.E, sc.mloc, t2);
-        return max(__float_as_int(t1), __float_as_int(t2));
-    };
-    auto pair_cand = [&](int i) -> bool {
-        const uint32_t a_local = AccF6::a_local(i, w4, lane), b_local = AccF6::b_local(i, w4, lane);
-        return ((okB >> b_local) & 1) && a0 + a_local < b0 + b_local && ((okA >> a_local) & 1) && margin(i) > 0;
-    };
-    bool cand = false;
-    if (okA == ~0ull && okB == ~0ull && ta != tb) {
-        int worst = -1;
-#pragma unroll
-        for (int i = 0; i < AccF6::kPairs; ++i) worst = max(worst, margin(i));
-        cand = worst > 0;
-    } else {
-#pragma unroll
-        for (int i = 0; i < AccF6::kPairs; ++i)
-            if (!cand) cand = pair_cand(i);
-    }
-    if (__ballot(cand) != 0 && lane == 0) sAny[h] = 1u;
-    __syncthreads();
-    const uint32_t any0 = sAny[0], any1 = sAny[1];
-    if (any0 | any1) {  // (uniform)
-        if (h ? any1 : any0) {
-            unsigned m = 0;
-#pragma unroll
-            for (int i = 0; i < AccF6::kPairs; ++i)
-                if (pair_cand(i)) m |= 1u << sub_block<AccF6>(i, w4, lane);
-            if (m) atomicOr(&sMask[h], (unsigned long long)m);
-        }
-        __syncthreads();
-    }
-    if (live) screen_verdict((uint32_t)sMask[h], ta, tb, lt, n_chunk_rows, o, sc);
 }
 
 void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b4,
@@ -1806,17 +1433,9 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
         sc.f32 = 2;
         sc.bail = m.fp6_bail;
         screen_consts(m.fp6->Tg, 2.0f * sc.Rf, sc.E, sc.mloc);
-        if (WLD_FP6_PIPE)  // (persistent workgroups along the XCD-ordered list)
-            hipLaunchKernelGGL(pair_fp6_pipe_kernel, dim3(std::min<uint32_t>(m.n_tiles, kF6PipeGrid)), dim3(256), 0, s,
-                               m.fp6->a6, m.fp6->b4, ok_bits, m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows,
-                               m.thr, o, sc);
-        else if (m.tile_pairs)  // (two tiles of a row per workgroup, the XCD-ordered entries)
-            hipLaunchKernelGGL(pair_fp6_screen2_kernel, dim3(std::max<uint32_t>(m.n_tile_pairs, 1)), dim3(512), 0, s,
-                               m.fp6->a6, m.fp6->b4, ok_bits, m.tile_pairs, m.n_tile_pairs, m.fp6->NK, m.L,
-                               m.n_chunk_rows, m.thr, o, sc);
-        else  // (one tile per workgroup, the XCD-ordered list)
-            hipLaunchKernelGGL(pair_fp6_screen_kernel, dim3(m.n_tiles), dim3(256), 0, s, m.fp6->a6, m.fp6->b4, ok_bits,
-                               m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
+        // (one tile per workgroup, the XCD-ordered list)
+        hipLaunchKernelGGL(pair_fp6_screen_kernel, dim3(m.n_tiles), dim3(256), 0, s, m.fp6->a6, m.fp6->b4, ok_bits,
+                           m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
         if (screen_done) (void)hipEventRecord(screen_done, s);
         launch_candidates(m, n, idx, ok_bits, o, dn, sc, s);
         return true;
