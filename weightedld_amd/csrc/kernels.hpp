@@ -209,16 +209,6 @@ constexpr uint32_t kRefItemGrid = 1024;
 #ifndef WLD_REF_ITEMS
 #define WLD_REF_ITEMS 1
 #endif
-// the screens' per-pair bound on full tiles two pairs per packed-f32
-// instruction (r2_screen_margin_xy2; the same bits as one pair at a time)
-#ifndef WLD_SCREEN_PK
-#define WLD_SCREEN_PK 0
-#endif
-// the one-plane i8 screen with its epilogue in the MFMA shadow (persistent
-// workgroups, pair_i8_pipe_kernel)
-#ifndef WLD_I8_PIPE
-#define WLD_I8_PIPE 0
-#endif
 // the reference-order gather enqueued behind the scan when the previous run
 // had rows (capi.hip enqueue_pass; 0: after the host has read the row count,
 // the round-3 order; A/B builds only)

@@ -131,25 +131,6 @@ __host__ __device__ __forceinline__ float r2_screen_terms_xy(float X0, float Y0,
     t2 = mloc - mlo;
     return nub * nub - thr_c * ((m1 * m2) * (m3 * m4));
 }
-// r2_screen_terms_xy for two pairs at once on packed f32 (v_pk_add/mul/fma_f32:
-// each lane of a packed op rounds as the scalar op does, and the sequence of
-// operations is the same, so both terms are bit for bit those of
-// r2_screen_terms_xy); returns max(t1, t2) of each pair as int bits (> 0: the
-// bound cannot reject the pair)
-typedef float wld_f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ int2 r2_screen_margin_xy2(wld_f2 X0, wld_f2 Y0, wld_f2 X1, wld_f2 Y1, float R,
-                                                     float thr_c, float E, float mloc) {
-    const wld_f2 Rv = {R, R}, two = {2.0f, 2.0f};
-    const wld_f2 T = X0 + Y0, B = X0 - Y0, A = X1 + Y1;
-    const wld_f2 m1 = A - Rv, m2 = (T - A) - Rv, m3 = B - Rv, m4 = __builtin_elementwise_fma(two, Y0, -Rv);
-    const wld_f2 num = __builtin_elementwise_fma(X0, Y1, -(X1 * Y0));
-    const wld_f2 an = {fabsf(num.x), fabsf(num.y)};
-    const wld_f2 nub = __builtin_elementwise_fma(two, an, (wld_f2){E, E});
-    const wld_f2 t1 = nub * nub - (wld_f2){thr_c, thr_c} * ((m1 * m2) * (m3 * m4));
-    const float mlo0 = fminf(fminf(m1.x, m2.x), fminf(m3.x, m4.x)), mlo1 = fminf(fminf(m1.y, m2.y), fminf(m3.y, m4.y));
-    const wld_f2 t2 = (wld_f2){mloc, mloc} - (wld_f2){mlo0, mlo1};
-    return make_int2(max(__float_as_int(t1.x), __float_as_int(t2.x)), max(__float_as_int(t1.y), __float_as_int(t2.y)));
-}
 __host__ __device__ __forceinline__ float r2_screen_violation(float T, float A, float B, float AB, float R,
                                                               float thr_c) {
     float E, mloc, t2;

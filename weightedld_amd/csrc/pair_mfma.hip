@@ -544,19 +544,8 @@ __device__ __forceinline__ void tile_epilogue(const SumFn &sum, const Acc &acc, 
             // every pair valid (the tile touches neither the diagonal nor a
             // filtered/padding site)
             int worst = -1;
-            if (WLD_SCREEN_PK) {  // two pairs per packed-f32 instruction (the same bits)
 #pragma unroll
-                for (int i = 0; i < Acc::kPairs; i += 2) {
-                    const auto u = acc.raw(0, i), v = acc.raw(1, i), x = acc.raw(0, i + 1), y = acc.raw(1, i + 1);
-                    const int2 mg = r2_screen_margin_xy2(
-                        (wld_f2){(float)u.x, (float)x.x}, (wld_f2){(float)u.y, (float)x.y},
-                        (wld_f2){(float)v.x, (float)y.x}, (wld_f2){(float)v.y, (float)y.y}, R2, thr_c, sc.E, sc.mloc);
-                    worst = max(worst, max(mg.x, mg.y));
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < Acc::kPairs; ++i) worst = max(worst, margin(i));
-            }
+            for (int i = 0; i < Acc::kPairs; ++i) worst = max(worst, margin(i));
             cand = worst > 0;
         } else {
 #pragma unroll
@@ -837,149 +826,6 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
             __syncthreads();
         }
         scan_tail(sc.scan, nt);
-    }
-}
-
-// The one-plane i8 screen (kModeScreen, NPL = 1, f32 == 2) with its epilogue
-// in the MFMA shadow (WLD_I8_PIPE; A/B): persistent workgroups along the
-// XCD-ordered list (entries blockIdx.x, + gridDim.x, ...: one XCD queue), tile
-// j accumulated while tile j - 1's pairs (sums in a second accumulator set)
-// are bounded two per 64-sequence step (eight steps cover the tile), the
-// copies running on across tiles.  Operands, layout and sums are those of
-// pair_mfma_kernel<kModeScreen, 1> (4-stage groups).
-constexpr uint32_t kI8PipeWgPerCu = 2, kI8PipeGrid = 256 * kI8PipeWgPerCu;
-__global__ __launch_bounds__(256, kI8PipeWgPerCu) void pair_i8_pipe_kernel(
-    const uint8_t *__restrict__ frag, const uint8_t *__restrict__ frag_b, const int8_t *__restrict__ planes,
-    const uint64_t *__restrict__ ok_bits, const uint32_t *__restrict__ tiles, uint32_t n_tiles, uint32_t NP,
-    uint32_t n_chunk_rows, float thr, uint32_t plane_idx, OrderArgs o, ScreenArgs sc) {
-    constexpr int KG = GroupShape<1>::kStages, KGB = GroupShape<1>::kBytes;
-    using Acc = Acc16<1, 4>;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * KGB];
-    __shared__ unsigned long long sMask[2];
-    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t G = gridDim.x, NKB = NP / 32, n_groups = (NKB + KG - 1) / KG;
-    auto tile_at = [&](uint32_t j) -> uint32_t {
-        const uint32_t e = blockIdx.x + j * G;
-        return e < n_tiles ? tiles[e] : kNoTile;
-    };
-    uint32_t cur = tile_at(0);
-    if (cur == kNoTile) return;  // (uniform)
-    const uint32_t wb = wave & 3, lane16 = lane * 16, smem_lds = lds_addr(smem);
-    const int8_t *digf = planes + digf_offset(NP);
-    // this wave's 1 KB code block per stage (pair_mfma_kernel's issue)
-    auto issue = [&](uint32_t tile, uint32_t grp, uint32_t buf) {
-        const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
-        const uint32_t g = wb < 2 ? 2 * ta + wb : 2 * tb + (wb - 2);
-        const uint32_t kb0 = grp * KG;
-        const uint8_t *base = (wb < 2 ? frag : frag_b) + ((size_t)g * NKB + kb0) * 1024;
-        const uint32_t gb = smem_lds + buf * KGB;
-#pragma unroll
-        for (int st = 0; st < KG; ++st)
-            if (kb0 + st < NKB) glds16_s(base + st * 1024, lane16, gb + st * kStageCodes + wb * 1024);
-        if (wave == 0) glds16_s(digf + digf_stage(kb0), lane16, gb + KG * kStageCodes);
-    };
-    if (tid == 0) sMask[0] = sMask[1] = 0ull;  // (published by the first group barrier)
-    issue(cur, 0, 0);
-    const uint32_t g4 = lane >> 4, so = g4 >> 1, hh = g4 & 1;
-    const uint32_t lrow = so * kStageCodes + (32 * hh + (lane & 15)) * 16;
-    const uint32_t offA = lrow + (wb >> 1) * 1024 + (wb & 1) * 256, offB = lrow + 2048;
-    const uint32_t offP = KG * kStageCodes + so * kDigStage + hh * 16 + 32 * (plane_idx & 3);
-    const float thr_c = thr * (1.0f - 0x1p-7f), R2 = 2.0f * sc.Rf;
-    uint32_t p_a0 = 0, p_b0 = 0, j = 0, buf = 0;
-    uint64_t p_okA = 0, p_okB = 0;
-    bool has_prev = false;
-    unsigned m = 0;
-    auto part = [&](const Acc &prev, int p, uint32_t kb) {
-        auto u = prev.raw(0, 2 * p), v = prev.raw(1, 2 * p), x = prev.raw(0, 2 * p + 1), y = prev.raw(1, 2 * p + 1);
-        asm("" : "+v"(u.x), "+v"(u.y), "+v"(v.x), "+v"(v.y) : "s"(kb));
-        asm("" : "+v"(x.x), "+v"(x.y), "+v"(y.x), "+v"(y.y) : "s"(kb));
-        const int2 mg = r2_screen_margin_xy2((wld_f2){(float)u.x, (float)x.x}, (wld_f2){(float)u.y, (float)x.y},
-                                             (wld_f2){(float)v.x, (float)y.x}, (wld_f2){(float)v.y, (float)y.y}, R2,
-                                             thr_c, sc.E, sc.mloc);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int i = 2 * p + q;
-            const uint32_t al = Acc::a_local(i, wave, lane), bl = Acc::b_local(i, wave, lane);
-            const bool valid = ((p_okB >> bl) & 1) && p_a0 + al < p_b0 + bl && ((p_okA >> al) & 1);
-            m |= ((q ? mg.y : mg.x) > 0 && valid ? 1u : 0u) << sub_block<Acc>(i, wave, lane);
-        }
-    };
-    auto verdict = [&]() {
-        if (has_prev && m) atomicOr(&sMask[(j - 1) & 1], (unsigned long long)m);
-        __syncthreads();
-        if (has_prev)
-            screen_verdict((uint32_t)sMask[(j - 1) & 1], p_a0 / kTile, p_b0 / kTile, tid, n_chunk_rows, o, sc);
-    };
-    auto step = [&](Acc &acc, const Acc &prev) -> bool {
-        const uint32_t next = tile_at(j + 1);
-        const uint32_t ta = cur >> 16, tb = cur & 0xFFFFu;
-        zero_acc(acc);
-        m = 0;
-        for (uint32_t g0 = 0; g0 < n_groups; g0 += 4) {
-#pragma unroll
-            for (int gg = 0; gg < 4; ++gg) {
-                const uint32_t grp = g0 + gg;
-                if (grp < n_groups) {  // (uniform)
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __builtin_amdgcn_s_barrier();
-                    asm volatile("" ::: "memory");
-                    if (grp == 0 && tid == 0) sMask[j & 1] = 0ull;  // (tile j - 2's verdict has been read)
-                    if (grp + 1 < n_groups)
-                        issue(cur, grp + 1, buf ^ 1);
-                    else if (next != kNoTile)
-                        issue(next, 0, buf ^ 1);
-                    const uint8_t *gb = smem + buf * KGB;
-                    const uint32_t n_st = min((uint32_t)KG, NKB - grp * KG);
-#pragma unroll
-                    for (int h = 0; h < KG / 2; ++h) {
-                        if ((uint32_t)(2 * h) < n_st) {  // (n_st is even: NP is a multiple of 64)
-                            const uint8_t *sc_ = gb + 2 * h * kStageCodes;
-                            const uint8_t *sd = gb + 2 * h * kDigStage;
-                            const v4i ca = *reinterpret_cast<const v4i *>(sc_ + offA);
-                            v4i cb[4];
-#pragma unroll
-                            for (int n = 0; n < 4; ++n)
-                                cb[n] = *reinterpret_cast<const v4i *>(sc_ + offB + (n >> 1) * 1024 + (n & 1) * 256);
-                            v4i dp[1];
-                            dp[0] = *reinterpret_cast<const v4i *>(sd + offP);
-                            mfma_block_sel16<1, 4>(acc.v, ca, cb, dp);
-                        }
-                        part(prev, 2 * gg + h, grp);  // (again in later blocks of four groups: the same bits)
-                    }
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    buf ^= 1;
-                }
-            }
-        }
-#pragma unroll
-        for (int gg = 0; gg < 4; ++gg)
-            if ((uint32_t)gg >= n_groups) {  // (fewer than four groups)
-                part(prev, 2 * gg, 0u);
-                part(prev, 2 * gg + 1, 0u);
-            }
-        verdict();
-        p_a0 = ta * kTile;
-        p_b0 = tb * kTile;
-        p_okA = ok_bits[ta];
-        p_okB = ok_bits[tb];
-        has_prev = true;
-        ++j;
-        cur = next;
-        return next != kNoTile;
-    };
-    Acc accA, accB;
-    zero_acc(accB);
-    for (;;) {
-        const bool more = step(accA, accB);
-        accB = accA;  // (tile j's sums become the previous tile's)
-        if (!more) {
-            m = 0;
-#pragma unroll
-            for (int p = 0; p < 8; ++p) part(accB, p, 0u);
-            verdict();
-            break;
-        }
     }
 }
 
@@ -1448,12 +1294,7 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     sc.f32 = m.nonneg ? (m.NP <= kScrF32MaxNP ? 2 : m.NP <= kScreenF32MaxNP ? 1 : 0) : 0;
     // every doubled one-plane T <= 2 sum_k |d_top,k| <= 256 NP <= 2^22 (exact in f32)
     if (sc.f32 == 2) screen_consts((float)(2 * m.dsum[top]), 2.0f * sc.Rf, sc.E, sc.mloc);
-    if (WLD_I8_PIPE && sc.f32 == 2)  // (persistent workgroups along the XCD-ordered list)
-        hipLaunchKernelGGL(pair_i8_pipe_kernel, dim3(std::min<uint32_t>(m.n_tiles, kI8PipeGrid)), dim3(256), 0, s,
-                           m.frag, m.frag_b, m.wplanes, ok_bits, m.tiles, m.n_tiles, m.NP, m.n_chunk_rows, m.thr, top,
-                           o, sc);
-    else
-        launch_lds<kModeScreen, 1>(m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, top, o, dn, sc, s);
+    launch_lds<kModeScreen, 1>(m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, top, o, dn, sc, s);
     if (screen_done) (void)hipEventRecord(screen_done, s);
     launch_candidates(m, n, idx, ok_bits, o, dn, sc, s);
     return true;
