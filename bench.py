@@ -14,7 +14,7 @@ With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts its
 own N ranks (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE set) before
 anything touches torch or the GPU, and relays rank 0's line; under torchrun
 WORLD_SIZE must equal --gpus.  Rank 0 prints ONE JSON line.  The CPU baseline
-(rank 0, at every N, after the timed region) is the C restatement of the
+(rank 0 at N=1, after the timed region; null at N>1) is the C restatement of the
 lib.rs simd path (oracle/wld_oracle.c, "port"), threaded like rayon over
 256x256 chunks, timed on a bounded sample of the same workload.
 """
@@ -777,7 +777,11 @@ def main():
         out["steps_check"] = {"steps": len(checked), "equal_to_oracle": equal, "rows_per_step": len(ref["site_a"]),
                               "compare": "bitwise" if args.ref_sums else "within 1e-5"}
         assert equal == len(checked) == args.check_steps, out["steps_check"]
-    if not args.no_cpu_baseline:
+    if world > 1:
+        # the CPU baseline is an N=1 figure (rank 0 of a single-GPU run); an
+        # N>1 line checks its rows with --check-steps instead
+        out["cpu_baseline"] = None
+    elif not args.no_cpu_baseline:
         oref, ochunks, out["cpu_baseline"] = cpu_baseline(buf, weights, thr, args.cpu_seconds)
         # the same chunks on the GPU: rows against the oracle's (lib.rs
         # semantics).  Exact sums rounded once may put a pair whose r2 lies
