@@ -166,7 +166,7 @@ struct wld_ctx {
     bool screened2 = false; // ... on two digit planes
     uint64_t rows = 0;
     // the gather goes into the stream behind the scan, before the host has
-    // seen the row count, when the previous run had rows (WLD_SPEC_GATHER):
+    // seen the row count, when the previous run had rows:
     // no host round trip between scan and gather; gather_cap: the output
     // rows the enqueued gather may write (0: none enqueued)
     bool spec_gather = false;
@@ -1146,7 +1146,7 @@ int enqueue_pass(wld_ctx *c) {
     }
     HIP_TRY(hipEventRecord(c->ev[4], c->stream));
     c->gather_cap = 0;
-    if (WLD_SPEC_GATHER && c->spec_gather && lin_count) {
+    if (c->spec_gather && lin_count) {
         // outputs for a quarter more rows than the last run's (the scan's
         // count decides; more than that and run_complete gathers again)
         const uint64_t cap = std::min<uint64_t>(c->st_capacity, c->rows + c->rows / 4 + 4096);

@@ -203,18 +203,6 @@ constexpr uint32_t kCandidateGrid = 2048;
 constexpr uint32_t kRefCandidateGrid = 768;
 // ... and of its items (ref_item_kernel<LOOP>, one sub-block per wave: four per CU)
 constexpr uint32_t kRefItemGrid = 1024;
-// lib.rs's order on f32 MFMA in work items of one sub-block per wave: the
-// candidate launch after a screen, and full runs of few tiles (0: whole
-// 64x64 tiles per workgroup, the round-3 shape; A/B builds only)
-#ifndef WLD_REF_ITEMS
-#define WLD_REF_ITEMS 1
-#endif
-// the reference-order gather enqueued behind the scan when the previous run
-// had rows (capi.hip enqueue_pass; 0: after the host has read the row count,
-// the round-3 order; A/B builds only)
-#ifndef WLD_SPEC_GATHER
-#define WLD_SPEC_GATHER 1
-#endif
 // ... and of ref_sums_kernel / ref_compact_kernel (low-register: eight per CU)
 constexpr uint32_t kRefRowsGrid = 2048;
 

@@ -913,11 +913,6 @@ struct AccF6 {
 #ifndef WLD_FP6_WG
 #define WLD_FP6_WG 4  // workgroups per CU
 #endif
-// diagnostic builds (wrong results, timing only): 1 no epilogue, 2 also every
-// stage's copy from the first stage, 3 also no MFMA
-#ifndef WLD_FP6_DIAG
-#define WLD_FP6_DIAG 0
-#endif
 __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const uint8_t *__restrict__ a6,
                                                                   const uint8_t *__restrict__ b4,
                                                                   const uint64_t *__restrict__ ok_bits,
@@ -940,7 +935,6 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     const uint8_t *sB = b4 + (size_t)(4 * tb + wave) * NK * kF6BBytes;
     auto issue = [&](uint32_t kb, uint32_t buf) {
         const uint32_t gb = lds + buf * kF6Stage;
-        if (WLD_FP6_DIAG >= 2) kb = 0;  // (diagnostic: every stage from the first, cache-resident)
         const uint8_t *a = sA + (size_t)kb * kF6ABytes;
         glds16_s(a, lane16, gb + wave * kF6ABytes);
         glds16_s(a + 1024, lane16, gb + wave * kF6ABytes + 1024);
@@ -978,10 +972,6 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
             constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
             const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
             const v8i bmin = {(int)r.x & kMinor, (int)r.y & kMinor, (int)r.z & kMinor, (int)r.w & kMinor, 0, 0, 0, 0};
-            if (WLD_FP6_DIAG == 3) {  // (diagnostic: no MFMA, the operands consumed)
-                acc.v[n][0][0][0] += (float)(ai[0] ^ am[5] ^ braw[n] ^ bmin[3]);
-                continue;
-            }
             acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, braw, acc.v[n][0][0], 2, 4, 0,
                                                                               0x7F7F7F7F, 0, 0x7F7F7F7F);
             acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc.v[n][0][1], 2, 4, 0,
@@ -1030,14 +1020,6 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
         return ((double)p.x + (y ? -(double)p.y : (double)p.y)) * 0.5;
     };
     const DenseArgs dn{nullptr, nullptr, nullptr, nullptr};
-    if (WLD_FP6_DIAG) {  // (diagnostic: no epilogue; the sums kept live, the tile rejected)
-        float t = 0.0f;
-#pragma unroll
-        for (int i = 0; i < AccF6::kPairs; ++i) t += acc.raw(0, i).x + acc.raw(1, i).y;
-        if (t == -1.0f) sBits[0] = 1;
-        screen_verdict(0u, ta, tb, tid, n_chunk_rows, o, sc);
-        return;
-    }
     tile_epilogue<kModeScreen, AccF6>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, 0, o, dn, sc, sBits,
                                       sRowBase);
 }
@@ -1244,7 +1226,7 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     sc.scan = m.scan;  // from here on a screen runs (and a candidate launch after it)
     // lib.rs's order on the f32 kernel: candidates as 16-row-block items
     // (buckets 0-3 of capacity 4 n_tiles: the 16 n_tiles list entries)
-    if (WLD_REF_ITEMS && m.ref_valu && !m.ref_valu->safe) {
+    if (m.ref_valu && !m.ref_valu->safe) {
         sc.rb_items = 1;
         sc.cand_cap = 4 * m.n_tiles;
     }

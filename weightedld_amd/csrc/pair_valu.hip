@@ -63,11 +63,6 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 // ty + 16i), so the epilogue and compaction only change how a row slot maps
 // to a.  The VALU's code extraction then overlaps the matrix pipe instead of
 // competing with the FMAs for VALU issue.
-// the reference-order item kernel: ref_item_kernel (1) or the LDS-staged
-// one-slot pair_valu_kernel (0; A/B builds)
-#ifndef WLD_REF_ITEM_KERNEL
-#define WLD_REF_ITEM_KERNEL 1
-#endif
 #ifndef WLD_VALU_MF_WG
 #define WLD_VALU_MF_WG 2  // MF: 164 VGPRs would fit 3 per CU; measured equal
 #endif
@@ -517,9 +512,6 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_
         __shared__ uint32_t s_next, s_pre[17];
         if constexpr (NS == 1) cand_prefix(tile_buckets, s_pre);
         const uint32_t nt = NS == 1 ? s_pre[16] : (*tile_count & kAbandonBit) ? 0u : *tile_count;
-#ifndef WLD_CAND_MIX
-#define WLD_CAND_MIX 1
-#endif
         // first items: the list is heaviest first and the dispatcher deals
         // workgroups i, i + m, i + 2m, ... (m = grid / R, R resident per CU)
         // to one CU, so that CU would start R of the heaviest items at once
@@ -527,7 +519,7 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_
         // instead (j, 2m - 1 - j, 2m + j, ...), heavy next to light (a
         // permutation of [0, grid))
         uint32_t first = blockIdx.x;
-        if (WLD_CAND_MIX && tile_buckets) {
+        if (tile_buckets) {
             constexpr uint32_t R = NS == 1 ? WLD_VALU_REF1L_WG : WLD_VALU_REF_WG;
             const uint32_t m = gridDim.x / R, k = m ? blockIdx.x / m : R, j = blockIdx.x - (k < R ? k * m : 0u);
             if (k < R) first = (k & 1) ? (k + 1) * m - 1 - j : k * m + j;
@@ -594,11 +586,8 @@ __global__ __launch_bounds__(256) void ref_layout_kernel(const uint8_t *__restri
 // LOOP: the candidate launch over the screen's item list (buckets, work
 // counter, fused chunk scan); else the full run's tiles in four 16-row items
 // each (workgroup 4t + q: tile t's row block q).
-// the item kernel's operands: byte converts of masked code dwords (1) or
-// per-element selects (0, A/B builds)
-#ifndef WLD_ITEM_CVT
-#define WLD_ITEM_CVT 1
-#endif
+// the item kernel's operands: byte converts of masked code dwords (per-element
+// selects were 8.5% slower at C2, DESIGN Appendix A)
 // byte e of x as a float by v_cvt_f32_ubyte<e> (no shift or mask first; the
 // compiler's own lowering extracts the byte first).  Inline asm is invisible
 // to the hazard recognizer as a VALU write: a result that an MFMA reads
@@ -628,7 +617,7 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
     return r;
 }
 #ifndef WLD_REF_ITEM_WG
-#define WLD_REF_ITEM_WG 5  // workgroups per CU, full runs (<= 102 VGPRs, no spill)
+#define WLD_REF_ITEM_WG 5  // workgroups per CU, full runs (<= 102 VGPRs; two spill, outside the loop)
 #endif
 #ifndef WLD_REF_ITEML_WG
 #define WLD_REF_ITEML_WG 4  // ... the candidate loop (its loop state: <= 128 VGPRs)
@@ -710,28 +699,16 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
 #pragma unroll
                 for (int grp = 0; grp < 4; ++grp) {
                     const float we[4] = {Wt[grp].x, Wt[grp].y, Wt[grp].z, Wt[grp].w};
-#if WLD_ITEM_CVT
                     // the four elements' in / major bits as bytes 0/1 (one mask
                     // per dword), each turned into 0.0/1.0 by a byte convert
                     const uint32_t ai = A[grp] & 0x01010101u, am = (A[grp] >> 1) & 0x01010101u;
                     const uint32_t bi = B[grp] & 0x01010101u, bm = (B[grp] >> 1) & 0x01010101u;
-#endif
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-#if WLD_ITEM_CVT && !defined(WLD_DIAG_NOSEL)
                         // w x 1.0 or w x 0.0: exact; a -0.0 term (negative w
                         // masked) adds nothing to a chain that starts at +0.0
                         const float u = we[e] * cvt_ubyte<0>(ai, e), v = we[e] * cvt_ubyte<0>(am, e);
                         const float fi = cvt_ubyte<1>(bi, e), fm = cvt_ubyte<1>(bm, e);
-#else
-                        const uint32_t xa = A[grp] >> (8 * e), xb = B[grp] >> (8 * e);
-#ifndef WLD_DIAG_NOSEL
-                        const float u = (xa & kCodeIn) ? we[e] : 0.0f, v = (xa & kCodeMaj) ? we[e] : 0.0f;
-                        const float fi = (float)(xb & 1u), fm = (float)((xb >> 1) & 1u);
-#else  // diagnostic (wrong sums): the operands without their selects and converts
-                        const float u = we[e], v = __uint_as_float(xa), fi = __uint_as_float(xb), fm = we[e];
-#endif
-#endif
                         acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fi, acc[0], 0, 0, 0);
                         acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fi, acc[1], 0, 0, 0);
                         acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fm, acc[2], 0, 0, 0);
@@ -1111,9 +1088,6 @@ bool launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
             else launch_v<true, false, true, true, false>(v, grid, flush, cs, o, dn, s);
         } else if (v.tile_count) {
             if (v.safe) launch_v<false, true, false, true, true>(v, grid, flush, cs, o, dn, s);
-            else if (v.rb_items && !WLD_REF_ITEM_KERNEL)
-                launch_v<false, false, true, true, true, 1>(v, std::min<uint32_t>(4 * v.n_tiles, 1280u), flush, cs, o,
-                                                             dn, s);
             else if (v.rb_items)  // items of <= 4 sub-blocks, one per wave, no LDS staging
                 hipLaunchKernelGGL(ref_item_kernel<true>, dim3(std::min<uint32_t>(4 * v.n_tiles, kRefItemGrid)),
                                    dim3(256), 0, s, v.codes, v.w, v.site_ok, v.tiles, v.n_tiles, v.tile_bits,
@@ -1125,9 +1099,7 @@ bool launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
             // resident workgroups (BASELINE config 2: 528 tiles), each tile's
             // four 16-row blocks are separate work items (f32 MFMA path)
             if (v.safe) launch_v<false, true, false, true, false>(v, grid, flush, cs, o, dn, s);
-            else if (WLD_REF_ITEMS && !WLD_REF_ITEM_KERNEL && v.n_tiles <= 4 * kRefCandidateGrid)
-                launch_v<false, false, true, true, false, 1>(v, grid, flush, cs, o, dn, s, 4);
-            else if (WLD_REF_ITEMS && v.n_tiles <= 4 * kRefCandidateGrid) {
+            else if (v.n_tiles <= 4 * kRefCandidateGrid) {
                 // (the run's chunk scan in the last workgroup when given)
                 hipLaunchKernelGGL(ref_item_kernel<false>, dim3(4 * grid), dim3(256), 0, s, v.codes, v.w, v.site_ok,
                                    v.tiles, v.n_tiles, nullptr, nullptr, nullptr, 0u, v.L, v.NP, cs, v.ref_tail_n,
