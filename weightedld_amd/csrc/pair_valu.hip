@@ -69,26 +69,14 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 #ifndef WLD_VALU_REF_WG
 #define WLD_VALU_REF_WG 3  // MF + REF: three workgroups per CU (<= 168 VGPRs; 2 leave 208)
 #endif
-#ifndef WLD_VALU_REF1_WG
-#define WLD_VALU_REF1_WG 6  // MF + REF, one slot per wave: six workgroups per CU (<= 85 VGPRs)
-#endif
-#ifndef WLD_VALU_REF1L_WG
-#define WLD_VALU_REF1L_WG 5  // ... the candidate loop (its loop state: <= 102 VGPRs, no spill)
-#endif
-// NS: 16x16 slots per wave (4: a whole 64x64 tile per workgroup; 1, MF +
-// REF only: one 16-row block of a tile per workgroup, one sub-block per wave —
-// a quarter of the accumulators, so more workgroups fit a CU)
-template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP, int NS = 4>
-__global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_WG : WLD_VALU_REF1_WG)
-                                                                : WLD_VALU_REF_WG)
-                                              : WLD_VALU_MF_WG)
-                                     : 2) void pair_valu_kernel(
+template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
+__global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) : 2) void pair_valu_kernel(
     const uint8_t *__restrict__ codes, const float *__restrict__ w, const uint8_t *__restrict__ site_ok,
     const uint32_t *__restrict__ tiles, uint32_t n_tiles, const unsigned *tile_count,
     const uint32_t *__restrict__ tile_bits, unsigned *tile_work, const unsigned *tile_buckets, uint32_t bucket_cap,
     uint32_t L, uint32_t NP, uint32_t flush,
-    uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, uint32_t split, OrderArgs o, DenseArgs dn,
-    ScanArgs sa) {
+    uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, OrderArgs o, DenseArgs dn, ScanArgs sa) {
+    constexpr int NS = 4;  // 16x16 slots per wave: a whole 64x64 tile per workgroup
     __shared__ __attribute__((aligned(16))) uint8_t sA[kTile * kStride];
     __shared__ __attribute__((aligned(16))) uint8_t sB[kTile * kStride];
     __shared__ __attribute__((aligned(16))) float sW[64];
@@ -104,7 +92,6 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_
         const uint32_t a0 = ta * kTile, b0 = tb * kTile;
         const uint32_t tx = tid & 15, ty = tid >> 4;
 
-        static_assert(NS == 4 || (MF && REF), "one slot per wave: the f32 MFMA reference-order path only");
         float acc[4][4][4], tot[4][NS][4];
         v4f accM[NS][4];  // MF: [slot j][sum q], element e = a row slot
         // MF + REF: the computed sub-blocks dealt over the waves.  In
@@ -151,18 +138,6 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_
         const uint32_t lr = tid >> 2, part = tid & 3;  // loader: site row, 16-byte part
         const uint8_t *gA = codes + (size_t)(a0 + lr) * NP + part * 16;
         const uint8_t *gB = codes + (size_t)(b0 + lr) * NP + part * 16;
-        // only the a rows of row blocks and the b rows of column blocks that
-        // hold a computed sub-block are staged (the other LDS rows are never read)
-        // (NS = 1 items; a whole-tile workgroup stages every row)
-        uint32_t rows_used = 0xFu, cols_used = 0xFu;
-        if constexpr (NS == 1) {
-            rows_used = cols_used = 0;
-            for (uint32_t q = 0; q < 4; ++q) {
-                rows_used |= ((bits >> (4 * q)) & 0xFu) ? 1u << q : 0u;
-                cols_used |= (bits >> (4 * q)) & 0xFu;
-            }
-        }
-        const bool ldA = NS != 1 || ((rows_used >> (lr >> 4)) & 1u), ldB = NS != 1 || ((cols_used >> (lr >> 4)) & 1u);
 
         // one 64-sequence stage of both panels' codes and the weights: fetch
         // (global loads into registers, issued a stage ahead so that their
@@ -170,20 +145,20 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_
         // PF: the fetch a stage ahead; a whole tile per workgroup in lib.rs's
         // order has no registers to spare for it (it would spill), and fetches
         // each stage just before storing it
-        constexpr bool PF = !(REF && NS == 4);
+        constexpr bool PF = !REF;
         uint4 va, vb;
         float wv;
         auto fetch_stage = [&](uint32_t k0) {
-            if (ldA) va = *reinterpret_cast<const uint4 *>(gA + k0);
-            if (ldB) vb = *reinterpret_cast<const uint4 *>(gB + k0);
+            va = *reinterpret_cast<const uint4 *>(gA + k0);
+            vb = *reinterpret_cast<const uint4 *>(gB + k0);
             wv = tid < 64 ? w[k0 + tid] : 0.0f;
         };
         auto store_stage = [&]() {
             __syncthreads();
             uint32_t *pa = reinterpret_cast<uint32_t *>(sA + lr * kStride + part * 16);
             uint32_t *pb = reinterpret_cast<uint32_t *>(sB + lr * kStride + part * 16);
-            if (ldA) pa[0] = va.x, pa[1] = va.y, pa[2] = va.z, pa[3] = va.w;
-            if (ldB) pb[0] = vb.x, pb[1] = vb.y, pb[2] = vb.z, pb[3] = vb.w;
+            pa[0] = va.x, pa[1] = va.y, pa[2] = va.z, pa[3] = va.w;
+            pb[0] = vb.x, pb[1] = vb.y, pb[2] = vb.z, pb[3] = vb.w;
             if (tid < 64) sW[tid] = wv;
             __syncthreads();
         };
@@ -494,12 +469,9 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_
     };
 
     if constexpr (!LOOP) {
-        // split 4 (REF, few tiles): workgroup 4t + q computes tile t's 16-row
-        // block q (its four 16x16 sub-blocks, one per wave) — four times the
-        // work items where one tile per workgroup would leave CUs idle
-        const uint32_t tile = tiles[blockIdx.x / split], q = blockIdx.x % split;
+        const uint32_t tile = tiles[blockIdx.x];
         if (tile != kNoTile)  // kNoTile: padding of an XCD-ordered list
-            compute_tile(tile, threadIdx.x, split == 1 ? 0xFFFFu : 0xFu << (4 * q), split == 1 ? 0xFu : 1u << q);
+            compute_tile(tile, threadIdx.x, 0xFFFFu, 0xFu);
     } else {
         // (the list entries come from the screen's atomics: each is checked —
         // bucket slot, then the tile — before anything is read through it)
@@ -507,11 +479,8 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_
         // (tile_work, zeroed by the screen): the workgroups that finish first
         // take the list's tail, not fixed ones (tiles differ in their computed
         // sub-blocks)
-        // NS = 1: the list holds 16-row-block items (the screen's rb_items),
-        // as many as the buckets count; each owns its row block's segments
         __shared__ uint32_t s_next, s_pre[17];
-        if constexpr (NS == 1) cand_prefix(tile_buckets, s_pre);
-        const uint32_t nt = NS == 1 ? s_pre[16] : (*tile_count & kAbandonBit) ? 0u : *tile_count;
+        const uint32_t nt = (*tile_count & kAbandonBit) ? 0u : *tile_count;
         // first items: the list is heaviest first and the dispatcher deals
         // workgroups i, i + m, i + 2m, ... (m = grid / R, R resident per CU)
         // to one CU, so that CU would start R of the heaviest items at once
@@ -520,22 +489,17 @@ __global__ __launch_bounds__(256, MF ? (REF ? (NS == 1 ? (LOOP ? WLD_VALU_REF1L_
         // permutation of [0, grid))
         uint32_t first = blockIdx.x;
         if (tile_buckets) {
-            constexpr uint32_t R = NS == 1 ? WLD_VALU_REF1L_WG : WLD_VALU_REF_WG;
+            constexpr uint32_t R = WLD_VALU_REF_WG;
             const uint32_t m = gridDim.x / R, k = m ? blockIdx.x / m : R, j = blockIdx.x - (k < R ? k * m : 0u);
             if (k < R) first = (k & 1) ? (k + 1) * m - 1 - j : k * m + j;
         }
-        if (NS != 1 && tile_buckets && first < nt) cand_prefix(tile_buckets, s_pre);  // (a workgroup without a tile skips it)
+        if (tile_buckets && first < nt) cand_prefix(tile_buckets, s_pre);  // (a workgroup without a tile skips it)
         for (uint32_t bi = first; bi < nt;) {
             const uint32_t e = tile_buckets ? cand_entry_checked(o, s_pre, bucket_cap, bi) : bi < n_tiles ? bi : ~0u;
             const uint32_t tile = e != ~0u ? tiles[e] : kNoTile;
             const uint32_t bits = tile_bits ? tile_bits[e] : 0xFFFFu;
-            uint32_t owned = 0xFu;  // a whole-tile entry writes all 64 rows' segments
-            if constexpr (NS == 1) {
-                owned = 0;
-                for (uint32_t q = 0; q < 4; ++q) owned |= ((bits >> (4 * q)) & 0xFu) ? 1u << q : 0u;
-            }
-            if (tile_in_range(tile, L) && (NS != 1 || __popc(bits) <= 4))
-                compute_tile(tile, threadIdx.x, bits, owned);
+            if (tile_in_range(tile, L))
+                compute_tile(tile, threadIdx.x, bits, 0xFu);  // (a whole-tile entry writes all 64 rows' segments)
             else if (e != ~0u && threadIdx.x == 0)
                 report_guard(o, kGuardTile);
             if (threadIdx.x == 0) s_next = gridDim.x + atomicAdd(tile_work, 1u);
@@ -1064,12 +1028,12 @@ void launch_ref_layout(const uint8_t *codes, const float *w_pad, size_t LP, size
 }
 
 namespace {
-template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP, int NS = 4>
+template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
 void launch_v(const ValuLaunch &v, uint32_t grid, uint32_t flush, uint32_t cs, const OrderArgs &o,
-              const DenseArgs &dn, hipStream_t s, uint32_t split = 1) {
-    hipLaunchKernelGGL((pair_valu_kernel<DENSE, SAFE, MF, REF, LOOP, NS>), dim3(grid * split), dim3(256), 0, s, v.codes, v.w,
+              const DenseArgs &dn, hipStream_t s) {
+    hipLaunchKernelGGL((pair_valu_kernel<DENSE, SAFE, MF, REF, LOOP>), dim3(grid), dim3(256), 0, s, v.codes, v.w,
                        v.site_ok, v.tiles, v.n_tiles, v.tile_count, v.tile_bits, v.tile_work, v.tile_buckets,
-                       v.bucket_cap, v.L, v.NP, flush, cs, v.ref_tail_n, v.n_chunk_rows, v.thr, split, o, dn, v.scan);
+                       v.bucket_cap, v.L, v.NP, flush, cs, v.ref_tail_n, v.n_chunk_rows, v.thr, o, dn, v.scan);
 }
 }  // namespace
 
