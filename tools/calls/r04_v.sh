@@ -7,4 +7,6 @@ tools/gpu_step.sh 700 $out/gpu_tests.txt python -u -m pytest -v --timeout 300 --
 tools/gpu_step.sh 120 $out/smoke.txt python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit $?
 tools/gpu_step.sh 200 $out/bench_c4.log python bench.py || exit $?
 tools/gpu_step.sh 200 $out/prof_c4.log rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof_c4 -o c4 -- python3 bench.py --no-cpu-baseline || exit $?
+tools/gpu_step.sh 200 $out/bench_ldb.log python bench.py --data ldblocks --no-cpu-baseline || exit $?
+tools/gpu_step.sh 150 $out/bench_c2.log python bench.py --config c2 --no-cpu-baseline || exit $?
 echo done
