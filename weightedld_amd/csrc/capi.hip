@@ -483,9 +483,6 @@ void rows_to_linear(uint32_t n, uint32_t rb, uint32_t re, uint32_t &lb, uint32_t
 // L2 instead of 1.11 GB with kS = 8, step -0.5% (archive/profiles_r01_r03/r03ar, r03as,
 // r03au).  Otherwise kS = 8, two whole super-blocks resident (C5, 323 KB
 // columns: 3% faster than 16).
-#ifndef WLD_XCD_SUPER
-#define WLD_XCD_SUPER 0  // super-block side in tiles (0: by the L2 footprint as above; A/B builds)
-#endif
 std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t, uint32_t kS) {
     constexpr uint32_t kX = 8;
     std::vector<std::vector<uint32_t>> blocks;
@@ -546,7 +543,7 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
                 t.push_back((ta << 16) | tb);
     }
     std::sort(t.begin(), t.end());
-    const uint32_t kS = WLD_XCD_SUPER ? WLD_XCD_SUPER : 24ull * kTile * c->NP <= (4ull << 20) ? 16u : 8u;
+    const uint32_t kS = 24ull * kTile * c->NP <= (4ull << 20) ? 16u : 8u;
     // only with many rounds of resident tiles: whole super-blocks per XCD
     // leave up to one super-block of imbalance (C2's 528 tiles: +14%)
     if (!c->opt_tile_rows && t.size() >= 4096 && T_used < 65535) t = xcd_order(t, kS);
