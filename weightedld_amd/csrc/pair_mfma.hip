@@ -913,21 +913,6 @@ struct AccF6 {
 #ifndef WLD_FP6_WG
 #define WLD_FP6_WG 4  // workgroups per CU
 #endif
-// A/B: wave w computes a rows 32 (w >> 1).. against b columns 32 (w & 1)..
-// (two A blocks x two B blocks) instead of 16 rows x 64 columns: half the B
-// minor-bit masks per wave for a third more A reads from LDS
-#ifndef WLD_FP6_2X2
-#define WLD_FP6_2X2 0
-#endif
-struct AccF6q : AccF6 {  // block n = 2 ra + nb: a rows 32 (w >> 1) + 16 ra, b columns 32 (w & 1) + 16 nb
-    static __device__ __forceinline__ uint32_t a_local(int i, uint32_t wave, uint32_t lane) {
-        return 32 * ((wave >> 1) & 1) + 16 * ((i >> 2) >> 1) + 4 * (lane >> 4) + (i & 3);
-    }
-    static __device__ __forceinline__ uint32_t b_local(int i, uint32_t wave, uint32_t lane) {
-        return 32 * (wave & 1) + 16 * ((i >> 2) & 1) + (lane & 15);
-    }
-};
-using AccF6K = std::conditional_t<WLD_FP6_2X2 != 0, AccF6q, AccF6>;
 __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const uint8_t *__restrict__ a6,
                                                                   const uint8_t *__restrict__ b4,
                                                                   const uint64_t *__restrict__ ok_bits,
@@ -971,7 +956,7 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
         sBail = v;
     }
     const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
-    AccF6K acc;
+    AccF6 acc;
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
@@ -1018,47 +1003,14 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     for (uint32_t kb = 0; kb < NK; ++kb) {
         if (!stage_top(kb)) return;
         if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
-        auto a_block = [&](uint32_t r, v8i &ai, v8i &am) {  // row block r's (in, major) operands
-            const uint8_t *pa = smem + buf * kF6Stage + r * kF6ABytes + lane * 24;
-            const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
-                        i2 = *reinterpret_cast<const uint2 *>(pa + 16);
-            const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536),
-                        m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
-                        m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
-            ai = v8i{(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
-            am = v8i{(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
-        };
-        if constexpr (WLD_FP6_2X2 != 0) {
-            v8i ai[2], am[2], braw[2], bmin[2];
-            const uint32_t rh = wave >> 1, ch = wave & 1;
-#pragma unroll
-            for (int r = 0; r < 2; ++r) a_block(2 * rh + r, ai[r], am[r]);
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                const uint4 q = *reinterpret_cast<const uint4 *>(smem + buf * kF6Stage + kF6AStage +
-                                                                 (2 * ch + nb) * kF6BBytes + lane * 16);
-                constexpr int kMinor = 0x22222222;
-                braw[nb] = v8i{(int)q.x, (int)q.y, (int)q.z, (int)q.w, 0, 0, 0, 0};
-                bmin[nb] = v8i{(int)q.x & kMinor, (int)q.y & kMinor, (int)q.z & kMinor, (int)q.w & kMinor, 0, 0, 0, 0};
-            }
-#pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                const int r = n >> 1, nb = n & 1;
-                acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai[r], braw[nb], acc.v[n][0][0], 2, 4,
-                                                                                  0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
-                acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai[r], bmin[nb], acc.v[n][0][1], 2, 4,
-                                                                                  0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
-                acc.v[n][1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am[r], braw[nb], acc.v[n][1][0], 2, 4,
-                                                                                  0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
-                acc.v[n][1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am[r], bmin[nb], acc.v[n][1][1], 2, 4,
-                                                                                  0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
-        } else {
-            v8i ai, am;
-            a_block(wave, ai, am);
-            stage_mfma(buf, ai, am);
-        }
+        const uint8_t *pa = smem + buf * kF6Stage + wave * kF6ABytes + lane * 24;
+        const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
+                    i2 = *reinterpret_cast<const uint2 *>(pa + 16);
+        const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536), m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
+                    m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
+        const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
+        const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
+        stage_mfma(buf, ai, am);
         buf ^= 1;
     }
     // (the f64 fallback of pair_cand: exact sums from X, Y; the launch uses
@@ -1068,7 +1020,7 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
         return ((double)p.x + (y ? -(double)p.y : (double)p.y)) * 0.5;
     };
     const DenseArgs dn{nullptr, nullptr, nullptr, nullptr};
-    tile_epilogue<kModeScreen, AccF6K>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, 0, o, dn, sc, sBits,
+    tile_epilogue<kModeScreen, AccF6>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, 0, o, dn, sc, sBits,
                                       sRowBase);
 }
 
