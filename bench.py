@@ -157,7 +157,7 @@ def cpu_baseline(buf, w, thr, target_s=15.0, max_s=30.0):
     import _oracle as O  # checker / baseline only
 
     O.use_native()  # gcc -O3 -march=native on the measuring host
-    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    threads, share = host_cpu_share()
     L = buf.shape[0]
     n = (L + 255) // 256
     nchunks = n * (n + 1) // 2
@@ -190,7 +190,65 @@ def cpu_baseline(buf, w, thr, target_s=15.0, max_s=30.0):
     p, t = run(k2)
     return last["rows"], last["chunks"], {"value": p / t, "unit": "site-pairs/s", "cores": threads, "kind": "port",
             "sample": "%s = %d pairs in %.1f s; C restatement of the lib.rs simd path (8-lane f32, rayon-style "
-                      "chunk scheduling), gcc -O3 -march=native" % (what, p, t)}
+                      "chunk scheduling), gcc -O3 -march=native" % (what, p, t), "host_cpus": share}
+
+
+def fp6_rows_check(ctx, buf, w, L, N, thr):
+    """The fp6 screen forced (WLD_OPT_SCREEN_FP6 2: it completes, never
+    handing over to i8) over the whole workload at thr, its rows against the
+    oracle's bit for bit; the context's options are restored after."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _oracle as O  # checker only
+    O.use_native()
+    t0 = time.perf_counter()
+    ref = O.all_pairs(buf, w, np.float32(thr), n_threads=host_cpu_share()[0])
+    oracle_s = time.perf_counter() - t0
+    keep = ctx.get_option("screen_fp6")
+    ctx.set_option("screen_fp6", 2)
+    n = ctx.run_chunks(thr, 0, ctx.chunks(L))
+    st = ctx.stats()
+    g = ctx.rows()
+    ctx.set_option("screen_fp6", keep)
+    equal = n == len(ref["r2"]) and all(
+        np.array_equal(np.asarray(getattr(g, f)).astype(np.uint32), np.asarray(ref[f]).astype(np.uint32))
+        for f in ("site_a", "site_b")) and all(
+        np.array_equal(np.asarray(getattr(g, f), dtype=np.float32).view(np.uint32),
+                       np.asarray(ref[f], dtype=np.float32).view(np.uint32)) for f in ("d", "d_prime", "r2"))
+    return {"thr": thr, "gpu_rows": n, "oracle_rows": int(len(ref["r2"])), "equal": bool(equal),
+            "screen_fp6": st["screen_fp6"], "candidate_tiles": st["candidate_tiles"], "tiles": st["tiles"],
+            "oracle_s": oracle_s}
+
+
+def host_cpu_share():
+    """The threads the CPU baseline runs on: every CPU this process may use
+    (rayon's default is all logical cores, lib.rs:635-637) — its affinity set,
+    capped by a cgroup CPU quota when one is set (a leased share of a larger
+    host: os.cpu_count() then counts CPUs the process cannot get).  Returns
+    (threads, the figures that decided it)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):  # cgroup v2: "<quota> <period>" or "max <period>"
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:  # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    threads = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    why = ("affinity set" if quota is None or threads == aff else "cgroup CPU quota (below the affinity set)")
+    return threads, {"os_cpu_count": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota,
+                     "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"), "threads_from": why}
 
 
 def load_traffic(config, kernel):
@@ -777,12 +835,14 @@ def main():
         out["steps_check"] = {"steps": len(checked), "equal_to_oracle": equal, "rows_per_step": len(ref["site_a"]),
                               "compare": "bitwise" if args.ref_sums else "within 1e-5"}
         assert equal == len(checked) == args.check_steps, out["steps_check"]
-    if world > 1:
-        # the CPU baseline is an N=1 figure (rank 0 of a single-GPU run); an
-        # N>1 line checks its rows with --check-steps instead
+    if args.no_cpu_baseline:
         out["cpu_baseline"] = None
-    elif not args.no_cpu_baseline:
-        oref, ochunks, out["cpu_baseline"] = cpu_baseline(buf, weights, thr, args.cpu_seconds)
+    else:
+        # rank 0 (at N>1 after the other ranks have left: no rank polls beside
+        # it), a bounded sample at N>1 so that a scaling run stays short
+        oref, ochunks, out["cpu_baseline"] = cpu_baseline(buf, weights, thr, args.cpu_seconds if world == 1 else
+                                                          min(args.cpu_seconds, 5.0),
+                                                          max_s=30.0 if world == 1 else 8.0)
         # the same chunks on the GPU: rows against the oracle's (lib.rs
         # semantics).  Exact sums rounded once may put a pair whose r2 lies
         # within 1e-5 of the threshold on the other side of the strict '>'
@@ -803,6 +863,12 @@ def main():
         assert out["rows_check"]["one_sided_outside_1e-5_of_thr"] == 0, out["rows_check"]
         assert not args.ref_sums or len(one_sided) == 0, out["rows_check"]
         assert not whole or rows == len(kg), (rows, len(kg))
+        if fp6 and whole and world == 1 and len(kr) < 1000 and args.ref_sums:
+            # the check above is vacuous where no row passes (C4 at 0.05): the
+            # fp6 screen forced on the whole workload at a threshold where
+            # rows do pass, every row against the oracle (same rows, order, bits)
+            out["rows_check_fp6"] = fp6_rows_check(ctx, buf, weights, L, N, min(thr, 0.01))
+            assert out["rows_check_fp6"]["equal"], out["rows_check_fp6"]
     print(json.dumps(out), flush=True)
 
 

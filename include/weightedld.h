@@ -419,6 +419,10 @@ typedef struct {
     int screen_fp6;          /* screened == 1 on fp6 x fp4 block-scaled MFMA (WLD_OPT_SCREEN_FP6), not i8;
                                 2: the fp6 screen gave the pass up (more than a sixteenth of the tiles were
                                 candidates) and it re-ran on the i8 screen */
+    uint64_t progress_filled; /* per-chunk progress (wld_run_host with a callback): chunk reports the
+                                 host made up from the chunk pair counts because the pass's log lacked
+                                 their entries once it had completed; 0 unless the kernels' chunk
+                                 accounting lost a count (the tests assert 0) */
 } wld_run_stats;
 int wld_last_stats(wld_ctx *ctx, wld_run_stats *out);
 

@@ -7,7 +7,11 @@
 // launch-wide bound Tg >= T, passed in the nonneg field, then r2_screen_terms;
 // skip iff both terms are <= 0).  "f32xy": the same from the accumulator form
 // (X0 = (T + B) / 2, Y0 = (T - B) / 2, X1 = (A + AB) / 2, Y1 = (A - AB) / 2;
-// r2_screen_terms_xy).
+// r2_screen_terms_xy).  "f32fg": the fp6 screen's form (F0 = T - B/2, G0 =
+// T - 3B/4, F1 = A - AB/2, G1 = A - 3AB/4 of the doubled record sums; R put on
+// the accumulators' grid, here 1/2, as the kernel does; r2_screen_terms_fg,
+// skip iff t1 <= 0 and every marginal >= mloc).  "f32xy2": r2_screen_terms_xy2
+// on the X/Y accumulators, R on the same grid, the same skip rule.
 #include <cmath>
 #include <cstdio>
 #include <string>
@@ -19,7 +23,9 @@ int main(int argc, char **argv) {
     if (argc != 3 && argc != 4) return 2;
     const bool f32 = argc == 4 && std::string(argv[3]) == "f32";
     const bool f32xy = argc == 4 && std::string(argv[3]) == "f32xy";
-    const bool f32g = f32xy || (argc == 4 && std::string(argv[3]) == "f32g");
+    const bool f32fg = argc == 4 && std::string(argv[3]) == "f32fg";
+    const bool f32xy2 = argc == 4 && std::string(argv[3]) == "f32xy2";
+    const bool f32g = f32xy || f32fg || f32xy2 || (argc == 4 && std::string(argv[3]) == "f32g");
     FILE *f = fopen(argv[1], "rb");
     if (!f) return 3;
     std::vector<double> rec;
@@ -33,10 +39,27 @@ int main(int argc, char **argv) {
         if (f32g) {
             float R = (float)r[4], Tg = (float)r[6];
             if ((double)R < r[4]) R = std::nextafter(R, INFINITY);
+            if (f32fg || f32xy2) R = (float)(std::ceil(r[4] * 2.0) / 2.0);
             if ((double)Tg < r[6]) Tg = std::nextafter(Tg, INFINITY);
             float E, mloc, t2;
             wld::screen_consts(Tg, R, E, mloc);
             const float thr_c = (float)r[5] * (1.0f - 0x1p-7f);
+            if (f32xy2) {
+                float mlo;
+                const float t1 = wld::r2_screen_terms_xy2((float)((r[0] + r[2]) / 2), (float)((r[0] - r[2]) / 2),
+                                                          (float)((r[1] + r[3]) / 2), (float)((r[1] - r[3]) / 2), R,
+                                                          thr_c, E, mlo);
+                out[i] = t1 <= 0.0f && mlo >= mloc ? 1 : 0;
+                continue;
+            }
+            if (f32fg) {
+                float mlo;
+                const float t1 = wld::r2_screen_terms_fg((float)(r[0] - r[2] / 2), (float)(r[0] - 0.75 * r[2]),
+                                                         (float)(r[1] - r[3] / 2), (float)(r[1] - 0.75 * r[3]), R,
+                                                         thr_c, E, mlo);
+                out[i] = t1 <= 0.0f && mlo >= mloc ? 1 : 0;
+                continue;
+            }
             const float t1 =
                 f32xy ? wld::r2_screen_terms_xy((float)((r[0] + r[2]) / 2), (float)((r[0] - r[2]) / 2),
                                                 (float)((r[1] + r[3]) / 2), (float)((r[1] - r[3]) / 2), R, thr_c, E,

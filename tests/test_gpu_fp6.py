@@ -212,3 +212,40 @@ def test_fp6_sequence_counts(W, N):
         c.run(thr)
         _bits_equal(c.rows(), O.all_pairs(buf, w, np.float32(thr)))
     c.close()
+
+
+@pytest.mark.parametrize("cfg", ["c4", "c5"])
+def test_fp6_forced_full_size_rows(W, cfg):
+    """The headline kernel where it can fail: the fp6 screen forced
+    (WLD_OPT_SCREEN_FP6 2: the pass always completes, never hands over to i8)
+    on BASELINE configs 4 and 5 at full size (the bench's own seeded inputs,
+    Henikoff weights: 313 / 782 tile rows, every tile of the XCD-ordered
+    list), at thresholds where rows pass: >= 1,000 oracle rows at C4, >= 10^4
+    at C5.  The pass must run on fp6 (stats screen_fp6 1), and its rows,
+    their order and every bit of d, d', r2 equal the oracle's (lib.rs:482-520,
+    :660, :623-683).  One oracle run at the lowest threshold; the others are
+    its strict-'>' subsets."""
+    import bench
+    N, L, thr, _ = bench.CONFIGS[cfg]
+    buf = bench.synth(L, N)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    thrs = (0.02, 0.015, 0.01) if cfg == "c4" else (0.01, 0.005, 0.004)
+    lo = np.float32(min(thrs))
+    ref = O.all_pairs(buf, w, lo)
+    assert ref["pairs"] == L * (L - 1) // 2
+    c = W.Context(0)
+    c.set_option("screen_fp6", 2)
+    c.load(buf, w)
+    counts = []
+    for t in thrs:
+        t32 = np.float32(t)
+        sub = {f: v[ref["r2"] > t32] for f, v in ref.items() if f != "pairs"}
+        n = c.run(t)
+        st = c.stats()
+        assert st["screened"] == 1 and st["screen_fp6"] == 1, st
+        assert n == len(sub["r2"])
+        _bits_equal(c.rows(), sub)
+        counts.append((t, n, st["candidate_tiles"], st["tiles"]))
+    print("fp6 forced full size %s: (thr, rows, candidate tiles, tiles) %s" % (cfg, counts))
+    assert max(n for _, n, _, _ in counts) >= (1000 if cfg == "c4" else 10000), counts
+    c.close()

@@ -932,18 +932,21 @@ def test_progress_once_per_chunk_config2(W, devices):
     assert threads == {threading.get_ident()}
     steps = sorted(np.diff(seen[1:]).tolist() + [L * (L - 1) // 2 - seen[-1]])
     assert steps == sorted(chunk_pairs(L, i) for i in range(n_chunks))
+    assert ctx.stats()["progress_filled"] == 0  # every chunk's report came from the kernels' log
     assert len(store) > 1_990_000
 
 
 
-@pytest.mark.parametrize("thr,screen", [(0.05, 1), (0.002, 4)], ids=["screen_items", "candidate_pairs"])
-def test_progress_once_per_chunk_screened(W, thr, screen):
+@pytest.mark.parametrize("thr,screen,fp6", [(0.05, 1, 0), (0.002, 4, 0), (0.05, 1, 2)],
+                         ids=["screen_items", "candidate_pairs", "fp6_screen"])
+def test_progress_once_per_chunk_screened(W, thr, screen, fp6):
     """Per-chunk progress through the screened paths on linkage-block data:
-    at 0.05 the i8 screen and the f32 candidate launch over 16-row-block items
-    (a chunk finishes when the screen's rejected row blocks and every item's
-    row block are done), at 0.002 the exact candidate pairs (a tile is done
-    after ref_compact).  One callback per chunk, values in lib.rs's fetch_add
-    sequence; the rows equal the oracle's bit for bit."""
+    at 0.05 the i8 (or, forced, the fp6) screen and the f32 candidate launch
+    over 16-row-block items (a chunk finishes when the screen's rejected row
+    blocks and every item's row block are done), at 0.002 the exact candidate
+    pairs (a tile is done after ref_compact).  One callback per chunk, values
+    in lib.rs's fetch_add sequence, none made up by the host; the rows equal
+    the oracle's bit for bit."""
     sys_path_bench()
     from bench import chunk_pairs, ld_blocks
     L, N = 3000, 600
@@ -951,10 +954,13 @@ def test_progress_once_per_chunk_screened(W, thr, screen):
     w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
     ctx = W.Context(0)
     ctx.set_option("screen", screen)
+    ctx.set_option("screen_fp6", fp6)
     seen = []
     store = W.all_weighted_ld_pairs(W.SiteSet.from_buffer(buf), w, thr, progress_report=seen.append, ctx=ctx)
     st = ctx.stats()
     assert st["screened"] == screen and st["candidate_tiles"] > 0, st
+    assert st["screen_fp6"] == (1 if fp6 else 0), st
+    assert st["progress_filled"] == 0, st
     n_chunks = ctx.chunks(L)
     assert len(seen) == 1 + n_chunks and seen[0] == 0 and seen == sorted(seen)
     steps = sorted(np.diff(seen[1:]).tolist() + [L * (L - 1) // 2 - seen[-1]])

@@ -255,6 +255,23 @@ def test_cli_help_and_arg_errors(tmp_path):
     assert r.returncode == 1
 
 
+@pytest.mark.parametrize("rust_log", [None, "error"])
+def test_cli_exact_sums_warns(tmp_path, rust_log):
+    # --exact-sums is this build's addition, not a reference flag (main.rs:14-68):
+    # its TSV is not lib.rs's, so the CLI says so on stderr at any log level,
+    # before any GPU step (checkable here, without a device)
+    env = dict(os.environ)
+    if rust_log:
+        env["RUST_LOG"] = rust_log
+    r = subprocess.run([CLI, "--fasta-input", os.path.join(FIXTURES, "example.fasta"), "--pair-output",
+                        str(tmp_path / "p.tsv"), "--exact-sums"], capture_output=True, text=True, env=env)
+    assert "WARN" in r.stderr and "--exact-sums departs from the reference" in r.stderr
+    assert "1.11" in r.stderr
+    r = subprocess.run([CLI, "--fasta-input", os.path.join(FIXTURES, "example.fasta"), "--pair-output",
+                        str(tmp_path / "p.tsv")], capture_output=True, text=True, env=env)
+    assert "exact-sums" not in r.stderr
+
+
 def test_cli_weights_output_before_gpu_step(tmp_path):
     # the weights file is written before the all-pairs step (main.rs:161-164),
     # so it is checkable without a GPU: example.fasta lib.rs-derived weights.

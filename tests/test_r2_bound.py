@@ -24,13 +24,14 @@ def harness(tmp_path_factory):
                     "-I", os.path.join(REPO, "include"), "-I", os.path.join(REPO, "weightedld_amd", "csrc"),
                     "-x", "hip", os.path.join(REPO, "tests", "cpp", "bound_check.cpp"), "-o", exe], check=True)
 
-    def run(T, A, B, AB, R, thr, nonneg=True, f32=False, Tg=None, xy=False):
+    def run(T, A, B, AB, R, thr, nonneg=True, f32=False, Tg=None, xy=False, fg=False, xy2=False):
         n = len(T)
         last = float(nonneg) if Tg is None else Tg
         rec = np.stack([np.asarray(x, np.float64) * np.ones(n) for x in (T, A, B, AB, R, thr, last)], 1)
         d = tmp_path_factory.mktemp("io")
         rec.tofile(str(d / "in.bin"))
-        mode = ["f32xy" if xy else "f32g"] if Tg is not None else ["f32"] if f32 else []
+        mode = (["f32xy2" if xy2 else "f32fg" if fg else "f32xy" if xy else "f32g"] if Tg is not None else
+                ["f32"] if f32 else [])
         subprocess.run([exe, str(d / "in.bin"), str(d / "out.bin")] + mode, check=True)
         return np.fromfile(str(d / "out.bin"), dtype=np.uint8).astype(bool)
     return run
@@ -264,4 +265,57 @@ def test_screen_accumulator_form_near_threshold(harness, thr):
         for R in (0.0, 1.0, 17.5):
             for Tg in (2 * float(T.max()), 4 * float(T.max())):
                 viol += int((harness(2 * T, 2 * A, 2 * B, 2 * AB, 2 * R, thr, Tg=Tg, xy=True) & passes).sum())
+    assert viol == 0
+
+
+@pytest.mark.parametrize("form", ["fg", "xy2"])
+@pytest.mark.parametrize("rare", [False, True])
+def test_screen_fp6_dual_form_sound(harness, rare, form):
+    # r2_screen_terms_fg (the fp6 screen's form, from the e2m3 / e3m2 readings
+    # of the b codes; exact marginals, R on the accumulators' grid, marginals
+    # tested against mloc as the screen's per-lane minimum): never skips a pair
+    # whose exact sums pass the f32 epilogue, for any Tg >= T, and decides like
+    # the X/Y form but for pairs on the edge of a rounding.
+    rng = np.random.default_rng(67 + rare)
+    viol = diff = more = total = skipped = 0
+    for it in range(12):
+        n = 200_000
+        scale = float(2 ** rng.integers(10, 21))
+        c = screen_tables(rng, n, scale, rare)
+        T, A, B, AB = c.sum(0), c[0] + c[1], c[0] + c[2], c[0]
+        thr = float(np.float32(rng.choice([0.001, 0.01, 0.05, 0.2, 0.6])))
+        R = rng.choice([0.0, 1e-4, 1e-3, 1e-2]) * scale * rng.random()
+        e = rng.random((4, n)) * rng.choice([-1.0, 1.0], (4, n))
+        e = np.trunc(e / np.maximum(np.abs(e).sum(0), 1e-12) * R * rng.random(n))
+        h = 2 * (c + e)
+        args = (h.sum(0), h[0] + h[1], h[0] + h[2], h[0], 2 * R, thr)
+        with np.errstate(invalid="ignore"):
+            passes = f32_r2(T, A, B, AB) > np.float32(thr)
+        for f in (1.0, 2.0):
+            Tg = float(h.sum(0).max()) * f
+            sf = harness(*args, Tg=Tg, **{form: True})
+            sx = harness(*args, Tg=Tg, xy=True)
+            viol += int((sf & passes).sum())
+            diff += int((sf != sx).sum())
+            more += int((sf & ~sx).sum())
+            skipped += int(sf.sum())
+            total += n
+    assert viol == 0
+    assert skipped > total // 4
+    print("%s vs xy: %d of %d decisions differ, %d of them skips only %s makes" % (form, diff, total, more, form))
+    assert more == 0  # never skips a pair the X/Y form keeps
+    assert diff <= total // 1000, (diff, total)
+
+
+@pytest.mark.parametrize("form", ["fg", "xy2"])
+@pytest.mark.parametrize("thr", [0.05, 0.3])
+def test_screen_fp6_dual_form_near_threshold(harness, thr, form):
+    rng = np.random.default_rng(int(thr * 1000) + 13)
+    viol = 0
+    for _ in range(6):
+        T, A, B, AB = near_threshold_tables(rng, 1_000_000, thr, scale=2.0 ** 21, window=0.05)
+        passes = f32_r2(T, A, B, AB) > np.float32(thr)
+        for R in (0.0, 1.0, 17.5):
+            for Tg in (2 * float(T.max()), 4 * float(T.max())):
+                viol += int((harness(2 * T, 2 * A, 2 * B, 2 * AB, 2 * R, thr, Tg=Tg, **{form: True}) & passes).sum())
     assert viol == 0

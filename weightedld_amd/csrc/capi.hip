@@ -135,6 +135,7 @@ struct wld_ctx {
     // the fp6 screen (fp6_prepare): weight codes, packed operands, constants
     DevBuf w6, f6a, f6b;
     Fp6Screen f6{};
+    bool fp6_tried = false;   // fp6_prepare ran for this load
     bool fp6_ok = false;      // operands built for this load (the weights allow it)
     bool fp6_pass = false;    // the last pass screened on fp6
     bool fp6_better = false;  // ... and its residual is within twice the i8 top digit's (auto)
@@ -156,6 +157,8 @@ struct wld_ctx {
 
     // run state
     DevBuf tiles, cand, seg_cnt, seg_off, chunk_total, chunk_base, counters;
+    DevBuf f6_pairs;          // the fp6 screen's tile-pair list of the tile list (fp6_uses_pairs)
+    uint32_t f6_n_pairs = 0;
     DevBuf st_a, st_b, st_d, st_dp, st_r2;
     DevBuf out_a, out_b, out_d, out_dp, out_r2;
     uint64_t st_capacity = 0;
@@ -188,7 +191,7 @@ struct wld_ctx {
         // work queued on a borrowed stream (wld_set_stream) may still use the
         // buffers: it completes before they are freed
         if (stream && stream != own_stream) (void)hipStreamSynchronize(stream);
-        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &rcodes, &rw, &w6, &f6a, &f6b, &tiles, &cand,
+        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &rcodes, &rw, &w6, &f6a, &f6b, &tiles, &cand, &f6_pairs,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &chunk_left, &prog_n, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
@@ -238,18 +241,20 @@ int weight_shift(float maxabs, int planes) {
 double ref_extra_residual(const wld_ctx *c);
 
 // e2m3 (fp6) encoding of a value in [0, 7.5] rounded to the nearest grid
-// point (ties to the even code): sign 0, exponent bias 1, 3 mantissa bits
+// point, ties to the even code: sign 0, exponent bias 1, 3 mantissa bits.
+// The grid steps by 1/8 below 2, by 1/4 in [2, 4) and by 1/2 from 4; within
+// each the code's parity is the grid index's, so round-half-even on the index
+// (nearbyint) is ties-to-even on the code (an index rounding up to the next
+// binade's first point lands on its even code, m = 0).
 uint32_t fp6_code(double x, double *rounded) {
-    uint32_t best = 0;
-    double bv = 0.0, be = x;
-    for (uint32_t c = 0; c < 32; ++c) {
-        const uint32_t e = c >> 3, m = c & 7;
-        const double v = e ? (1.0 + m / 8.0) * std::ldexp(1.0, (int)e - 1) : m / 8.0;
-        const double err = std::fabs(x - v);
-        if (err < be || (err == be && !(c & 1))) best = c, bv = v, be = err;
-    }
-    *rounded = bv;
-    return best;
+    x = std::min(std::max(x, 0.0), 7.5);
+    const double step = x < 2.0 ? 0.125 : x < 4.0 ? 0.25 : 0.5;
+    const double v = std::min(std::nearbyint(x / step) * step, 7.5);
+    *rounded = v;
+    if (v < 1.0) return (uint32_t)(v * 8.0);                             // e = 0 (subnormal), m = 8v
+    if (v < 2.0) return 8u + (uint32_t)((v - 1.0) * 8.0);                // e = 1
+    if (v < 4.0) return 16u + (uint32_t)((v * 0.5 - 1.0) * 8.0);         // e = 2
+    return 24u + (uint32_t)((v * 0.25 - 1.0) * 8.0);                     // e = 3
 }
 
 // The fp6 screen's operands for this load (pair_mfma.hip): nonnegative
@@ -261,8 +266,11 @@ uint32_t fp6_code(double x, double *rounded) {
 // rounding, plus the fixed point's 0.5 per sequence (exact mode) and lib.rs's
 // f32 summation (9 gamma_m sum w, ref_extra_residual) — both added, so one
 // R serves either mode.
+// Built on the first run that may screen on fp6 (not at load: with
+// WLD_OPT_SCREEN_FP6 0 it never is).
 int fp6_prepare(wld_ctx *c) {
     c->fp6_ok = c->fp6_better = false;
+    c->fp6_tried = true;
     if (c->kernel != WLD_KERNEL_MFMA || !c->use_frag || !c->wst.nonneg || c->NP > 16384 || c->N == 0) return WLD_OK;
     std::vector<float> w(c->NP);
     HIP_TRY(hipMemcpyAsync(w.data(), c->w_pad.p, c->NP * sizeof(float), hipMemcpyDeviceToHost, c->stream));
@@ -310,7 +318,7 @@ int fp6_prepare(wld_ctx *c) {
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->f6.a6 = ptr<uint8_t>(c->f6a);
-    c->f6.b4 = ptr<uint8_t>(c->f6b);
+    c->f6.b6 = ptr<uint8_t>(c->f6b);
     c->fp6_ok = true;
     c->fp6_better = c->fp6_rel <= std::max(2.0 * c->i8_rel, 0.02);
     return WLD_OK;
@@ -409,7 +417,7 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     const unsigned all_planes = (1u << c->fixed_planes) - 1;
     c->plane_mask = c->kernel == WLD_KERNEL_MFMA && !c->opt_all_planes ? c->wst.plane_mask : all_planes;
     c->stats.load_ms = event_ms(c->ev[0], c->ev[1]);
-    WLD_TRY(fp6_prepare(c));
+    c->fp6_ok = c->fp6_better = c->fp6_tried = false;  // (fp6_prepare: at the first run that may use it)
     c->stats.mfma_planes = c->kernel == WLD_KERNEL_MFMA ? __builtin_popcount(c->plane_mask) : 0;
     c->stats.kernel = c->kernel;
     c->stats.weight_shift = c->shift;
@@ -544,6 +552,23 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
     }
     std::sort(t.begin(), t.end());
     const uint32_t kS = 24ull * kTile * c->NP <= (4ull << 20) ? 16u : 8u;
+    // the fp6 screen's tile pairs (ordered as the tiles below, by first tile;
+    // single tiles keep their flag through the ordering)
+    std::vector<uint32_t> pl;
+    if (fp6_uses_pairs() && T_used <= 0x7FFF) {
+        pl = fp6_pair_list(t);
+        if (!c->opt_tile_rows && pl.size() >= 2048) {
+            std::vector<uint32_t> plain(pl.size()), single;
+            for (size_t i = 0; i < pl.size(); ++i) {
+                plain[i] = pl[i] & ~0x8000u;
+                if (pl[i] & 0x8000u) single.push_back(plain[i]);
+            }
+            std::sort(single.begin(), single.end());
+            pl = xcd_order(plain, kS);
+            for (auto &v : pl)
+                if (v != kNoTile && std::binary_search(single.begin(), single.end(), v)) v |= 0x8000u;
+        }
+    }
     // only with many rounds of resident tiles: whole super-blocks per XCD
     // leave up to one super-block of imbalance (C2's 528 tiles: +14%)
     if (!c->opt_tile_rows && t.size() >= 4096 && T_used < 65535) t = xcd_order(t, kS);
@@ -553,6 +578,12 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
     WLD_TRY(ensure(c->cand, std::max<size_t>(t.size(), 1) * 32 * sizeof(uint32_t)));
     if (!t.empty())
         HIP_TRY(hipMemcpyAsync(c->tiles.p, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    c->f6_n_pairs = (uint32_t)pl.size();
+    if (!pl.empty()) {
+        WLD_TRY(ensure(c->f6_pairs, pl.size() * sizeof(uint32_t)));
+        HIP_TRY(hipMemcpyAsync(c->f6_pairs.p, pl.data(), pl.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                               c->stream));
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->tiles_lb = lb;
     c->tiles_le = le;
@@ -685,6 +716,8 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         // re-run rewrites it)
         m.fp6_bail = c->opt_fp6 == 1 && !c->prog_pass && !c->pend.count_out ? std::max<uint32_t>(c->n_tiles / 16, 1)
                                                                                 : 0;
+        m.f6_pairs = c->f6_n_pairs ? ptr<uint32_t>(c->f6_pairs) : nullptr;
+        m.f6_n_pairs = c->f6_n_pairs;
         for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
         m.cand_list = ptr<uint32_t>(c->cand);
         // this pass's candidate set (the scan zeroes the other one, enqueue_pass)
@@ -1171,6 +1204,7 @@ int run_enqueue(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uns
     const uint32_t n = chunk_rows_of(c->L);
     c->have_rows = false;
     c->pend.active = false;
+    if (!c->fp6_tried && c->opt_fp6 != 0) WLD_TRY(fp6_prepare(c));
     WLD_TRY(build_tiles(c, lin_begin, lin_end));
     const uint64_t pairs = pairs_in_chunks(c->L, lin_begin, lin_end);
     const uint32_t T = (uint32_t)(c->LP / kTile);
@@ -1215,8 +1249,10 @@ int run_enqueue(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uns
 // logged so far, in slot order, to on_chunk (on the calling thread), polled
 // while the pass runs; then the rest once it has completed.  Progress is a
 // report, not a result: entries still missing once the pass has completed
-// (a re-run, a refused tile) are reported from the chunk pair counts the host
-// knows, never turned into a failed run.
+// are reported from the chunk pair counts the host knows rather than failing
+// the run, and counted in wld_run_stats.progress_filled — a pass that
+// completes logs every chunk (a refused tile fails the run at check_guard),
+// so a nonzero count is a lost tile_done count, which the tests look for.
 int drain_progress(wld_ctx *c, uint32_t lin_begin, uint32_t n_chunks) {
     uint32_t seen = 0;
     auto drain = [&] {
@@ -1245,6 +1281,7 @@ int drain_progress(wld_ctx *c, uint32_t lin_begin, uint32_t n_chunks) {
         uint64_t rest = pairs_in_chunks(c->L, lin_begin, lin_begin + n_chunks) - std::min<uint64_t>(
                             logged, pairs_in_chunks(c->L, lin_begin, lin_begin + n_chunks));
         const uint32_t missing = n_chunks - seen;
+        c->stats.progress_filled += missing;
         for (uint32_t k = 0; k < missing; ++k) {
             const uint64_t v = rest / (missing - k);
             (*c->on_chunk)(v);
@@ -1538,6 +1575,7 @@ int run_host_range(wld_ctx *c, float r2_threshold, uint32_t lb, uint32_t le,
     memset(out, 0, sizeof(*out));
     WLD_TRY(set_dev(c));
     if (!c->loaded) return fail(WLD_E_STATE, "wld_run_host before wld_load");
+    c->stats.progress_filled = 0;
     const uint64_t limit = std::max<uint64_t>(1, c->opt_host_batch_pairs);
     uint64_t cap = 0, done = 0, pairs_done = 0;
     auto grow = [&](uint64_t need) -> int {
@@ -1677,6 +1715,8 @@ int run_host_group(wld_ctx *g, float thr, const std::function<void(uint64_t)> *o
     }
     for (auto &p : part) wld_pairs_free(&p);
     g->stats = g->members[0]->stats;
+    g->stats.progress_filled = 0;
+    for (wld_ctx *m : g->members) g->stats.progress_filled += m->stats.progress_filled;
     g->stats.pairs = pairs_done;
     g->stats.rows = st == WLD_OK ? total : 0;
     double kms = 0.0;

@@ -210,15 +210,20 @@ constexpr uint32_t kRefRowsGrid = 2048;
 // (residual bound of the rounded weights plus the reference's rounding) and
 // Tg (>= every doubled T), in the units of the fp6 weights (capi.hip).
 struct Fp6Screen {
-    const uint8_t *a6, *b4;
+    const uint8_t *a6, *b6;
     uint32_t NK;  // 128-sequence blocks
     double R;
     float Tg;
 };
 size_t fp6_a_bytes(size_t LP, size_t NP);
 size_t fp6_b_bytes(size_t LP, size_t NP);
+// the fp6 screen runs on tile pairs (pair_fp6_screen2_kernel: one A image for
+// two column tiles) rather than single tiles
+bool fp6_uses_pairs();
+// the pair list of a (ta, tb)-sorted tile list (pair_mfma.hip)
+std::vector<uint32_t> fp6_pair_list(const std::vector<uint32_t> &sorted_tiles);
 // w6: NP fp6 (e2m3) codes of the rounded weights (0 for padding)
-void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b4,
+void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b6,
                   hipStream_t s);
 
 struct MfmaLaunch {
@@ -259,6 +264,9 @@ struct MfmaLaunch {
     const Fp6Screen *fp6;
     // ... gives up past this many candidate tiles (0: never; kAbandonBit)
     uint32_t fp6_bail;
+    // ... its tile-pair list (fp6_uses_pairs; XCD-ordered, kNoTile padded)
+    const uint32_t *f6_pairs;
+    uint32_t f6_n_pairs;
 };
 // Enqueues the MFMA pair kernel(s) of one pass; returns true when a screen
 // (one- or two-plane) ran (then screen_done, if given, is recorded between

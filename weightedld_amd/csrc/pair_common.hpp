@@ -131,6 +131,54 @@ __host__ __device__ __forceinline__ float r2_screen_terms_xy(float X0, float Y0,
     t2 = mloc - mlo;
     return nub * nub - thr_c * ((m1 * m2) * (m3 * m4));
 }
+// The same test from the fp6 screen's accumulators (pair_mfma.hip): the b
+// codes read as e2m3 (F: minor 2, major 1) and as e3m2 (G: minor 2, major
+// 0.5) give, in doubled units, F0 = 2T - SB, G0 = 2T - 1.5 SB (channel_a
+// "in") and F1 = 2SA - SAB, G1 = 2SA - 1.5 SAB (channel_a major), so D0 =
+// F0 - G0 = SB / 2, D1 = SAB / 2, and the doubled marginals of
+// r2_screen_terms_xy are 2T = F0 + 2 D0, 2SB = 4 D0, 2(T - SB) = F0 - 2 D0,
+// 2SA = F1 + 2 D1.  Every accumulator is an exact multiple of 1/16 below 2^19
+// and R (doubled, R2) is put on that grid by the caller, so every marginal
+// below, R subtracted, is exact — the xy form's marginals rounded, these equal
+// the exact values.  The numerator A B - AB T = F1 D0 - F0 D1 by one product
+// and one FMA: |error| <= 2u (F1 D0 + F0 D1)(1 + u) <= 4u (1 + u) T^2 of the
+// doubled T, so 4 |.| is within the 4.02u Tb^2 the derivation allows (nub
+// rounds once, as in the xy form).  t1 = fma(nub, nub, -fl(thr_c P)) is <= 0
+// only if fl(nub^2) <= fl(thr_c P) (rounding is monotone), i.e. only where
+// the xy form's t1 is <= 0.  The second test (every marginal >= mloc) is left
+// to the caller as mlo (the screen tracks one minimum over a lane's pairs:
+// a tile whose minimum falls below mloc is a candidate, as the xy form's t2
+// would make the pair holding it).  Skip iff t1 <= 0 and mlo >= mloc.
+__host__ __device__ __forceinline__ float r2_screen_terms_fg(float F0, float G0, float F1, float G1, float R2,
+                                                             float thr_c, float E, float &mlo) {
+    const float D0 = F0 - G0, D1 = F1 - G1;
+    const float F0r = F0 - R2;
+    const float m4 = fmaf(-2.0f, D0, F0r), T2r = fmaf(2.0f, D0, F0r), m3 = fmaf(4.0f, D0, -R2);
+    const float A2 = fmaf(2.0f, D1, F1);
+    const float m1 = A2 - R2, m2 = T2r - A2;
+    mlo = fminf(fminf(m1, m2), fminf(m3, m4));
+    const float nub = fmaf(4.0f, fabsf(fmaf(F1, D0, -(F0 * D1))), E);
+    return fmaf(nub, nub, -(thr_c * ((m1 * m2) * (m3 * m4))));
+}
+// The same from the fp4-coded b sites' accumulators (pair_mfma.hip, the
+// tile-pair fp6 screen with fp4 B): X = the raw codes read as e2m1 (minor 1,
+// major 2), Y = their minor bit (raw & 0x2222...): X0 = T + SB, Y0 = T - SB,
+// X1 = SA + SAB, Y1 = SA - SAB, so 2T = X0 + Y0, 2SB = X0 - Y0, 2(T - SB) =
+// 2 Y0, 2SA = X1 + Y1 (doubled units, as r2_screen_terms_xy).  Accumulators
+// and R2 on the 1/8 grid below 2^19: the marginals are exact; the numerator
+// and t1 as in r2_screen_terms_xy / _fg (X0 Y1 - X1 Y0 = 2 num, error <= 2u
+// (X0 Y1 + X1 Y0)(1 + u) <= 4u T^2: 2u T2^2 after doubling).  Skip iff t1 <= 0
+// and mlo >= mloc.
+__host__ __device__ __forceinline__ float r2_screen_terms_xy2(float X0, float Y0, float X1, float Y1, float R2,
+                                                              float thr_c, float E, float &mlo) {
+    const float X0r = X0 - R2;
+    const float T2r = X0r + Y0, m3 = X0r - Y0, m4 = fmaf(2.0f, Y0, -R2);
+    const float A2 = X1 + Y1;
+    const float m1 = A2 - R2, m2 = T2r - A2;
+    mlo = fminf(fminf(m1, m2), fminf(m3, m4));
+    const float nub = fmaf(2.0f, fabsf(fmaf(X0, Y1, -(X1 * Y0))), E);
+    return fmaf(nub, nub, -(thr_c * ((m1 * m2) * (m3 * m4))));
+}
 __host__ __device__ __forceinline__ float r2_screen_violation(float T, float A, float B, float AB, float R,
                                                               float thr_c) {
     float E, mloc, t2;

@@ -43,6 +43,7 @@
 // Passing rows are compacted per tile in LDS (order.hip assembles the
 // reference order).
 #include <algorithm>
+#include <vector>
 
 #include "pair_common.hpp"
 
@@ -832,46 +833,68 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
 // ---- fp6 screen (block-scaled MFMA, twice the i8 rate) ----------------------
 //
 // The one-plane screen's sums from v_mfma_scale_f32_16x16x128_f8f6f4 with fp6
-// (e2m3) A and fp4 (e2m1) B operands, unit block scales: 128 sequences per
+// (e2m3) operands on both sides, unit block scales: 128 sequences per
 // instruction at the cycles of the i8 kernel's 64.  Every weight is rounded
 // to its nearest e2m3 value at a common scale S (w6_k = fp6(S w_k), a multiple
 // of 1/8 in [0, 7.5]); A = w6 where the a site's symbol is major or minor
-// ("in") or major, B = minor + 2 major of the b site (0, 1.0, 2.0).  Products
-// are exact and every sum is a multiple of 1/8 below 2^21, so the f32 MFMA
-// sums are the exact sums of the rounded weights, and the screen's f32 bound
-// (r2_screen_terms_xy on doubled sums, sound for any power-of-two unit) holds
-// with R = sum_k |S w_k - w6_k| plus the reference's rounding, in the same
-// units (capi.hip fp6_prepare).  Operands come pre-packed from memory (no
-// per-element VALU; the minor channel is raw & 0x22222222):
-//   a6 [16-site group][128-seq block kb][channel in, major][lane][24 B]: lane l
-//      = site l & 15, sequences 32 (l >> 4) + j at bits 6j (fp6_probe.hip)
-//   b4 [16-site group][kb][lane][16 B]: nibble j = fp4 of minor + 2 major
-// One 64x64 tile per 4-wave workgroup, four per CU; per 128 sequences each
-// wave LDS-DMAs its row block's A (3 KB) and its column block's B (1 KB)
-// into a double-buffered 16 KB stage; wave w computes a rows 16w.. against
-// the four column blocks (16 MFMAs per stage), then the screen epilogue.
-constexpr int kF6ABytes = 3072, kF6BBytes = 1024;
-constexpr int kF6AStage = 4 * kF6ABytes;  // A bytes in an LDS stage
-constexpr int kF6Stage = kF6AStage + 4 * kF6BBytes;
+// ("in", lib.rs:435) or major (lib.rs:430-432), two channels.  B holds one
+// 6-bit code per b symbol, 0 (neither), 8 (major) or 16 (minor), and each B
+// register is multiplied twice: read as e2m3 (blgp 2) the codes are 0 / 1.0 /
+// 2.0, read as e3m2 (blgp 3) 0 / 0.5 / 2.0 (tools/probes/fp6_dual_probe.hip)
+// — two independent channels from the same bytes, with no mask instruction.
+// Per pair the four accumulators (channel_a in / major x reading F / G) are
+//   F0 = 2T - SB, G0 = 2T - 1.5 SB, F1 = 2SA - SAB, G1 = 2SA - 1.5 SAB
+// (T, SA, SB, SAB: lib.rs:441-444's sums of the rounded weights).  Products
+// are exact and every sum is a multiple of 1/16 below 2^19, so the f32 MFMA
+// sums are exact, and so is every marginal the per-pair test forms from them
+// (r2_screen_terms_fg; R is put on the same grid): the screen's f32 bound
+// holds with R = sum_k |S w_k - w6_k| plus the reference's rounding, in the
+// same units (capi.hip fp6_prepare).  Operands come pre-packed from memory,
+// per 64-site tile and 128-sequence block kb one contiguous stage image:
+//   a6 [tile][kb][16-site block][channel in, major][1536 B] (12 KB): lane l =
+//      site l & 15 of the block, sequences 32 (l >> 4) + j at bits 6j of six
+//      dwords, dwords 0-3 at 16 l, dwords 4-5 at 1024 + 8 l (one ds_read_b128
+//      and one ds_read_b64 fill the operand registers in place)
+//   b6 [tile][kb][16-site block][1536 B]: the b codes, same packing (6 KB)
+// One 64x64 tile per 4-wave workgroup, four per CU; per 128 sequences the
+// waves LDS-DMA the row tile's A image and the column tile's B image (18 1-KB
+// pieces) into a double-buffered 18 KB stage; wave w computes a rows 16w..
+// against the four column blocks (16 MFMAs per stage), then the screen
+// epilogue.
+// B operand format (WLD_F6_B4): 1 (default) the b codes as fp4 (e2m1) nibbles
+// of minor + 2 major (1.0 / 2.0; 16 B per lane and block), the minor channel
+// by one mask per dword (raw & 0x2222...), accumulators X / Y of the X/Y form
+// (r2_screen_terms_xy2); 0: 6-bit codes read twice, as e2m3 and as e3m2 (the
+// F / G form above, r2_screen_terms_fg; no mask, but 1.5x the B bytes and a
+// slower MFMA: 19.6 against 18.1 cycles in tools/probes/fp6_dual_probe.hip)
+#ifndef WLD_F6_B4
+#define WLD_F6_B4 1
+#endif
+constexpr int kF6ABytes = 3072;                         // per 16-site block: A, two channels
+constexpr int kF6BBytes = WLD_F6_B4 ? 1024 : 1536;      // ... and B
+constexpr int kF6AStage = 4 * kF6ABytes;                // a tile's A image per 128 sequences
+constexpr int kF6BStage = 4 * kF6BBytes;                // ... and B image
+constexpr int kF6Stage = kF6AStage + kF6BStage;
+constexpr uint32_t kF6Major = 8, kF6Minor = 16;         // 6-bit b codes: e2m3 1.0 / 2.0, e3m2 0.5 / 2.0
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 
-size_t fp6_a_bytes(size_t LP, size_t NP) { return LP / 16 * ((NP + 127) / 128) * kF6ABytes; }
-size_t fp6_b_bytes(size_t LP, size_t NP) { return LP / 16 * ((NP + 127) / 128) * kF6BBytes; }
+size_t fp6_a_bytes(size_t LP, size_t NP) { return LP / 64 * ((NP + 127) / 128) * kF6AStage; }
+size_t fp6_b_bytes(size_t LP, size_t NP) { return LP / 64 * ((NP + 127) / 128) * kF6BStage; }
 
-// one thread per (16-site group, 128-sequence block, lane)
+// one thread per (64-site tile, 128-sequence block, 16-site block, lane)
 __global__ __launch_bounds__(256) void frag6_kernel(const uint8_t *__restrict__ codes, const uint8_t *__restrict__ w6,
                                                      uint32_t LP, uint32_t NP, uint8_t *__restrict__ a6,
-                                                     uint8_t *__restrict__ b4) {
+                                                     uint8_t *__restrict__ b6) {
     const uint32_t NK = (NP + 127) / 128;
     const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (idx >= (size_t)LP / 16 * NK * 64) return;
-    const uint32_t lane = idx & 63;
-    const size_t t = idx >> 6, g16 = t / NK;
-    const uint32_t kb = (uint32_t)(t % NK);
-    const uint8_t *row = codes + (g16 * 16 + (lane & 15)) * (size_t)NP;
+    const uint32_t lane = idx & 63, blk = (idx >> 6) & 3;
+    const size_t tk = idx >> 8, tile = tk / NK;  // tk = tile * NK + kb
+    const uint32_t kb = (uint32_t)(tk % NK);
+    const uint8_t *row = codes + (tile * 64 + blk * 16 + (lane & 15)) * (size_t)NP;
     const uint32_t k0 = 128 * kb + 32 * (lane >> 4);
-    uint32_t ai[6] = {0, 0, 0, 0, 0, 0}, am[6] = {0, 0, 0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+    uint32_t ai[6] = {0, 0, 0, 0, 0, 0}, am[6] = {0, 0, 0, 0, 0, 0}, b[6] = {0, 0, 0, 0, 0, 0};
     for (uint32_t j = 0; j < 32; ++j) {
         const uint32_t k = k0 + j;
         const uint32_t c = k < NP ? row[k] : 0u, v = k < NP ? w6[k] : 0u;
@@ -883,45 +906,133 @@ __global__ __launch_bounds__(256) void frag6_kernel(const uint8_t *__restrict__ 
             ai[d + 1] |= vi >> (32 - o);
             am[d + 1] |= vm >> (32 - o);
         }
-        b[j >> 3] |= ((c & kCodeIn) ? ((c & kCodeMaj) ? 4u : 2u) : 0u) << (4 * (j & 7));
+        if (WLD_F6_B4) {  // fp4 nibble j: 0, 2 (1.0: minor), 4 (2.0: major)
+            b[j >> 3] |= ((c & kCodeIn) ? ((c & kCodeMaj) ? 4u : 2u) : 0u) << (4 * (j & 7));
+        } else {
+            const uint32_t vb = (c & kCodeIn) ? ((c & kCodeMaj) ? kF6Major : kF6Minor) : 0u;
+            b[d] |= vb << o;
+            if (o > 26) b[d + 1] |= vb >> (32 - o);
+        }
     }
-    uint32_t *pa = reinterpret_cast<uint32_t *>(a6 + ((g16 * NK + kb) * 2) * (size_t)1536 + lane * 24);
-    uint32_t *pm = pa + 1536 / 4;
-    for (int d = 0; d < 6; ++d) pa[d] = ai[d], pm[d] = am[d];
-    *reinterpret_cast<uint4 *>(b4 + (g16 * NK + kb) * (size_t)kF6BBytes + lane * 16) = make_uint4(b[0], b[1], b[2], b[3]);
-
+    uint8_t *pa = a6 + tk * kF6AStage + blk * kF6ABytes, *pm = pa + 1536;
+    uint8_t *pb = b6 + tk * kF6BStage + blk * kF6BBytes;
+    *reinterpret_cast<uint4 *>(pa + 16 * lane) = make_uint4(ai[0], ai[1], ai[2], ai[3]);
+    *reinterpret_cast<uint2 *>(pa + 1024 + 8 * lane) = make_uint2(ai[4], ai[5]);
+    *reinterpret_cast<uint4 *>(pm + 16 * lane) = make_uint4(am[0], am[1], am[2], am[3]);
+    *reinterpret_cast<uint2 *>(pm + 1024 + 8 * lane) = make_uint2(am[4], am[5]);
+    *reinterpret_cast<uint4 *>(pb + 16 * lane) = make_uint4(b[0], b[1], b[2], b[3]);
+    if (!WLD_F6_B4) *reinterpret_cast<uint2 *>(pb + 1024 + 8 * lane) = make_uint2(b[4], b[5]);
 }
 
-// the wave's 16 a rows x 64 b columns as f32 sums of fp6 x fp4 products:
-// [n][channel_a in / major][channel_b X = S(minor + 2 major) / Y = S(minor)]
-// (the layout of Acc16<1, 4>: C/D col = lane & 15, row = 4 (lane >> 4) + e)
-struct AccF6 {
-    static constexpr int kPlanes = 1;
-    static constexpr int kPairs = 16;
-    v4f v[4][2][2];
-    __device__ __forceinline__ float2 raw(int x, int i) const {
-        return make_float2(v[i >> 2][x][0][i & 3], v[i >> 2][x][1][i & 3]);
+namespace {
+// a 16-site block's fp6 operand from its 1536 B LDS image: dwords 0-3, then
+// 4-5 (the empty asm keeps the compiler from pairing two blocks' b64 reads
+// into one ds_read2, whose four registers would then be copied apart)
+__device__ __forceinline__ v8i f6_ld24(const uint8_t *p, uint32_t lane) {
+    const uint4 x = *reinterpret_cast<const uint4 *>(p + 16 * lane);
+    const uint2 y = *reinterpret_cast<const uint2 *>(p + 1024 + 8 * lane);
+    asm volatile("" ::: "memory");
+    return v8i{(int)x.x, (int)x.y, (int)x.z, (int)x.w, (int)y.x, (int)y.y, 0, 0};
+}
+// a 16-site block's B operand (either format)
+__device__ __forceinline__ v8i f6_ldb(const uint8_t *p, uint32_t lane) {
+    if constexpr (WLD_F6_B4) {
+        const uint4 x = *reinterpret_cast<const uint4 *>(p + 16 * lane);
+        return v8i{(int)x.x, (int)x.y, (int)x.z, (int)x.w, 0, 0, 0, 0};
+    } else {
+        return f6_ld24(p, lane);
     }
-    static __device__ __forceinline__ uint32_t a_local(int i, uint32_t wave, uint32_t lane) {
-        return 16 * (wave & 3) + 4 * (lane >> 4) + (i & 3);
+}
+// one B block's four MFMAs against the wave's A channels (in: ai, major: am):
+// acc[channel_a][0 / 1] = X / Y (fp4 B: raw, minor bit) or F / G (6-bit B:
+// e2m3, e3m2 reading)
+__device__ __forceinline__ void f6_block_mfma(v4f (&acc)[2][2], const v8i &ai, const v8i &am, const v8i &b) {
+    constexpr int kOne = 0x7F7F7F7F;  // unit E8M0 block scales
+    if constexpr (WLD_F6_B4) {
+        constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
+        const v8i bmin = {b[0] & kMinor, b[1] & kMinor, b[2] & kMinor, b[3] & kMinor, 0, 0, 0, 0};
+        acc[0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, b, acc[0][0], 2, 4, 0, kOne, 0, kOne);
+        acc[0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc[0][1], 2, 4, 0, kOne, 0, kOne);
+        acc[1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, b, acc[1][0], 2, 4, 0, kOne, 0, kOne);
+        acc[1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, bmin, acc[1][1], 2, 4, 0, kOne, 0, kOne);
+    } else {
+        acc[0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, b, acc[0][0], 2, 2, 0, kOne, 0, kOne);
+        acc[0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, b, acc[0][1], 2, 3, 0, kOne, 0, kOne);
+        acc[1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, b, acc[1][0], 2, 2, 0, kOne, 0, kOne);
+        acc[1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, b, acc[1][1], 2, 3, 0, kOne, 0, kOne);
     }
-    static __device__ __forceinline__ uint32_t b_local(int i, uint32_t wave, uint32_t lane) {
-        return 16 * (i >> 2) + (lane & 15);
+}
+// t1 of pair e of a B block's accumulators, mlo its smallest marginal
+__device__ __forceinline__ float f6_terms(const v4f (&acc)[2][2], int e, float R2, float thr_c, float E,
+                                          float &mlo) {
+    if constexpr (WLD_F6_B4)
+        return r2_screen_terms_xy2(acc[0][0][e], acc[0][1][e], acc[1][0][e], acc[1][1][e], R2, thr_c, E, mlo);
+    else
+        return r2_screen_terms_fg(acc[0][0][e], acc[0][1][e], acc[1][0][e], acc[1][1][e], R2, thr_c, E, mlo);
+}
+
+// The screen epilogue of one wave's 16 rows x 64 columns (acc[n] = b block n),
+// the wave being wave wq (0-3) of the 256 threads (ltid) that own tile (ta,
+// tb): whether any pair may pass (cand), and its 16x16 sub-block bits
+// (blocks: the tile's mask word in LDS, zeroed before).
+struct F6Epi {
+    uint32_t ta, tb, wq, lane;
+    uint64_t okA, okB;
+    float R2, thr_c, E, mloc;
+    __device__ __forceinline__ bool valid_pair(int i) const {
+        const uint32_t al = 16 * wq + 4 * (lane >> 4) + (i & 3), bl = (lane & 15) + 16 * (i >> 2);
+        return ((okB >> bl) & 1) && ta * kTile + al < tb * kTile + bl && ((okA >> al) & 1);
+    }
+    __device__ __forceinline__ bool pair_cand(const v4f (&acc)[4][2][2], int i) const {
+        float mlo;
+        const float t1 = f6_terms(acc[i >> 2], i & 3, R2, thr_c, E, mlo);
+        return valid_pair(i) && (t1 > 0.0f || !(mlo >= mloc));
+    }
+    // may any of the wave's pairs pass?
+    __device__ __forceinline__ bool any(const v4f (&acc)[4][2][2]) const {
+        if (okA == ~0ull && okB == ~0ull && ta != tb) {
+            // every pair valid (the tile touches neither the diagonal nor a
+            // filtered/padding site): branch-free, t1's f32 bits as an int (the
+            // maximum is > 0 iff some t1 is > 0; finite terms)
+            int worst = -1;
+            float mlo_all = INFINITY;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                float mlo;
+                worst = max(worst, __float_as_int(f6_terms(acc[i >> 2], i & 3, R2, thr_c, E, mlo)));
+                mlo_all = fminf(mlo_all, mlo);
+            }
+            return worst > 0 || !(mlo_all >= mloc);
+        }
+        bool cand = false;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (!cand) cand = pair_cand(acc, i);
+        return cand;
+    }
+    // the wave's sub-block bits (of the tile's 16: 4 (a / 16) + b / 16)
+    __device__ __forceinline__ unsigned blocks(const v4f (&acc)[4][2][2]) const {
+        unsigned mk = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (pair_cand(acc, i)) mk |= 1u << (4 * wq + (i >> 2));
+        return mk;
     }
 };
+}  // namespace
 
 #ifndef WLD_FP6_WG
 #define WLD_FP6_WG 4  // workgroups per CU
 #endif
+// one 64x64 tile per 4-wave workgroup (WLD_FP6_PAIRS 0)
 __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const uint8_t *__restrict__ a6,
-                                                                  const uint8_t *__restrict__ b4,
+                                                                  const uint8_t *__restrict__ b6,
                                                                   const uint64_t *__restrict__ ok_bits,
                                                                   const uint32_t *__restrict__ tiles, uint32_t n_tiles,
                                                                   uint32_t NK, uint32_t L, uint32_t n_chunk_rows,
                                                                   float thr, OrderArgs o, ScreenArgs sc) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6Stage];
-    __shared__ unsigned long long sBits[kTile];
-    __shared__ uint32_t sRowBase[kTile];
+    __shared__ unsigned long long sMask;
     __shared__ uint32_t sBail;
     if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -930,23 +1041,22 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     const uint32_t tile = blockIdx.x < n_tiles ? tiles[blockIdx.x] : kNoTile;
     if (tile == kNoTile) return;  // (uniform: the whole workgroup)
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
-    // this wave's DMA sources: A of row block 4 ta + wave, B of column block 4 tb + wave
-    const uint8_t *sA = a6 + (size_t)(4 * ta + wave) * NK * kF6ABytes;
-    const uint8_t *sB = b4 + (size_t)(4 * tb + wave) * NK * kF6BBytes;
+    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB = b6 + (size_t)tb * NK * kF6BStage;
+    // a stage's 1-KB pieces (A image, then B image): wave w copies w, w + 4, ...
     auto issue = [&](uint32_t kb, uint32_t buf) {
         const uint32_t gb = lds + buf * kF6Stage;
-        const uint8_t *a = sA + (size_t)kb * kF6ABytes;
-        glds16_s(a, lane16, gb + wave * kF6ABytes);
-        glds16_s(a + 1024, lane16, gb + wave * kF6ABytes + 1024);
-        glds16_s(a + 2048, lane16, gb + wave * kF6ABytes + 2048);
-        glds16_s(sB + (size_t)kb * kF6BBytes, lane16, gb + kF6AStage + wave * kF6BBytes);
+        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b = sB + (size_t)kb * kF6BStage;
+#pragma unroll
+        for (uint32_t p = wave; p < kF6Stage / 1024; p += 4)
+            glds16_s(p < kF6AStage / 1024 ? a + p * 1024 : b + (p * 1024 - kF6AStage), lane16, gb + p * 1024);
     };
     issue(0, 0);
     // the give-up test: read by thread 0 while the first stage is in flight,
-    // published by the first stage barrier (one decision for the workgroup):
-    // 0 go on, 1 give up and mark the set, 2 give up (already marked: the
-    // mark is two atomics on one word each; tens of thousands of workgroups
-    // repeating them serialise for milliseconds)
+    // published to the other waves by the first stage barrier (one decision
+    // for the workgroup; the LDS write completes before this wave reaches
+    // it): 0 go on, 1 give up and mark the set, 2 give up (already marked:
+    // the mark is two atomics on one word each; tens of thousands of
+    // workgroups repeating them serialise for milliseconds)
     if (tid == 0) {
         uint32_t v = 0;
         if (sc.bail) {
@@ -955,39 +1065,19 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
         }
         sBail = v;
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
-    AccF6 acc;
+    v4f acc[4][2][2];  // [b block n][channel_a in / major][X, Y / F, G]
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int x = 0; x < 2; ++x)
 #pragma unroll
-            for (int y = 0; y < 2; ++y) acc.v[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-    // a stage's 16 MFMAs: A (in, major) against the four B blocks of LDS buffer buf
-    auto stage_mfma = [&](uint32_t buf, const v8i &ai, const v8i &am) {
-        const uint8_t *g = smem + buf * kF6Stage;
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const uint4 r = *reinterpret_cast<const uint4 *>(g + kF6AStage + n * kF6BBytes + lane * 16);
-            constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
-            const v8i braw = {(int)r.x, (int)r.y, (int)r.z, (int)r.w, 0, 0, 0, 0};
-            const v8i bmin = {(int)r.x & kMinor, (int)r.y & kMinor, (int)r.z & kMinor, (int)r.w & kMinor, 0, 0, 0, 0};
-            acc.v[n][0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, braw, acc.v[n][0][0], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-            acc.v[n][0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc.v[n][0][1], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-            acc.v[n][1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, braw, acc.v[n][1][0], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-            acc.v[n][1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, bmin, acc.v[n][1][1], 2, 4, 0,
-                                                                              0x7F7F7F7F, 0, 0x7F7F7F7F);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
-    };
-    // the top of a stage: this wave's copies (and register loads) of it landed,
-    // then every other wave's (the barrier); false: the pass is given up
-    auto stage_top = [&](uint32_t kb) -> bool {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // the buffer read last stage is free from here
+            for (int y = 0; y < 2; ++y) acc[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+    uint32_t buf = 0;
+    for (uint32_t kb = 0; kb < NK; ++kb) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of the stage landed
+        __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
         asm volatile("" ::: "memory");
         if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
             if (tid == 0 && sBail == 1) {
@@ -995,40 +1085,160 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
                 atomicOr(sc.cand_buckets, kAbandonBit);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            return false;
+            return;
         }
-        return true;
-    };
-    uint32_t buf = 0;
-    for (uint32_t kb = 0; kb < NK; ++kb) {
-        if (!stage_top(kb)) return;
         if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
-        const uint8_t *pa = smem + buf * kF6Stage + wave * kF6ABytes + lane * 24;
-        const uint2 i0 = *reinterpret_cast<const uint2 *>(pa), i1 = *reinterpret_cast<const uint2 *>(pa + 8),
-                    i2 = *reinterpret_cast<const uint2 *>(pa + 16);
-        const uint2 m0 = *reinterpret_cast<const uint2 *>(pa + 1536), m1 = *reinterpret_cast<const uint2 *>(pa + 1544),
-                    m2 = *reinterpret_cast<const uint2 *>(pa + 1552);
-        const v8i ai = {(int)i0.x, (int)i0.y, (int)i1.x, (int)i1.y, (int)i2.x, (int)i2.y, 0, 0};
-        const v8i am = {(int)m0.x, (int)m0.y, (int)m1.x, (int)m1.y, (int)m2.x, (int)m2.y, 0, 0};
-        stage_mfma(buf, ai, am);
+        const uint8_t *g = smem + buf * kF6Stage;
+        const v8i ai = f6_ld24(g + wave * kF6ABytes, lane), am = f6_ld24(g + wave * kF6ABytes + 1536, lane);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) f6_block_mfma(acc[n], ai, am, f6_ldb(g + kF6AStage + n * kF6BBytes, lane));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
         buf ^= 1;
     }
-    // (the f64 fallback of pair_cand: exact sums from X, Y; the launch uses
-    // the f32 test, sc.f32 == 2)
-    auto sum = [&](int x, int y, int i) -> double {
-        const float2 p = acc.raw(x, i);
-        return ((double)p.x + (y ? -(double)p.y : (double)p.y)) * 0.5;
-    };
-    const DenseArgs dn{nullptr, nullptr, nullptr, nullptr};
-    tile_epilogue<kModeScreen, AccF6>(sum, acc, ta, tb, tid, okA, okB, L, n_chunk_rows, thr, 0, o, dn, sc, sBits,
-                                      sRowBase);
+    const F6Epi ep{ta, tb, wave, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
+    const bool cand = ep.any(acc);
+    if (tid == 0) sMask = 0ull;
+    if (__syncthreads_or(cand)) {
+        // which 16x16 sub-blocks hold a pair that may pass: the candidate
+        // launch computes only those (the others' pairs provably fail)
+        const unsigned mk = ep.blocks(acc);
+        if (mk) atomicOr(&sMask, (unsigned long long)mk);
+        __syncthreads();
+        screen_verdict((uint32_t)sMask, ta, tb, tid, n_chunk_rows, o, sc);
+    } else {
+        screen_verdict(0u, ta, tb, tid, n_chunk_rows, o, sc);
+    }
 }
 
-void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b4,
+// Tile pairs (WLD_FP6_PAIRS 1, the default): one 8-wave workgroup per entry
+// of the pair list, tiles (ta, tb) and (ta, tb + 1) (kF6Single: tile (ta, tb)
+// alone), two workgroups per CU.  Both tiles' rows are the same 64 sites, so
+// one A image per stage serves both: per 128 sequences the workgroup copies
+// A (12 KB) and the two B images, 3/4 of the two single tiles' bytes with fp6
+// B and 5/8 with fp4 B — the stage copies, not the MFMAs, bound the
+// single-tile kernel.  Waves 0-3 compute tile tb, waves 4-7
+// tile tb + 1 (the second B image), each as the single-tile kernel's wave;
+// each half decides its own tile.  A single entry's second half computes on
+// the first B image and decides nothing (it keeps the workgroup's barriers).
+constexpr uint32_t kF6Single = 0x8000u;
+constexpr int kF6PStage = kF6AStage + 2 * kF6BStage;
+__global__ __launch_bounds__(512, 2) void pair_fp6_screen2_kernel(const uint8_t *__restrict__ a6,
+                                                          const uint8_t *__restrict__ b6,
+                                                          const uint64_t *__restrict__ ok_bits,
+                                                          const uint32_t *__restrict__ pairs, uint32_t n_pairs,
+                                                          uint32_t NK, uint32_t L, uint32_t n_chunk_rows, float thr,
+                                                          OrderArgs o, ScreenArgs sc) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6PStage];
+    __shared__ unsigned long long sMask[2];
+    __shared__ uint32_t sBail, sCand[2];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t half = wave >> 2, wq = wave & 3, ltid = tid & 255;
+    const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
+    const uint32_t entry = blockIdx.x < n_pairs ? pairs[blockIdx.x] : kNoTile;
+    if (entry == kNoTile) return;  // (uniform: the whole workgroup)
+    const uint32_t ta = entry >> 16, tb0 = entry & 0x7FFFu;
+    const bool single = (entry & kF6Single) != 0, idle = single && half;  // (uniform per wave)
+    const uint32_t tb = tb0 + (idle ? 0u : half);
+    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB0 = b6 + (size_t)tb0 * NK * kF6BStage;
+    const uint8_t *sB1 = single ? sB0 : sB0 + (size_t)NK * kF6BStage;
+    // a stage's 1-KB pieces (A image, B image of tb, B image of tb + 1): wave w copies w, w + 8, ...
+    auto issue = [&](uint32_t kb, uint32_t buf) {
+        const uint32_t gb = lds + buf * kF6PStage;
+        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b0 = sB0 + (size_t)kb * kF6BStage,
+                      *b1 = sB1 + (size_t)kb * kF6BStage;
+#pragma unroll
+        for (uint32_t p = wave; p < kF6PStage / 1024; p += 8) {
+            const uint32_t off = p * 1024;
+            glds16_s(off < kF6AStage ? a + off
+                                     : off < kF6AStage + kF6BStage ? b0 + (off - kF6AStage)
+                                                                   : b1 + (off - kF6AStage - kF6BStage),
+                     lane16, gb + off);
+        }
+    };
+    issue(0, 0);
+    if (tid == 0) {  // the give-up test (as the single-tile kernel)
+        uint32_t v = 0;
+        if (sc.bail) {
+            const unsigned cc = __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v = cc > sc.bail ? ((cc & kAbandonBit) ? 2u : 1u) : 0u;
+        }
+        sBail = v;
+    }
+    if (tid < 2) sCand[tid] = 0u, sMask[tid] = 0ull;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
+    v4f acc[4][2][2];
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) acc[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+    const uint32_t boff = kF6AStage + (idle ? 0u : half) * kF6BStage;  // this half's B image in a stage
+    uint32_t buf = 0;
+    for (uint32_t kb = 0; kb < NK; ++kb) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of the stage landed
+        __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
+        asm volatile("" ::: "memory");
+        if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
+            if (tid == 0 && sBail == 1) {
+                atomicOr(sc.cand_count, kAbandonBit);
+                atomicOr(sc.cand_buckets, kAbandonBit);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            return;
+        }
+        if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
+        const uint8_t *g = smem + buf * kF6PStage;
+        const v8i ai = f6_ld24(g + wq * kF6ABytes, lane), am = f6_ld24(g + wq * kF6ABytes + 1536, lane);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) f6_block_mfma(acc[n], ai, am, f6_ldb(g + boff + n * kF6BBytes, lane));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
+        buf ^= 1;
+    }
+    const F6Epi ep{ta, tb, wq, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
+    const bool cand = !idle && ep.any(acc);
+    if (cand) sCand[half] = 1u;  // (benign race: every writer stores 1)
+    __syncthreads();
+    const bool mine = sCand[half] != 0;  // (uniform per half)
+    if (mine && !idle) {
+        const unsigned mk = ep.blocks(acc);
+        if (mk) atomicOr(&sMask[half], (unsigned long long)mk);
+    }
+    __syncthreads();
+    if (!idle) screen_verdict(mine ? (uint32_t)sMask[half] : 0u, ta, tb, ltid, n_chunk_rows, o, sc);
+}
+
+void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b6,
                   hipStream_t s) {
     const size_t n = LP / 16 * ((NP + 127) / 128) * 64;
     hipLaunchKernelGGL(frag6_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, codes, w6, (uint32_t)LP,
-                       (uint32_t)NP, a6, b4);
+                       (uint32_t)NP, a6, b6);
+}
+
+#ifndef WLD_FP6_PAIRS
+#define WLD_FP6_PAIRS 1
+#endif
+bool fp6_uses_pairs() { return WLD_FP6_PAIRS != 0; }
+
+// The pair list of a tile list (sorted by (ta, tb)): tiles (ta, tb) and (ta,
+// tb + 1) with tb even form an entry ta << 16 | tb; any other tile is an entry
+// of its own (kF6Single set).  Within a 256-site chunk row the pairs never
+// cross a chunk (four tiles per chunk).  Returned in the tile list's order of
+// first tiles.
+std::vector<uint32_t> fp6_pair_list(const std::vector<uint32_t> &sorted_tiles) {
+    std::vector<uint32_t> out;
+    for (size_t i = 0; i < sorted_tiles.size(); ++i) {
+        const uint32_t t = sorted_tiles[i];
+        if ((t & 1u) == 0 && i + 1 < sorted_tiles.size() && sorted_tiles[i + 1] == t + 1) {
+            out.push_back(t);
+            ++i;
+        } else {
+            out.push_back(t | kF6Single);
+        }
+    }
+    return out;
 }
 
 // Site-major variant (one tile per workgroup, codes read straight into
@@ -1255,15 +1465,23 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     }
     if (m.fp6) {
         // the fp6 screen: R and the sums' bound Tg in its own units (fp6_prepare)
-        sc.R = m.fp6->R;
+        // R rounded up to a multiple of 1/32, so the doubled R2 = 2 R lies on
+        // the accumulators' 1/16 grid (r2_screen_terms_fg: exact marginals;
+        // exact in f32: R <= the sum of the fp6 weights < 2^17)
+        sc.R = std::ceil(m.fp6->R * 32.0) / 32.0;
         sc.Rf = (float)sc.R;
-        if ((double)sc.Rf < sc.R) sc.Rf = nextafterf(sc.Rf, INFINITY);
         sc.f32 = 2;
         sc.bail = m.fp6_bail;
         screen_consts(m.fp6->Tg, 2.0f * sc.Rf, sc.E, sc.mloc);
-        // (one tile per workgroup, the XCD-ordered list)
-        hipLaunchKernelGGL(pair_fp6_screen_kernel, dim3(m.n_tiles), dim3(256), 0, s, m.fp6->a6, m.fp6->b4, ok_bits,
-                           m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
+        if (fp6_uses_pairs() && m.f6_pairs) {
+            // (a tile pair per workgroup, the XCD-ordered pair list)
+            hipLaunchKernelGGL(pair_fp6_screen2_kernel, dim3(m.f6_n_pairs), dim3(512), 0, s, m.fp6->a6, m.fp6->b6,
+                               ok_bits, m.f6_pairs, m.f6_n_pairs, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
+        } else {
+            // (one tile per workgroup, the XCD-ordered list)
+            hipLaunchKernelGGL(pair_fp6_screen_kernel, dim3(m.n_tiles), dim3(256), 0, s, m.fp6->a6, m.fp6->b6,
+                               ok_bits, m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
+        }
         if (screen_done) (void)hipEventRecord(screen_done, s);
         launch_candidates(m, n, idx, ok_bits, o, dn, sc, s);
         return true;

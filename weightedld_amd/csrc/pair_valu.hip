@@ -497,7 +497,8 @@ __global__ __launch_bounds__(256, MF ? (REF ? WLD_VALU_REF_WG : WLD_VALU_MF_WG) 
         for (uint32_t bi = first; bi < nt;) {
             const uint32_t e = tile_buckets ? cand_entry_checked(o, s_pre, bucket_cap, bi) : bi < n_tiles ? bi : ~0u;
             const uint32_t tile = e != ~0u ? tiles[e] : kNoTile;
-            const uint32_t bits = tile_bits ? tile_bits[e] : 0xFFFFu;
+            // (a refused entry reads nothing through e: the guard has reported it)
+            const uint32_t bits = tile_bits && e != ~0u ? tile_bits[e] : 0xFFFFu;
             if (tile_in_range(tile, L))
                 compute_tile(tile, threadIdx.x, bits, 0xFu);  // (a whole-tile entry writes all 64 rows' segments)
             else if (e != ~0u && threadIdx.x == 0)
