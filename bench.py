@@ -434,8 +434,11 @@ def main():
     if not args.wide_weights:
         assert np.array_equal(pre.weights().view(np.uint32), weights.view(np.uint32))
     pre.close()
+    created = []  # every context of the run, closed explicitly at the end (newest first)
+
     def new_ctx():
         c = W.Context(dev_index, kernel)
+        created.append(c)
         if args.no_screen or args.no_prefilter:
             c.set_option("screen", 0)
         if args.no_prefilter:
@@ -464,7 +467,7 @@ def main():
     # RCCL count all_gather ordered after them on that stream, one host wait;
     # rows (if any) then gathered to rank 0 in reference order (shards
     # concatenate in descending rank order: chunk rows descend)
-    shard_step = wdist.ShardStep(ctx, rank, world, device, host_collectives=host_coll)
+    shard_step = wdist.ShardStep(ctx, rank, world, device, host_collectives=host_coll) if dist_on else None
     # N>1 timed steps: two contexts on the same resident inputs, step i's
     # kernel queued on the device behind step i-1's while step i-1's count
     # exchange / host read / row gather complete (PipelinedShardStep)
@@ -640,11 +643,23 @@ def main():
             if rank == 0:
                 checked = [wdist.unpack_rows(g) for _, g in res]
     torch.cuda.synchronize()
+
+    def close_all():
+        # the step streams first (their work done), then the contexts, newest
+        # first, while torch and the HIP runtime are up (not at interpreter exit)
+        if pipe is not None:
+            pipe.close()
+        if shard_step is not None:
+            shard_step.close()
+        for c in reversed(created):
+            c.close()
+
     if dist_on:
         # no collective after this: the other ranks leave, so that rank 0's
         # CPU baseline runs with no rank polling beside it
         dist.destroy_process_group()
     if rank != 0:
+        close_all()
         return
 
     total_pairs = L * (L - 1) // 2
@@ -870,6 +885,7 @@ def main():
             out["rows_check_fp6"] = fp6_rows_check(ctx, buf, weights, L, N, min(thr, 0.01))
             assert out["rows_check_fp6"]["equal"], out["rows_check_fp6"]
     print(json.dumps(out), flush=True)
+    close_all()
 
 
 if __name__ == "__main__":

@@ -118,4 +118,9 @@ def test_launcher_two_ranks_rows_equal_oracle_every_step():
     sc = out["steps_check"]
     assert sc["steps"] == 4 and sc["equal_to_oracle"] == 4 and sc["rows_per_step"] > 1_900_000
     assert out["config"]["rows_passing"] == sc["rows_per_step"]
-    assert out["cpu_baseline"] is None
+    # an N>1 line carries rank 0's CPU baseline too (after the other ranks left),
+    # on the CPUs the process may use, the count justified in the record
+    cb = out["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+    assert cb["host_cpus"]["affinity"] >= cb["cores"] and cb["host_cpus"]["threads_from"]
+    assert out["rows_check"]["one_sided"] == 0

@@ -5,6 +5,7 @@ the C ABI of libweightedld.so: the host pre-pass (FASTA, site filter, Henikoff
 weights) runs in the library's C++ host code, the all-pairs hot path on the
 gfx950 GPU.  There is no CPU fallback for the hot path.
 """
+import atexit
 import ctypes
 import weakref
 import enum
@@ -199,6 +200,26 @@ class PairStore:
     __iter__ = iter
 
 
+# Live contexts, closed (newest first) by an exit handler while the HIP
+# runtime and torch are still up: a context left to its finalizer at
+# interpreter shutdown would destroy its stream and buffers in arbitrary order
+# against torch objects that may still reference them (events, pinned-memory
+# copies recorded on a stream the context ran on).
+_LIVE = weakref.WeakValueDictionary()
+_SEQ = [0]
+
+
+@atexit.register
+def _close_live_contexts():
+    for k in sorted(list(_LIVE.keys()), reverse=True):
+        c = _LIVE.get(k)
+        if c is not None:
+            try:
+                c.close()
+            except Exception:
+                pass
+
+
 class Context:
     """One device context (wld_ctx): HIP stream, device buffers, results."""
 
@@ -219,6 +240,8 @@ class Context:
             check(self._lib.wld_create(device, ctypes.byref(h)), "wld_create")
         self._h = h
         self.device = device
+        _SEQ[0] += 1
+        _LIVE[_SEQ[0]] = self
         if kernel != KERNEL_AUTO:
             self.set_kernel(kernel)
         if ref_sums is not None:

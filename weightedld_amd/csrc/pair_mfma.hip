@@ -1120,9 +1120,16 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
 // tile tb + 1 (the second B image), each as the single-tile kernel's wave;
 // each half decides its own tile.  A single entry's second half computes on
 // the first B image and decides nothing (it keeps the workgroup's barriers).
+// (WLD_F6_PIPE 1: the stage loop with next-stage operands read into registers
+// during this stage's MFMAs; needs ~30 more VGPRs: spills at 4 waves per SIMD)
+#ifndef WLD_F6_PIPE
+#define WLD_F6_PIPE 0
+#endif
 constexpr uint32_t kF6Single = 0x8000u;
+// s_waitcnt immediate (gfx9 encoding): lgkmcnt(0), vmcnt and expcnt at their maxima
+[[maybe_unused]] constexpr int kWaitLgkm0 = 0xC07F;
 constexpr int kF6PStage = kF6AStage + 2 * kF6BStage;
-__global__ __launch_bounds__(512, 2) void pair_fp6_screen2_kernel(const uint8_t *__restrict__ a6,
+__global__ __launch_bounds__(512, 4) void pair_fp6_screen2_kernel(const uint8_t *__restrict__ a6,
                                                           const uint8_t *__restrict__ b6,
                                                           const uint64_t *__restrict__ ok_bits,
                                                           const uint32_t *__restrict__ pairs, uint32_t n_pairs,
@@ -1176,6 +1183,57 @@ __global__ __launch_bounds__(512, 2) void pair_fp6_screen2_kernel(const uint8_t 
 #pragma unroll
             for (int y = 0; y < 2; ++y) acc[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
     const uint32_t boff = kF6AStage + (idle ? 0u : half) * kF6BStage;  // this half's B image in a stage
+#if WLD_F6_PIPE
+    // The stage loop, software-pipelined: stage kb's operands are in registers
+    // when its MFMAs start (read from LDS during stage kb - 1), so no wave
+    // waits on LDS latency after a barrier; the copies of stage kb + 2 go into
+    // the buffer stage kb was read from (free once every wave has passed the
+    // barrier of stage kb); the copies of stage kb + 1 were issued one stage
+    // earlier and are waited for at stage kb's top.
+    struct Ops {
+        v8i ai, am, b[4];
+    };
+    auto ld_ops = [&](uint32_t buf, Ops &r) {
+        const uint8_t *g = smem + buf * kF6PStage;
+        r.ai = f6_ld24(g + wq * kF6ABytes, lane);
+        r.am = f6_ld24(g + wq * kF6ABytes + 1536, lane);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) r.b[n] = f6_ldb(g + boff + n * kF6BBytes, lane);
+    };
+    Ops r0, r1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of stage 0 landed
+    __builtin_amdgcn_s_barrier();                     // ... and every other wave's
+    asm volatile("" ::: "memory");
+    if (sBail) {  // (uniform) give the pass up: leave
+        if (tid == 0 && sBail == 1) {
+            atomicOr(sc.cand_count, kAbandonBit);
+            atomicOr(sc.cand_buckets, kAbandonBit);
+        }
+        return;
+    }
+    if (NK > 1) issue(1, 1);
+    ld_ops(0, r0);
+    // stage kb (its operands in cur; nxt receives stage kb + 1's)
+    auto stage = [&](uint32_t kb, const Ops &cur, Ops &nxt) {
+        if (kb + 1 < NK) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of stage kb + 1 landed
+            __builtin_amdgcn_s_barrier();                     // ... every wave's; every read of stage kb's buffer done
+            asm volatile("" ::: "memory");
+            if (kb + 2 < NK) issue(kb + 2, kb & 1);
+            ld_ops((kb + 1) & 1, nxt);
+        }
+#pragma unroll
+        for (int n = 0; n < 4; ++n) f6_block_mfma(acc[n], cur.ai, cur.am, cur.b[n]);
+        // stage kb + 1's reads done before the next barrier; as the builtin (not
+        // asm) the compiler sees it, so it puts no wait of its own in front of
+        // the next stage's MFMAs (it would wait for the reads issued there)
+        __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    };
+    for (uint32_t kb = 0; kb < NK; kb += 2) {
+        stage(kb, r0, r1);
+        if (kb + 1 < NK) stage(kb + 1, r1, r0);
+    }
+#else
     uint32_t buf = 0;
     for (uint32_t kb = 0; kb < NK; ++kb) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of the stage landed
@@ -1197,6 +1255,7 @@ __global__ __launch_bounds__(512, 2) void pair_fp6_screen2_kernel(const uint8_t 
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
         buf ^= 1;
     }
+#endif
     const F6Epi ep{ta, tb, wq, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
     const bool cand = !idle && ep.any(acc);
     if (cand) sCand[half] = 1u;  // (benign race: every writer stores 1)

@@ -142,7 +142,7 @@ class ShardStep:
     both.  Returns (rows on this rank, gathered [5, n] rows on rank 0 / None).
 
     ctx is anything with the Context methods the step uses
-    (run_chunks_async, run_wait, rows_copy_device, stream_ptr); with a CPU
+    (run_chunks_async, run_wait, rows_copy_device, set_stream); with a CPU
     `device` the step runs in program order on host tensors (gloo).
     host_collectives=True keeps the device's kernels and the context's
     stream but exchanges counts and rows as host tensors (gloo): several
@@ -158,9 +158,29 @@ class ShardStep:
         self.gather = RowGather(rank, world, torch.device("cpu") if self.host else device, group)
         self.cnt_dev = torch.zeros(1, dtype=torch.int64, device=device) if self.host else None
         self.device = device
-        self.stream = (torch.cuda.ExternalStream(ctx.stream_ptr(), device=device) if device.type == "cuda"
-                       else _HostStream())
+        # The context runs on a torch-owned stream (wld_set_stream): the count
+        # collective, its event and the pinned copy below are recorded on a
+        # stream that outlives every torch object referencing it (torch never
+        # destroys its pool streams), whatever order the context and those
+        # objects are released in.  (Round 4 recorded them on the context's own
+        # stream, wrapped as an ExternalStream, and the process crashed at exit,
+        # profiles/r04i/: the context was destroyed by its finalizer at
+        # interpreter shutdown, in no set order against the torch event and
+        # pinned-memory block recorded on the stream it destroyed.)
+        if device.type == "cuda":
+            self.stream = torch.cuda.Stream(device=device)
+            ctx.set_stream(self.stream.cuda_stream)
+        else:
+            self.stream = _HostStream()
         self.rows_seen = False  # some rank had rows in the last finished step
+        # the gathered counts go to pinned host memory by an async copy queued
+        # behind the all_gather; finish() waits on its event and reads them (no
+        # synchronous device-to-host read per step: the host's share of a short
+        # step, e.g. one of eight shards of config 4)
+        self.pinned = device.type == "cuda" and not self.host
+        if self.pinned:
+            self.cnts_host = torch.empty(world, dtype=torch.int64, pin_memory=True)
+            self.cnts_evt = torch.cuda.Event()
 
     def enqueue(self, thr, chunk_begin, chunk_end, kernel_done=None):
         """The pair kernel, its row count and the count all_gather, on the
@@ -176,6 +196,9 @@ class ShardStep:
                 kernel_done.record(self.stream)
             if not self.host:
                 dist.all_gather_into_tensor(g.cnts, g.cnt, group=g.group)
+                if self.pinned:
+                    self.cnts_host.copy_(g.cnts, non_blocking=True)
+                    self.cnts_evt.record(self.stream)
 
     def finish(self):
         """Completes an enqueued step: (rows on this rank, gathered rows on rank 0 / None)."""
@@ -187,8 +210,12 @@ class ShardStep:
             with _stream_scope(self.stream):
                 g.cnt.fill_(int(self.cnt_dev.item()))  # host wait for this step's count
             dist.all_gather_into_tensor(g.cnts, g.cnt, group=g.group)
-        with _stream_scope(self.stream):
-            counts = g.cnts.tolist()  # the step's one host wait when no rank has rows
+        if self.pinned:
+            self.cnts_evt.synchronize()  # the step's one host wait when no rank has rows
+            counts = self.cnts_host.tolist()
+        else:
+            with _stream_scope(self.stream):
+                counts = g.cnts.tolist()  # the step's one host wait when no rank has rows
         self.rows_seen = max(counts) > 0
         n = self.ctx.run_wait()  # returns at once: the stream is idle
         if max(counts) == 0:
@@ -201,6 +228,12 @@ class ShardStep:
     def __call__(self, thr, chunk_begin, chunk_end):
         self.enqueue(thr, chunk_begin, chunk_end)
         return self.finish()
+
+    def close(self):
+        """Waits for the step's stream; the context keeps running on it until
+        its owner closes it (its buffers are freed after that stream's work)."""
+        if not isinstance(self.stream, _HostStream):
+            self.stream.synchronize()
 
 
 class PipelinedShardStep:
@@ -259,6 +292,11 @@ class PipelinedShardStep:
     def drain(self):
         out = self.drain_all()
         return out[-1] if out else None
+
+    def close(self):
+        self.drain_all()
+        for st in self.steps:
+            st.close()
 
 
 def gather_rows(packed, rank, world, group=None):
