@@ -216,8 +216,13 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *                      within 2% of the sums or twice the i8 top digit's, at
  *                      thresholds above any at which it left more than a
  *                      quarter of the tiles as candidates; 0: the i8 screen;
- *                      2: fp6 whenever it applies.  Same rows (a screen only
- *                      decides which tiles are computed).
+ *                      2: fp6 whenever it applies; 3: auto without the
+ *                      sample run (below).  Auto decides a threshold it has
+ *                      not seen from a sample run first (about 1/64 of the
+ *                      tiles screened on fp6, counting only): past a
+ *                      sixteenth of them as candidates the pass screens on
+ *                      i8.  Same rows (a screen only decides which tiles are
+ *                      computed).
  *   WLD_OPT_FUSED_SCAN 1 (default): after a screen, the run's chunk scan runs
  *                      in the candidate launch's last workgroup (ranges up to
  *                      4096 chunks); 0: as a launch of its own (the kernel
@@ -419,6 +424,9 @@ typedef struct {
     int screen_fp6;          /* screened == 1 on fp6 x fp4 block-scaled MFMA (WLD_OPT_SCREEN_FP6), not i8;
                                 2: the fp6 screen gave the pass up (more than a sixteenth of the tiles were
                                 candidates) and it re-ran on the i8 screen */
+    int fp6_sampled;         /* 1: this pass's screen (fp6 or i8) was chosen by the fp6 screen's sample run
+                                (WLD_OPT_SCREEN_FP6 1: about 1/64 of the tiles screened first, at a
+                                threshold not decided before) */
     uint64_t progress_filled; /* per-chunk progress (wld_run_host with a callback): chunk reports the
                                  host made up from the chunk pair counts because the pass's log lacked
                                  their entries once it had completed; 0 unless the kernels' chunk

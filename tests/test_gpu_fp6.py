@@ -130,9 +130,39 @@ def test_fp6_handover_to_i8(W):
     c.close()
 
 
+def test_fp6_sample_run_on_ld_blocks(W):
+    """Linkage blocks, auto (WLD_OPT_SCREEN_FP6 1): the fp6 screen's sample
+    run (about 1/64 of the tiles, counting only) finds nearly every sampled
+    tile a candidate, so the first pass at that threshold already screens on
+    i8 (no pass is given up), and so does a lower threshold with no new
+    sample; on the bench's random data the sample keeps fp6, and a higher
+    threshold needs no new sample.  Rows equal the oracle's throughout."""
+    import bench
+    L, N, thr = 4096, 2000, 0.05
+    buf = bench.ld_blocks(L, N, seed=7)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    c = W.Context(0)
+    c.load(buf, w)
+    for t, sampled in ((thr, 1), (0.03, 0), (thr, 0)):
+        c.run(t)
+        st = c.stats()
+        assert st["fp6_sampled"] == sampled and st["screen_fp6"] == 0 and st["screened"] in (1, 3, 4), (t, st)
+        _bits_equal(c.rows(), O.all_pairs(buf, w, np.float32(t)))
+    buf = bench.synth(L, N)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    c.load(buf, w)
+    for t, sampled in ((0.05, 1), (0.1, 0), (0.05, 0)):
+        c.run(t)
+        st = c.stats()
+        assert st["fp6_sampled"] == sampled and st["screen_fp6"] == 1, (t, st)
+        _bits_equal(c.rows(), O.all_pairs(buf, w, np.float32(t)))
+    c.close()
+
+
 def test_fp6_abandoned_pass_on_ld_blocks(W):
     """Linkage blocks: nearly every tile holds a pair the fp6 bound (1.4%
-    residual on these weights) cannot reject.  Auto: the first pass gives up
+    residual on these weights) cannot reject.  Auto without the sample run
+    (WLD_OPT_SCREEN_FP6 3, the safety net behind it): the first pass gives up
     after a sixteenth of the tiles and re-runs on i8 inside the same call;
     rows equal the oracle's.  With per-chunk progress, or a caller's count
     word (the N>1 step's collective reads it), the pass is never given up:
@@ -146,6 +176,7 @@ def test_fp6_abandoned_pass_on_ld_blocks(W):
     ref = O.all_pairs(buf, w, np.float32(thr))
     assert len(ref["site_a"]) > 1000
     c = W.Context(0)
+    c.set_option("screen_fp6", 3)
     c.load(buf, w)
     c.run(thr)
     st = c.stats()

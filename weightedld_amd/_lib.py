@@ -63,6 +63,7 @@ class RunStats(ctypes.Structure):
         ("candidate_blocks", ctypes.c_uint64),
         ("candidate_pairs", ctypes.c_uint64),
         ("screen_fp6", ctypes.c_int),
+        ("fp6_sampled", ctypes.c_int),
         ("progress_filled", ctypes.c_uint64),
     ]
 

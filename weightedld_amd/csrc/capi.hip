@@ -116,6 +116,10 @@ struct wld_ctx {
     // auto: the largest threshold at which the fp6 screen left more than a
     // sixteenth of the tiles (there and below, the i8 screen's tighter bound)
     float fp6_bad_thr = -1.0f;
+    // auto: the smallest threshold at which the fp6 screen's sample run found
+    // few enough candidate tiles (there and above no sample run is needed)
+    float fp6_good_thr = INFINITY;
+    DevBuf fp6_probe_buf;  // the sample run's two counts
     float screen2_bad_thr = -1.0f;
     // auto, lib.rs's order: the largest threshold at which the exact candidate
     // pairs were more than a tenth of all pairs (then the full f32 kernel)
@@ -123,7 +127,7 @@ struct wld_ctx {
     bool ref_pairs_pass = false;  // the pass staged exact candidate pairs (ref_rows_kernel)
     bool opt_site_major = false, opt_valu_plain = false;
     bool opt_fused_scan = true;  // WLD_OPT_FUSED_SCAN: the chunk scan in the candidate launch's last workgroup
-    int opt_fp6 = 1;             // WLD_OPT_SCREEN_FP6: 0 off, 1 auto, 2 whenever it applies
+    int opt_fp6 = 1;             // WLD_OPT_SCREEN_FP6: 0 off, 1 auto, 2 whenever it applies, 3 auto without the sample run
     bool opt_ref_sums = true;  // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order (default)
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
 
@@ -136,6 +140,7 @@ struct wld_ctx {
     DevBuf w6, f6a, f6b;
     Fp6Screen f6{};
     bool fp6_tried = false;   // fp6_prepare ran for this load
+    bool fp6_sampled = false; // this pass's screen was chosen by a sample run (fp6_sample)
     bool fp6_ok = false;      // operands built for this load (the weights allow it)
     bool fp6_pass = false;    // the last pass screened on fp6
     bool fp6_better = false;  // ... and its residual is within twice the i8 top digit's (auto)
@@ -191,7 +196,7 @@ struct wld_ctx {
         // work queued on a borrowed stream (wld_set_stream) may still use the
         // buffers: it completes before they are freed
         if (stream && stream != own_stream) (void)hipStreamSynchronize(stream);
-        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &rcodes, &rw, &w6, &f6a, &f6b, &tiles, &cand, &f6_pairs,
+        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &rcodes, &rw, &w6, &f6a, &f6b, &tiles, &cand, &f6_pairs, &fp6_probe_buf,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &chunk_left, &prog_n, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
@@ -330,6 +335,7 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     // a new data set: the auto screen policy (thresholds learned on the last
     // one) starts over; the reference-order layout is rebuilt when needed
     c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = c->fp6_bad_thr = -1.0f;
+    c->fp6_good_thr = INFINITY;
     c->have_ref = false;
     c->LP = round_up(std::max<size_t>(L, 1), kChunk);
     c->NP = round_up(std::max<size_t>(N, 1), kSeqPad);
@@ -707,15 +713,15 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         c->screened2 = m.screen && m.screen2;
         for (int t = 0; t < 3; ++t) m.resid[t] = c->wst.resid[t];
         // the one-plane screen on fp6 x fp4 MFMA where the load allows it
-        m.fp6 = c->fp6_ok && (c->opt_fp6 == 2 || (c->opt_fp6 == 1 && c->fp6_better && thr > c->fp6_bad_thr))
+        const bool fp6_auto = c->opt_fp6 == 1 || c->opt_fp6 == 3;
+        m.fp6 = c->fp6_ok && (c->opt_fp6 == 2 || (fp6_auto && c->fp6_better && thr > c->fp6_bad_thr))
                     ? &c->f6 : nullptr;
         // auto: past a sixteenth of the tiles as candidates the fp6 screen
         // gives the pass up and run_complete re-runs it on the i8 screen (not
         // with per-chunk progress, which a re-run does not report again, nor
         // with a caller's count word, which a collective may read before the
         // re-run rewrites it)
-        m.fp6_bail = c->opt_fp6 == 1 && !c->prog_pass && !c->pend.count_out ? std::max<uint32_t>(c->n_tiles / 16, 1)
-                                                                                : 0;
+        m.fp6_bail = fp6_auto && !c->prog_pass && !c->pend.count_out ? std::max<uint32_t>(c->n_tiles / 16, 1) : 0;
         m.f6_pairs = c->f6_n_pairs ? ptr<uint32_t>(c->f6_pairs) : nullptr;
         m.f6_n_pairs = c->f6_n_pairs;
         for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
@@ -848,6 +854,7 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
             if (value < 0 || value > 4) return fail(WLD_E_ARG, "WLD_OPT_SCREEN takes 0 to 4");
             c->opt_screen = (int)value;
             c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = c->fp6_bad_thr = -1.0f;
+            c->fp6_good_thr = INFINITY;
             break;
         case WLD_OPT_TILE_ORDER:
             c->opt_tile_rows = value != 0;
@@ -863,7 +870,8 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
         case WLD_OPT_VALU_PLAIN: c->opt_valu_plain = value != 0; break;
         case WLD_OPT_REF_SUMS:
             c->opt_ref_sums = value != 0;
-            c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = c->fp6_bad_thr = -1.0f;  // the policy's break-even differs
+            c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = c->fp6_bad_thr = -1.0f;
+            c->fp6_good_thr = INFINITY;  // the policy's break-even differs
             break;
         case WLD_OPT_STAGING_ROWS:
             if (value < 1) return fail(WLD_E_ARG, "WLD_OPT_STAGING_ROWS must be >= 1");
@@ -875,9 +883,10 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
             break;
         case WLD_OPT_FUSED_SCAN: c->opt_fused_scan = value != 0; break;
         case WLD_OPT_SCREEN_FP6:
-            if (value < 0 || value > 2) return fail(WLD_E_ARG, "WLD_OPT_SCREEN_FP6 takes 0 to 2");
+            if (value < 0 || value > 3) return fail(WLD_E_ARG, "WLD_OPT_SCREEN_FP6 takes 0 to 3");
             c->opt_fp6 = (int)value;
-            c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = c->fp6_bad_thr = -1.0f;  // another screen's break-even
+            c->screen_bad_thr = c->screen2_bad_thr = c->ref_pairs_bad_thr = c->fp6_bad_thr = -1.0f;
+            c->fp6_good_thr = INFINITY;  // another screen's break-even
             break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }
@@ -1195,6 +1204,50 @@ int enqueue_pass(wld_ctx *c) {
     return WLD_OK;
 }
 
+// The fp6 screen's eligibility for this pass, decided from a sample (auto,
+// WLD_OPT_SCREEN_FP6 1) instead of a given-up pass: on linkage-structured
+// data the fp6 rounding leaves nearly every tile a candidate, and a pass that
+// gives up past a sixteenth of them still costs several times a screen
+// (DESIGN.md §4.1).  Every stride-th entry of the screen's list (about 1/64
+// of it) is screened, counting only; past a sixteenth of the sampled tiles as
+// candidates the threshold (and any lower one) goes to the i8 screen, else it
+// (and any higher one) stays on fp6 with no further sample.  Small lists
+// (fewer than 2,048 tiles) take the pass itself as the test, as before.
+int fp6_sample(wld_ctx *c, float thr) {
+    if (c->opt_fp6 != 1 || !c->fp6_ok || !c->fp6_better || !(thr > c->fp6_bad_thr) || thr >= c->fp6_good_thr)
+        return WLD_OK;
+    if (c->kernel != WLD_KERNEL_MFMA || !c->use_frag || !c->opt_prefilter || !(thr > 0.0f) || c->opt_screen == 0 ||
+        c->n_tiles < 2048)
+        return WLD_OK;
+    WLD_TRY(ensure(c->fp6_probe_buf, 2 * sizeof(unsigned)));
+    MfmaLaunch m{};
+    m.wplanes = ptr<int8_t>(c->planes);
+    m.tiles = ptr<uint32_t>(c->tiles);
+    m.n_tiles = c->n_tiles;
+    m.L = (uint32_t)c->L;
+    m.NP = (uint32_t)c->NP;
+    m.LP = (uint32_t)c->LP;
+    m.n_chunk_rows = chunk_rows_of(c->L);
+    m.thr = thr;
+    m.nonneg = c->wst.nonneg;
+    m.fp6 = &c->f6;
+    m.f6_pairs = c->f6_n_pairs ? ptr<uint32_t>(c->f6_pairs) : nullptr;
+    m.f6_n_pairs = c->f6_n_pairs;
+    const uint32_t entries = m.f6_pairs ? m.f6_n_pairs : m.n_tiles;
+    const uint32_t stride = std::max<uint32_t>(1, std::min<uint32_t>(64, entries / 256));
+    launch_fp6_probe(m, ptr<unsigned>(c->fp6_probe_buf), stride, c->stream);
+    HIP_TRY(hipGetLastError());
+    unsigned h[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(h, c->fp6_probe_buf.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->fp6_sampled = true;
+    if ((uint64_t)h[0] * 16 > h[1])
+        c->fp6_bad_thr = std::max(c->fp6_bad_thr, thr);
+    else
+        c->fp6_good_thr = std::min(c->fp6_good_thr, thr);
+    return WLD_OK;
+}
+
 // Phase 1 of a run over linear chunks [lin_begin, lin_end): sizing, then the
 // first pass, enqueued.  Staging starts at min(pairs, 32M rows); the pair
 // kernels count every passing row but store only below capacity, so an
@@ -1206,6 +1259,8 @@ int run_enqueue(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uns
     c->pend.active = false;
     if (!c->fp6_tried && c->opt_fp6 != 0) WLD_TRY(fp6_prepare(c));
     WLD_TRY(build_tiles(c, lin_begin, lin_end));
+    c->fp6_sampled = false;
+    WLD_TRY(fp6_sample(c, thr));
     const uint64_t pairs = pairs_in_chunks(c->L, lin_begin, lin_end);
     const uint32_t T = (uint32_t)(c->LP / kTile);
     const uint32_t n_chunks = n * (n + 1) / 2;
@@ -1378,6 +1433,7 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     c->stats.tiles = c->n_tiles;
     c->stats.screened = c->ref_pairs_pass ? 4 : c->screened ? (c->screened2 ? 3 : 1) : 0;
     c->stats.screen_fp6 = c->fp6_pass ? 1 : abandoned ? 2 : 0;
+    c->stats.fp6_sampled = c->fp6_sampled ? 1 : 0;
     c->stats.candidate_pairs = c->ref_pairs_pass ? h[0] : 0;
     // auto: a threshold at which even the i8 screen leaves more than half the
     // tiles is not screened from now on (nor any lower one): the screen costs a

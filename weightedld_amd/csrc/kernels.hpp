@@ -268,6 +268,10 @@ struct MfmaLaunch {
     const uint32_t *f6_pairs;
     uint32_t f6_n_pairs;
 };
+// The fp6 screen's sample run over every stride-th entry of its list: probe[0]
+// = the sampled tiles holding a pair its bound cannot reject, probe[1] = the
+// sampled tiles (m as for the pass; nothing else is written)
+void launch_fp6_probe(const MfmaLaunch &m, unsigned *probe, uint32_t stride, hipStream_t s);
 // Enqueues the MFMA pair kernel(s) of one pass; returns true when a screen
 // (one- or two-plane) ran (then screen_done, if given, is recorded between
 // the two launches).

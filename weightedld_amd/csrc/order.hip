@@ -69,14 +69,20 @@ __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t
         if (state[kCursorSeen] > o.st_capacity || state[1] > out_cap) return;  // (uniform) the host redoes it
         rows = state[1];
     }
-    const uint32_t base = chunk_base[blockIdx.x];
-    const uint64_t next = blockIdx.x + 1 < count ? chunk_base[blockIdx.x + 1] : rows;
-    if (next == base) return;  // (uniform) no row in this chunk
-    const uint32_t lin = lin_begin + blockIdx.x;
+    // work items (chunk, 16-row slice), chunk-major, over a capped grid (a
+    // grid of every item held the screen of the next step out of its CU
+    // slots while both ran)
+    constexpr uint32_t kSlices = kChunk / kGatherRows;
+    for (uint32_t item = blockIdx.x; item < count * kSlices; item += gridDim.x) {
+    const uint32_t ci = item / kSlices, slice = item % kSlices;
+    const uint32_t base = chunk_base[ci];
+    const uint64_t next = ci + 1 < count ? chunk_base[ci + 1] : rows;
+    if (next == base) continue;  // (uniform) no row in this chunk
+    const uint32_t lin = lin_begin + ci;
     uint32_t row, col;
     chunk_of_linear(n_chunk_rows, lin, row, col);
     const uint32_t tid = threadIdx.x;
-    const uint32_t r0 = blockIdx.y * kGatherRows;
+    const uint32_t r0 = slice * kGatherRows;
     const uint32_t a = row * kChunk + tid;
     // the tiles the pair kernel computed (b tile >= a tile, inside L) each
     // wrote their 64 counts; the other bytes of the dword are stale
@@ -93,7 +99,7 @@ __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t
     if ((tid & 63) == 63) sWave[tid >> 6] = incl;
     const uint32_t slice_end = r0 + kGatherRows;
     // the slice's own rows: any?
-    if (!__syncthreads_or(tid >= r0 && tid < slice_end && rowtot != 0)) return;
+    if (!__syncthreads_or(tid >= r0 && tid < slice_end && rowtot != 0)) continue;  // (after a barrier: sWave is free)
     if (tid >= r0 && tid < slice_end) {  // this slice's rows
         uint32_t wbase = 0;
         for (uint32_t k = 0; k < (tid >> 6); ++k) wbase += sWave[k];
@@ -139,6 +145,8 @@ __global__ __launch_bounds__(256) void gather_kernel(OrderArgs o, const uint32_t
         out_dp[dst[r]] = fdp[r];
         out_r2[dst[r]] = fr2[r];
     }
+    __syncthreads();  // the slice tables are rewritten by the next item
+    }
 }
 
 // tiles of each chunk of [lin_begin, lin_begin + count) in the pair kernels'
@@ -177,7 +185,10 @@ void launch_gather(const OrderArgs &o, const uint32_t *chunk_base, uint32_t lin_
                    uint64_t out_cap, const uint32_t *site_map, uint32_t *out_a, uint32_t *out_b, float *out_d,
                    float *out_dp, float *out_r2, hipStream_t s) {
     if (!count) return;
-    hipLaunchKernelGGL(gather_kernel, dim3(count, kChunk / kGatherRows), dim3(256), 0, s, o, chunk_base, lin_begin,
+    // two workgroups per CU at most (C4 at 16 slices per chunk would be 50,560)
+    constexpr uint32_t kGatherGrid = 512;
+    const uint32_t items = count * (kChunk / kGatherRows);
+    hipLaunchKernelGGL(gather_kernel, dim3(std::min(items, kGatherGrid)), dim3(256), 0, s, o, chunk_base, lin_begin,
                        count, n_chunk_rows, L, rows, state, out_cap, site_map, out_a, out_b, out_d, out_dp, out_r2);
 }
 

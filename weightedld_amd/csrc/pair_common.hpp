@@ -10,22 +10,63 @@ namespace wld {
 // -ffp-contract=off, divisions are IEEE-rounded, fminf/fmaxf ignore NaN like
 // Rust's f32::min/max).  Inputs are the four masked weight sums of
 // lib.rs:423-480: total_weight, PA (a major), PB (b major), ld_obs[3] (both).
-__device__ __forceinline__ void ld_epilogue(float total_weight, float PA, float PB, float ld3, float &d_out,
-                                            float &dp_out, float &r2_out) {
+//
+// The eight quotients by total_weight (WLD_EPI_DIVT 1, the default) are the
+// IEEE f32 quotients computed as RN_f32(x * r) in f64, r a reciprocal of
+// total_weight refined to within a few f64 ulps (one hardware estimate, two
+// Newton steps), instead of eight f32 division sequences.  Why that is the
+// correctly rounded quotient: a midpoint m between two f32 values (a 25-bit
+// odd significand M) can equal x / T only if T is a power of two, and then
+// x / T is an f32 value itself, so no quotient of two f32 values is a tie;
+// and a quotient that is not a midpoint lies at least 1 / (M U) >= 2^-49 of m
+// from it (|x - m T| is at least the unit of m T's last place, x = X 2^a with
+// 24-bit X, T = U 2^c), while RN_f64(x * r) is within ~2^-51 of x / T: both
+// round to the same f32 value (subnormal results too: their midpoints are
+// coarser).  T = 0 or non-finite takes the plain divisions (IEEE's inf / NaN).
+#ifndef WLD_EPI_DIVT
+#define WLD_EPI_DIVT 1
+#endif
+// (r0: the estimate to refine; the device's v_rcp_f64, the host check's a
+// coarser one, the f32 reciprocal)
+__host__ __device__ __forceinline__ double recip_f64(double t, double r0) {
+    double r = r0;
+    double e = fma(-t, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-t, r, 1.0);
+    return fma(r, e, r);
+}
+__host__ __device__ __forceinline__ void ld_epilogue(float total_weight, float PA, float PB, float ld3, float &d_out,
+                                                     float &dp_out, float &r2_out) {
     float ld_obs0, ld_obs1, ld_obs2, ld_obs3 = ld3;
     float Pa = total_weight - PA;
     float Pb = total_weight - PB;
     ld_obs2 = PA - ld_obs3;
     ld_obs1 = PB - ld_obs3;
     ld_obs0 = Pa - ld_obs1;
-    PA = PA / total_weight;
-    PB = PB / total_weight;
-    Pa = Pa / total_weight;
-    Pb = Pb / total_weight;
-    ld_obs0 = ld_obs0 / total_weight;
-    ld_obs1 = ld_obs1 / total_weight;
-    ld_obs2 = ld_obs2 / total_weight;
-    ld_obs3 = ld_obs3 / total_weight;
+    if (WLD_EPI_DIVT && total_weight != 0.0f && fabsf(total_weight) <= 3.4028235e38f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const double r = recip_f64((double)total_weight, __builtin_amdgcn_rcp((double)total_weight));
+#else
+        const double r = recip_f64((double)total_weight, (double)(1.0f / total_weight));
+#endif
+        PA = (float)((double)PA * r);
+        PB = (float)((double)PB * r);
+        Pa = (float)((double)Pa * r);
+        Pb = (float)((double)Pb * r);
+        ld_obs0 = (float)((double)ld_obs0 * r);
+        ld_obs1 = (float)((double)ld_obs1 * r);
+        ld_obs2 = (float)((double)ld_obs2 * r);
+        ld_obs3 = (float)((double)ld_obs3 * r);
+    } else {
+        PA = PA / total_weight;
+        PB = PB / total_weight;
+        Pa = Pa / total_weight;
+        Pb = Pb / total_weight;
+        ld_obs0 = ld_obs0 / total_weight;
+        ld_obs1 = ld_obs1 / total_weight;
+        ld_obs2 = ld_obs2 / total_weight;
+        ld_obs3 = ld_obs3 / total_weight;
+    }
     const float PAB = PA * PB;
     const float PAb = PA * Pb;
     const float PaB = Pa * PB;

@@ -402,6 +402,12 @@ struct ScreenArgs {
     // listed gives the pass up (kAbandonBit) instead of computing its tile
     // (0: never)
     uint32_t bail;
+    // the fp6 screen's sample run (capi.hip fp6_probe): workgroup i screens
+    // list entry i * probe_stride + i % probe_stride and only counts, into
+    // probe[0] its tiles that hold a pair the bound cannot reject and into
+    // probe[1] its tiles (no candidate list, counts or progress written)
+    unsigned *probe;
+    uint32_t probe_stride;
 };
 
 // Reference epilogue of one pair from its exact sums (fixed-point units):
@@ -1034,11 +1040,12 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6Stage];
     __shared__ unsigned long long sMask;
     __shared__ uint32_t sBail;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
+    if (!sc.probe && blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
     // (kNoTile: padding of an XCD-ordered list, or past the end of the grid)
-    const uint32_t tile = blockIdx.x < n_tiles ? tiles[blockIdx.x] : kNoTile;
+    const uint32_t ei = sc.probe ? blockIdx.x * sc.probe_stride + blockIdx.x % sc.probe_stride : blockIdx.x;
+    const uint32_t tile = ei < n_tiles ? tiles[ei] : kNoTile;
     if (tile == kNoTile) return;  // (uniform: the whole workgroup)
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
     const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB = b6 + (size_t)tb * NK * kF6BStage;
@@ -1097,6 +1104,14 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     }
     const F6Epi ep{ta, tb, wave, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
     const bool cand = ep.any(acc);
+    if (sc.probe) {  // the sample run: count, decide nothing
+        const bool any = __syncthreads_or(cand);
+        if (tid == 0) {
+            if (any) atomicAdd(sc.probe, 1u);
+            atomicAdd(sc.probe + 1, 1u);
+        }
+        return;
+    }
     if (tid == 0) sMask = 0ull;
     if (__syncthreads_or(cand)) {
         // which 16x16 sub-blocks hold a pair that may pass: the candidate
@@ -1138,11 +1153,12 @@ __global__ __launch_bounds__(512, 4) void pair_fp6_screen2_kernel(const uint8_t 
     __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6PStage];
     __shared__ unsigned long long sMask[2];
     __shared__ uint32_t sBail, sCand[2];
-    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
+    if (!sc.probe && blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t half = wave >> 2, wq = wave & 3, ltid = tid & 255;
     const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
-    const uint32_t entry = blockIdx.x < n_pairs ? pairs[blockIdx.x] : kNoTile;
+    const uint32_t ei = sc.probe ? blockIdx.x * sc.probe_stride + blockIdx.x % sc.probe_stride : blockIdx.x;
+    const uint32_t entry = ei < n_pairs ? pairs[ei] : kNoTile;
     if (entry == kNoTile) return;  // (uniform: the whole workgroup)
     const uint32_t ta = entry >> 16, tb0 = entry & 0x7FFFu;
     const bool single = (entry & kF6Single) != 0, idle = single && half;  // (uniform per wave)
@@ -1261,6 +1277,13 @@ __global__ __launch_bounds__(512, 4) void pair_fp6_screen2_kernel(const uint8_t 
     if (cand) sCand[half] = 1u;  // (benign race: every writer stores 1)
     __syncthreads();
     const bool mine = sCand[half] != 0;  // (uniform per half)
+    if (sc.probe) {  // the sample run: count, decide nothing
+        if (ltid == 0 && !idle) {
+            if (mine) atomicAdd(sc.probe, 1u);
+            atomicAdd(sc.probe + 1, 1u);
+        }
+        return;
+    }
     if (mine && !idle) {
         const unsigned mk = ep.blocks(acc);
         if (mk) atomicOr(&sMask[half], (unsigned long long)mk);
@@ -1421,6 +1444,46 @@ void launch_candidates(const MfmaLaunch &m, uint32_t n, uint32_t idx, const uint
 }
 }  // namespace
 
+namespace {
+// the fp6 screen's R, E, mloc in its own units (fp6_prepare): R rounded up to
+// a multiple of 1/32, so the doubled R2 = 2 R lies on the accumulators' grid
+// (1/8 or 1/16: the exact marginals of r2_screen_terms_xy2 / _fg; exact in f32,
+// R <= the sum of the fp6 weights < 2^17); Tg bounds every doubled T
+void fp6_screen_args(const MfmaLaunch &m, ScreenArgs &sc) {
+    sc.R = std::ceil(m.fp6->R * 32.0) / 32.0;
+    sc.Rf = (float)sc.R;
+    sc.f32 = 2;
+    screen_consts(m.fp6->Tg, 2.0f * sc.Rf, sc.E, sc.mloc);
+}
+// the fp6 screen over the pair list (or the tile list), every entry, or with
+// sc.probe every stride-th one
+void launch_fp6_screen(const MfmaLaunch &m, const uint64_t *ok_bits, const OrderArgs &o, const ScreenArgs &sc,
+                       uint32_t stride, hipStream_t s) {
+    if (fp6_uses_pairs() && m.f6_pairs) {
+        // (a tile pair per workgroup, the XCD-ordered pair list)
+        hipLaunchKernelGGL(pair_fp6_screen2_kernel, dim3((m.f6_n_pairs + stride - 1) / stride), dim3(512), 0, s,
+                           m.fp6->a6, m.fp6->b6, ok_bits, m.f6_pairs, m.f6_n_pairs, m.fp6->NK, m.L, m.n_chunk_rows,
+                           m.thr, o, sc);
+    } else {
+        // (one tile per workgroup, the XCD-ordered list)
+        hipLaunchKernelGGL(pair_fp6_screen_kernel, dim3((m.n_tiles + stride - 1) / stride), dim3(256), 0, s,
+                           m.fp6->a6, m.fp6->b6, ok_bits, m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr,
+                           o, sc);
+    }
+}
+}  // namespace
+
+void launch_fp6_probe(const MfmaLaunch &m, unsigned *probe, uint32_t stride, hipStream_t s) {
+    const uint64_t *ok_bits = reinterpret_cast<const uint64_t *>(m.wplanes + okbits_offset(m.NP));
+    ScreenArgs sc{};
+    sc.nonneg = m.nonneg;
+    fp6_screen_args(m, sc);
+    sc.probe = probe;
+    sc.probe_stride = std::max<uint32_t>(stride, 1);
+    (void)hipMemsetAsync(probe, 0, 2 * sizeof(unsigned), s);
+    launch_fp6_screen(m, ok_bits, OrderArgs{}, sc, sc.probe_stride, s);
+}
+
 bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *dense, hipStream_t s,
                       hipEvent_t screen_done) {
     const DenseArgs dn = dense ? *dense : DenseArgs{nullptr, nullptr, nullptr, nullptr};
@@ -1523,24 +1586,9 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
         return true;
     }
     if (m.fp6) {
-        // the fp6 screen: R and the sums' bound Tg in its own units (fp6_prepare)
-        // R rounded up to a multiple of 1/32, so the doubled R2 = 2 R lies on
-        // the accumulators' 1/16 grid (r2_screen_terms_fg: exact marginals;
-        // exact in f32: R <= the sum of the fp6 weights < 2^17)
-        sc.R = std::ceil(m.fp6->R * 32.0) / 32.0;
-        sc.Rf = (float)sc.R;
-        sc.f32 = 2;
+        fp6_screen_args(m, sc);
         sc.bail = m.fp6_bail;
-        screen_consts(m.fp6->Tg, 2.0f * sc.Rf, sc.E, sc.mloc);
-        if (fp6_uses_pairs() && m.f6_pairs) {
-            // (a tile pair per workgroup, the XCD-ordered pair list)
-            hipLaunchKernelGGL(pair_fp6_screen2_kernel, dim3(m.f6_n_pairs), dim3(512), 0, s, m.fp6->a6, m.fp6->b6,
-                               ok_bits, m.f6_pairs, m.f6_n_pairs, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
-        } else {
-            // (one tile per workgroup, the XCD-ordered list)
-            hipLaunchKernelGGL(pair_fp6_screen_kernel, dim3(m.n_tiles), dim3(256), 0, s, m.fp6->a6, m.fp6->b6,
-                               ok_bits, m.tiles, m.n_tiles, m.fp6->NK, m.L, m.n_chunk_rows, m.thr, o, sc);
-        }
+        launch_fp6_screen(m, ok_bits, o, sc, 1, s);
         if (screen_done) (void)hipEventRecord(screen_done, s);
         launch_candidates(m, n, idx, ok_bits, o, dn, sc, s);
         return true;
