@@ -685,7 +685,10 @@ def main():
         dom_ms = screen_ms if screened else kernel_ms
         achieved = alg_ops / (dom_ms * 1e-3) / 1e12
         if fp6:
-            kname = "pair_fp6_screen_kernel<fp6 x fp4 16x16x128>"
+            # tile pairs (two tiles sharing one A image per workgroup) unless the
+            # tile list outgrows the pair list's 15-bit tile index
+            kname = ("pair_fp6_screen2_kernel<tile pairs, fp6 x fp4 16x16x128>" if (L + 63) // 64 <= 0x7FFF
+                     else "pair_fp6_screen_kernel<fp6 x fp4 16x16x128>")
         elif screen_kind == 4:
             kname = "pair_mfma_kernel<candidate pairs, %d planes>" % min(planes, 2)
         elif screened:
@@ -750,6 +753,9 @@ def main():
     tr = load_traffic(args.config + ("-unweighted" if args.unweighted else ""), "fp6" if fp6 else kern_name)
     same_kernel = (screen_kind == 1 and args.thr is None and not args.wide_weights
                    and not (args.rehearse_dist and args.rehearse_shard > 1))
+    # ... and only for the kernel those counters were collected on
+    if tr and tr.get("kernel") and tr["kernel"].split("<")[0] != roof.get("kernel", "").split("<")[0]:
+        tr = None
     roof["traffic"] = tr.get("hbm_bytes_per_launch") if tr and same_kernel else None
     hbm_alg = shard_pairs * 2.0 * N / (kernel_ms * 1e-3) / 1e9  # 2N bytes per pair
     # the arithmetic the timed steps executed
