@@ -23,6 +23,10 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format c
 timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --output-format csv -d $out/pmc_l2 -o l2 -- \
   python3 bench.py $bargs > $out/pmc_l2.log 2>&1 || { echo "pmc l2 failed"; exit 1; }
 
+# the C2 item kernel's SIMD time
+timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+  SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_MFMA --output-format csv -d $out/pmc_c2 -o c2 -- \
+  python3 bench.py --config c2 $bargs > $out/pmc_c2.log 2>&1 || { echo "pmc c2 failed"; exit 1; }
 # where a fresh context's first pass spends its time (HIP API + kernel trace)
 timeout -k 10 200 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $out/trace_first -o first -- \
   python3 tools/first_pass.py random 0.05 > $out/trace_first.log 2>&1 || { echo "trace failed"; exit 1; }
