@@ -497,27 +497,35 @@ void rows_to_linear(uint32_t n, uint32_t rb, uint32_t re, uint32_t &lb, uint32_t
 // L2 instead of 1.11 GB with kS = 8, step -0.5% (archive/profiles_r01_r03/r03ar, r03as,
 // r03au).  Otherwise kS = 8, two whole super-blocks resident (C5, 323 KB
 // columns: 3% faster than 16).
+// The super-blocks in row-major block order, tiles inside a block ascending:
+// a counting sort by block over the (ta, tb)-sorted list, O(n) (a comparison
+// sort on the block key took ~3 ms per call on the GPU box's host at C4, twice
+// per first pass of a context: profiles/r05o/trace_first).
 std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t, uint32_t kS) {
     constexpr uint32_t kX = 8;
-    std::vector<std::vector<uint32_t>> blocks;
-    uint64_t last = ~0ull;
     std::vector<uint32_t> sorted(t);
-    auto block_of = [kS](uint32_t v) { return ((v >> 16) / kS) << 16 | ((v & 0xFFFFu) / kS); };
-    std::sort(sorted.begin(), sorted.end(), [&](uint32_t x, uint32_t y) {
-        const uint32_t bx = block_of(x), by = block_of(y);
-        return bx != by ? bx < by : x < y;
-    });
+    if (!std::is_sorted(sorted.begin(), sorted.end())) std::sort(sorted.begin(), sorted.end());
+    uint32_t nbr = 0, nbc = 0;
     for (uint32_t v : sorted) {
-        const uint64_t key = block_of(v);
-        if (key != last) blocks.emplace_back(), last = key;
-        blocks.back().push_back(v);
+        nbr = std::max(nbr, (v >> 16) / kS + 1);
+        nbc = std::max(nbc, (v & 0xFFFFu) / kS + 1);
+    }
+    auto block_of = [&](uint32_t v) { return (size_t)((v >> 16) / kS) * nbc + (v & 0xFFFFu) / kS; };
+    std::vector<uint32_t> start((size_t)nbr * nbc + 1, 0);
+    for (uint32_t v : sorted) ++start[block_of(v) + 1];
+    for (size_t b = 1; b < start.size(); ++b) start[b] += start[b - 1];
+    std::vector<uint32_t> by_block(sorted.size());
+    {
+        std::vector<uint32_t> at(start.begin(), start.end() - 1);
+        for (uint32_t v : sorted) by_block[at[block_of(v)]++] = v;  // stable: ascending inside a block
     }
     std::vector<std::vector<uint32_t>> q(kX);
-    for (auto &b : blocks) {
+    for (size_t b = 0; b + 1 < start.size(); ++b) {
+        if (start[b] == start[b + 1]) continue;
         size_t x = 0;
         for (size_t k = 1; k < kX; ++k)
             if (q[k].size() < q[x].size()) x = k;
-        q[x].insert(q[x].end(), b.begin(), b.end());
+        q[x].insert(q[x].end(), by_block.begin() + start[b], by_block.begin() + start[b + 1]);
     }
     // Even out the queues to within one tile: the kernel runs in rounds of
     // (resident workgroups per XCD) and a queue a few tiles longer than the
