@@ -587,6 +587,9 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
 #ifndef WLD_REF_ITEML_WG
 #define WLD_REF_ITEML_WG 4  // ... the candidate loop (its loop state: <= 128 VGPRs)
 #endif
+#ifndef WLD_ITEM_DIAG
+#define WLD_ITEM_DIAG 0  // diagnostic builds only (tools/build_variant.sh): 1 no compaction, 2 no epilogue
+#endif
 template <bool LOOP>
 __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) void ref_item_kernel(
     const uint8_t *__restrict__ rcodes, const float *__restrict__ rw, const uint8_t *__restrict__ site_ok,
@@ -723,6 +726,20 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
             }
         }
         // ---- epilogue (lib.rs:482-520, 660) --------------------------------
+#if WLD_ITEM_DIAG & 2  // diagnostic build (timing only): the sums, no epilogue, nothing stored
+        {
+            float keep = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) keep += tot[e][q];
+            asm volatile("" ::"v"(keep), "v"(okA4), "v"(okB));
+            if (tid < kTile && ((owned >> (tid >> 4)) & 1u)) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
+            __syncthreads();
+            if (tid == 0) tile_done(o, ta, tb, n_chunk_rows, (uint32_t)__popc(owned));
+            return;
+        }
+#endif
         uint32_t passmask = 0;  // bit e
         float res[4][3];
 #pragma unroll
@@ -738,6 +755,15 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
         // ---- compaction: the tile's 64x64 pass bits, rows in b order ---------
         const bool own_row = tid < kTile && ((owned >> (tid >> 4)) & 1u);
         const uint32_t quarters = (uint32_t)__popc(owned);
+#if WLD_ITEM_DIAG & 1  // diagnostic build (timing only): the epilogue, no compaction, nothing stored
+        {
+            float keep = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) keep += res[e][0] + res[e][1] + res[e][2];
+            asm volatile("" ::"v"(passmask), "v"(keep));
+            passmask = 0;
+        }
+#endif
         if (!__syncthreads_or(passmask != 0)) {
             if (own_row) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
             if (tid == 0) tile_done(o, ta, tb, n_chunk_rows, quarters);
