@@ -227,6 +227,12 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *                      in the candidate launch's last workgroup (ranges up to
  *                      4096 chunks); 0: as a launch of its own (the kernel
  *                      boundary orders it).  Same rows.
+ *   WLD_OPT_TEST_GUARD 0 (default); 1 (tests only): before each candidate
+ *                      launch the last candidate bucket's count is set one
+ *                      past its capacity, so the launch meets an entry outside
+ *                      the buckets.  Its guard refuses the entry and the run
+ *                      fails with WLD_E_STATE instead of reading through it;
+ *                      the next run (option back at 0) starts clean.
  *                      (Ids 9 and 10, an experimental 64x128-tile screen and an fp4
  *                      screen of round 2, are retired: WLD_E_ARG.) */
 #define WLD_OPT_PREFILTER 1
@@ -240,6 +246,7 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
 #define WLD_OPT_REF_SUMS 11
 #define WLD_OPT_FUSED_SCAN 12
 #define WLD_OPT_SCREEN_FP6 13
+#define WLD_OPT_TEST_GUARD 14
 int wld_set_option(wld_ctx *ctx, int option, int64_t value);
 int wld_get_option(wld_ctx *ctx, int option, int64_t *value);
 

@@ -467,3 +467,33 @@ def test_weights_at_mfma_range_boundary(W, N, spread, planes):
         w[small] = np.float32(spread * (1 - 2.0 ** -12))
         ctx.load(buf, w)
         assert ctx.stats()["kernel"] == W.KERNEL_VALU
+
+
+@pytest.mark.parametrize("opts", [{}, {"screen_fp6": 0}, {"screen_fp6": 2}, {"ref_sums": 0}],
+                         ids=["auto", "i8", "fp6", "exact_sums"])
+def test_guard_refuses_corrupt_candidate_entry(W, opts):
+    """a candidate entry outside the screen's buckets is refused by
+    the candidate launch's guard (cand_entry_checked) and the run fails with
+    WLD_E_STATE instead of reading through it (WLD_OPT_TEST_GUARD corrupts the
+    last bucket's count between the screen and the candidate launch); the
+    next run is clean and its rows equal the oracle's."""
+    L, N, thr = 900, 300, 0.2
+    buf = synth(L, N, 11)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    ref = O.all_pairs(buf, w, np.float32(thr))
+    c = W.Context(0, W.KERNEL_MFMA)
+    for k, v in opts.items():
+        c.set_option(k, v)
+    c.load(buf, w)
+    c.run(thr)
+    compare_rows(c.rows(), ref, thr, buf=buf, w=w)
+    assert c.stats()["screened"] == 1
+    c.set_option("test_guard", 1)
+    with pytest.raises(W.WldError) as e:
+        c.run(thr)
+    assert e.value.name == "WLD_E_STATE", e.value
+    assert "out-of-range" in str(e.value), e.value
+    c.set_option("test_guard", 0)
+    c.run(thr)
+    compare_rows(c.rows(), ref, thr, buf=buf, w=w)
+    c.close()

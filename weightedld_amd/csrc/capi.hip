@@ -127,6 +127,7 @@ struct wld_ctx {
     bool ref_pairs_pass = false;  // the pass staged exact candidate pairs (ref_rows_kernel)
     bool opt_site_major = false, opt_valu_plain = false;
     bool opt_fused_scan = true;  // WLD_OPT_FUSED_SCAN: the chunk scan in the candidate launch's last workgroup
+    int opt_test_guard = 0;      // WLD_OPT_TEST_GUARD (tests: a bucket count corrupted before the candidate launch)
     int opt_fp6 = 1;             // WLD_OPT_SCREEN_FP6: 0 off, 1 auto, 2 whenever it applies, 3 auto without the sample run
     bool opt_ref_sums = true;  // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order (default)
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
@@ -739,6 +740,7 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         m.cand_count = reinterpret_cast<unsigned *>(set);
         m.cand_work = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 2) + 1;  // beside the ticket
         m.cand_buckets = reinterpret_cast<unsigned *>(set + 1);
+        m.test_guard = c->opt_test_guard;
         if (scan && !dense) m.scan = *scan;
         RefRowsLaunch rr{};
         if (ref_screen) {
@@ -890,6 +892,7 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
             c->opt_host_batch_pairs = (uint64_t)value;
             break;
         case WLD_OPT_FUSED_SCAN: c->opt_fused_scan = value != 0; break;
+        case WLD_OPT_TEST_GUARD: c->opt_test_guard = value != 0; break;
         case WLD_OPT_SCREEN_FP6:
             if (value < 0 || value > 3) return fail(WLD_E_ARG, "WLD_OPT_SCREEN_FP6 takes 0 to 3");
             c->opt_fp6 = (int)value;
@@ -914,6 +917,7 @@ int wld_get_option(wld_ctx *c, int option, int64_t *value) {
         case WLD_OPT_STAGING_ROWS: *value = (int64_t)c->opt_staging_rows; break;
         case WLD_OPT_HOST_BATCH_PAIRS: *value = (int64_t)c->opt_host_batch_pairs; break;
         case WLD_OPT_FUSED_SCAN: *value = c->opt_fused_scan; break;
+        case WLD_OPT_TEST_GUARD: *value = c->opt_test_guard; break;
         case WLD_OPT_SCREEN_FP6: *value = c->opt_fp6; break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }

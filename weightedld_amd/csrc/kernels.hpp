@@ -245,6 +245,7 @@ struct MfmaLaunch {
     uint32_t *cand_list;   // 32 n_tiles entries: 16 buckets of tiles, then 16 of their sub-block bits
     unsigned *cand_count;  // 0 before the launch (chunk_scan_kernel resets it)
     unsigned *cand_buckets;  // 16 bucket counts, 0 before the launch (chunk_scan_kernel resets them)
+    int test_guard = 0;      // WLD_OPT_TEST_GUARD (launch_candidates)
     unsigned *cand_work;   // the candidate launch's work counter (the screen zeroes it)
     // WLD_OPT_REF_SUMS: the candidate tiles go to the reference-order f32
     // kernel (ref_valu, tiles/tile_count filled in here) and the screen's

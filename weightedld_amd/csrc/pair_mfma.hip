@@ -1425,6 +1425,18 @@ void launch_lds_planes(uint32_t n_planes, const MfmaLaunch &m, const uint64_t *o
 // prefilter, or (WLD_OPT_REF_SUMS) the reference-order f32 kernel.
 void launch_candidates(const MfmaLaunch &m, uint32_t n, uint32_t idx, const uint64_t *ok_bits, const OrderArgs &o,
                        const DenseArgs &dn, const ScreenArgs &sc, hipStream_t s) {
+    // WLD_OPT_TEST_GUARD: the last bucket's count one past its capacity, so
+    // the launch meets an entry outside the buckets (its guard must refuse
+    // it); the bucket's slots zeroed first, so the entries below the capacity
+    // are tile 0 with no sub-block (refused too) rather than stale data.  The
+    // list holds 16 n_tiles entries: buckets 0-15 of n_tiles, or with
+    // 16-row items buckets 0-3 of 4 n_tiles
+    if (m.test_guard && sc.cand_buckets && m.cand_list && sc.cand_bits && sc.cand_cap) {
+        const size_t cap = sc.cand_cap, last = 16 * (size_t)m.n_tiles / cap - 1;
+        (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(m.cand_list + last * cap), 0, cap, s);
+        (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(sc.cand_bits + last * cap), 0, cap, s);
+        (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(sc.cand_buckets + last), (int)(cap + 1), 1, s);
+    }
     if (m.ref_valu) {
         ValuLaunch v = *m.ref_valu;
         v.tiles = m.cand_list;
