@@ -37,7 +37,10 @@ def child(path, config, reps, thr, unweighted=False):
         k, v = kv.split("=", 1)
         ctx.set_option(k, int(v))
     ctx.load(buf, w)
-    ctx.run(thr)
+    shard = int(os.environ.get("WLD_AB_SHARD", "1"))  # rank 0's 1/K shard of the chunk sequence
+    lb, le = W.Context.shard_chunks(Ls, shard, 0) if shard > 1 else (0, 0)
+    run = (lambda t: ctx.run_chunks(t, lb, le)) if shard > 1 else ctx.run
+    run(thr)
     import ctypes
     lib = W.lib()
     st = None
@@ -46,7 +49,7 @@ def child(path, config, reps, thr, unweighted=False):
         lib.wld_debug_stamps(st, 1)
     t, rows, ts = [], 0, []
     for _ in range(reps):
-        rows = ctx.run(thr)
+        rows = run(thr)
         sx = ctx.stats()
         t.append(sx["pair_kernel_ms"])
         ts.append(sx.get("screen_ms", 0.0))
