@@ -590,6 +590,17 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
 #ifndef WLD_ITEM_DIAG
 #define WLD_ITEM_DIAG 0  // diagnostic builds only (tools/build_variant.sh): 1 no compaction, 2 no epilogue
 #endif
+// WLD_ITEM_TRACE (diagnostic builds only): the full-run item kernel records,
+// per wave, {HW_ID | XCC_ID << 32, start, sums done, end} (wall_clock64, 100
+// MHz) of its last launch; wld_diag_item_trace copies them out
+// (tools/item_trace.py)
+#ifndef WLD_ITEM_TRACE
+#define WLD_ITEM_TRACE 0
+#endif
+#if WLD_ITEM_TRACE
+constexpr uint32_t kTraceWaves = 65536;
+__device__ unsigned long long g_item_trace[kTraceWaves * 4];
+#endif
 template <bool LOOP>
 __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) void ref_item_kernel(
     const uint8_t *__restrict__ rcodes, const float *__restrict__ rw, const uint8_t *__restrict__ site_ok,
@@ -601,6 +612,10 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
     const uint32_t tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
+#if WLD_ITEM_TRACE
+    const unsigned long long t_start = wall_clock64();
+    unsigned long long t_sums = 0;
+#endif
     auto compute_item = [&](uint32_t tile, uint32_t bits, uint32_t owned) {
         const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
         const uint32_t a0 = ta * kTile, b0 = tb * kTile;
@@ -726,6 +741,9 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
             }
         }
         // ---- epilogue (lib.rs:482-520, 660) --------------------------------
+#if WLD_ITEM_TRACE
+        t_sums = wall_clock64();
+#endif
 #if WLD_ITEM_DIAG & 2  // diagnostic build (timing only): the sums, no epilogue, nothing stored
         {
             float keep = 0.0f;
@@ -816,6 +834,18 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
         const uint32_t cols = (tile >> 16) == (tile & 0xFFFFu) ? 0xFu & ~((1u << q) - 1u) : 0xFu;
         if (tile != kNoTile) compute_item(tile, cols << (4 * q), 1u << q);  // kNoTile: padding of an XCD-ordered list
         scan_tail(sa, gridDim.x);  // (every workgroup takes a ticket when the scan is fused)
+#if WLD_ITEM_TRACE
+        const size_t wi = (size_t)blockIdx.x * 4 + wave;
+        if (lane == 0 && wi < kTraceWaves) {
+            unsigned hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            g_item_trace[4 * wi] = hw | (unsigned long long)xcc << 32;
+            g_item_trace[4 * wi + 1] = t_start;
+            g_item_trace[4 * wi + 2] = t_sums;
+            g_item_trace[4 * wi + 3] = wall_clock64();
+        }
+#endif
     } else {
         // the screen's items, heaviest bucket first; the first by workgroup id
         // (rounds dealt in snake order, heavy beside light on a CU), the next
@@ -1117,3 +1147,15 @@ bool launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
 }
 
 }  // namespace wld
+
+#if WLD_ITEM_TRACE
+extern "C" int wld_diag_item_trace(unsigned long long *out, size_t n_words, int reset) {
+    if (reset) {
+        void *p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(wld::g_item_trace)) != hipSuccess) return -1;
+        return hipMemset(p, 0, sizeof(wld::g_item_trace)) == hipSuccess ? 0 : -1;
+    }
+    n_words = n_words < sizeof(wld::g_item_trace) / 8 ? n_words : sizeof(wld::g_item_trace) / 8;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(wld::g_item_trace), n_words * 8) == hipSuccess ? 0 : -1;
+}
+#endif
