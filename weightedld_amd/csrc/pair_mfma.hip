@@ -1144,13 +1144,19 @@ constexpr uint32_t kF6Single = 0x8000u;
 // s_waitcnt immediate (gfx9 encoding): lgkmcnt(0), vmcnt and expcnt at their maxima
 [[maybe_unused]] constexpr int kWaitLgkm0 = 0xC07F;
 constexpr int kF6PStage = kF6AStage + 2 * kF6BStage;
+// stage buffers of the tile-pair kernel: 2 (default: one stage in flight while
+// one is computed) or 3 (WLD_F6_RING 3: two stages in flight, counted vmcnt;
+// 120 KB of LDS for the CU's two workgroups)
+#ifndef WLD_F6_RING
+#define WLD_F6_RING 2
+#endif
 __global__ __launch_bounds__(512, 4) void pair_fp6_screen2_kernel(const uint8_t *__restrict__ a6,
                                                           const uint8_t *__restrict__ b6,
                                                           const uint64_t *__restrict__ ok_bits,
                                                           const uint32_t *__restrict__ pairs, uint32_t n_pairs,
                                                           uint32_t NK, uint32_t L, uint32_t n_chunk_rows, float thr,
                                                           OrderArgs o, ScreenArgs sc) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6PStage];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[WLD_F6_RING * kF6PStage];
     __shared__ unsigned long long sMask[2];
     __shared__ uint32_t sBail, sCand[2];
     if (!sc.probe && blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
@@ -1248,6 +1254,40 @@ __global__ __launch_bounds__(512, 4) void pair_fp6_screen2_kernel(const uint8_t 
     for (uint32_t kb = 0; kb < NK; kb += 2) {
         stage(kb, r0, r1);
         if (kb + 1 < NK) stage(kb + 1, r1, r0);
+    }
+#elif WLD_F6_RING == 3
+    // three buffers, stages kb + 1 and kb + 2 in flight while kb is computed:
+    // at stage kb's top this wave's copies of kb have landed once no more than
+    // its copies of kb + 1 are outstanding (pieces p = wave, wave + 8, wave +
+    // 16 of 20: three for waves 0-3, two for 4-7)
+    if (NK > 1) issue(1, 1);
+    uint32_t buf = 0;
+    for (uint32_t kb = 0; kb < NK; ++kb) {
+        if (kb + 1 < NK) {
+            if (wave < 4)
+                asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();  // every wave's copies of stage kb landed; stage kb - 1's buffer is free
+        asm volatile("" ::: "memory");
+        if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
+            if (tid == 0 && sBail == 1) {
+                atomicOr(sc.cand_count, kAbandonBit);
+                atomicOr(sc.cand_buckets, kAbandonBit);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            return;
+        }
+        if (kb + 2 < NK) issue(kb + 2, buf == 0 ? 2u : buf - 1u);
+        const uint8_t *g = smem + buf * kF6PStage;
+        const v8i ai = f6_ld24(g + wq * kF6ABytes, lane), am = f6_ld24(g + wq * kF6ABytes + 1536, lane);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) f6_block_mfma(acc[n], ai, am, f6_ldb(g + boff + n * kF6BBytes, lane));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
+        buf = buf == 2 ? 0u : buf + 1u;
     }
 #else
     uint32_t buf = 0;
