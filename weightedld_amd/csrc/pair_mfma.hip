@@ -1476,6 +1476,10 @@ void launch_candidates(const MfmaLaunch &m, uint32_t n, uint32_t idx, const uint
         (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(m.cand_list + last * cap), 0, cap, s);
         (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(sc.cand_bits + last * cap), 0, cap, s);
         (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(sc.cand_buckets + last), (int)(cap + 1), 1, s);
+        // ... and the tile count (the exact mode's candidate loop runs to it)
+        // past every bucket: its last entry lies beyond their total
+        if (m.cand_count)
+            (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(m.cand_count), (int)(16 * m.n_tiles + 2), 1, s);
     }
     if (m.ref_valu) {
         ValuLaunch v = *m.ref_valu;
