@@ -685,9 +685,12 @@ def main():
         dom_ms = screen_ms if screened else kernel_ms
         achieved = alg_ops / (dom_ms * 1e-3) / 1e12
         if fp6:
-            # tile pairs (two tiles sharing one A image per workgroup) unless the
-            # tile list outgrows the pair list's 15-bit tile index
-            kname = ("pair_fp6_screen2_kernel<tile pairs, fp6 x fp4 16x16x128>" if (L + 63) // 64 <= 0x7FFF
+            # tile pairs (two tiles sharing one A image per workgroup) from
+            # WLD_OPT_FP6_PAIRS_MIN_TILES tiles (default 32768) while the pair
+            # list's 15-bit tile index holds the sites
+            pairs_min = ctx.get_option("fp6_pairs_min_tiles")
+            kname = ("pair_fp6_screen2_kernel<tile pairs, fp6 x fp4 16x16x128>"
+                     if (L + 63) // 64 <= 0x7FFF and n_tiles >= pairs_min
                      else "pair_fp6_screen_kernel<fp6 x fp4 16x16x128>")
         elif screen_kind == 4:
             kname = "pair_mfma_kernel<candidate pairs, %d planes>" % min(planes, 2)

@@ -227,6 +227,10 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *                      in the candidate launch's last workgroup (ranges up to
  *                      4096 chunks); 0: as a launch of its own (the kernel
  *                      boundary orders it).  Same rows.
+ *   WLD_OPT_FP6_PAIRS_MIN_TILES  the fp6 screen computes two tiles of a row
+ *                      per workgroup (one shared A operand stream) when the
+ *                      run's tile list has at least this many tiles (default
+ *                      32768), else one tile per workgroup.  Same rows.
  *   WLD_OPT_TEST_GUARD 0 (default); 1 (tests only): before each candidate
  *                      launch the last candidate bucket's count is set one
  *                      past its capacity, so the launch meets an entry outside
@@ -247,6 +251,7 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
 #define WLD_OPT_FUSED_SCAN 12
 #define WLD_OPT_SCREEN_FP6 13
 #define WLD_OPT_TEST_GUARD 14
+#define WLD_OPT_FP6_PAIRS_MIN_TILES 15
 int wld_set_option(wld_ctx *ctx, int option, int64_t value);
 int wld_get_option(wld_ctx *ctx, int option, int64_t *value);
 

@@ -128,6 +128,11 @@ struct wld_ctx {
     bool opt_site_major = false, opt_valu_plain = false;
     bool opt_fused_scan = true;  // WLD_OPT_FUSED_SCAN: the chunk scan in the candidate launch's last workgroup
     int opt_test_guard = 0;      // WLD_OPT_TEST_GUARD (tests: a bucket count corrupted before the candidate launch)
+    // WLD_OPT_FP6_PAIRS_MIN_TILES: the fp6 screen runs on tile pairs from this
+    // many tiles in the run's list (below it, one tile per workgroup: rank 0's
+    // 1/8 shard of C4, 6,128 tiles, screens 7% faster on single tiles,
+    // profiles/r05q/ab_shard8.log; C5 4.8% slower, profiles/r05j/)
+    int64_t opt_fp6_pairs_min = 32768;
     int opt_fp6 = 1;             // WLD_OPT_SCREEN_FP6: 0 off, 1 auto, 2 whenever it applies, 3 auto without the sample run
     bool opt_ref_sums = true;  // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order (default)
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
@@ -570,7 +575,7 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
     // the fp6 screen's tile pairs (ordered as the tiles below, by first tile;
     // single tiles keep their flag through the ordering)
     std::vector<uint32_t> pl;
-    if (fp6_uses_pairs() && T_used <= 0x7FFF) {
+    if (fp6_uses_pairs() && T_used <= 0x7FFF && (int64_t)t.size() >= c->opt_fp6_pairs_min) {
         pl = fp6_pair_list(t);
         if (!c->opt_tile_rows && pl.size() >= 2048) {
             std::vector<uint32_t> plain(pl.size()), single;
@@ -893,6 +898,11 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
             break;
         case WLD_OPT_FUSED_SCAN: c->opt_fused_scan = value != 0; break;
         case WLD_OPT_TEST_GUARD: c->opt_test_guard = value != 0; break;
+        case WLD_OPT_FP6_PAIRS_MIN_TILES:
+            if (value < 0) return fail(WLD_E_ARG, "WLD_OPT_FP6_PAIRS_MIN_TILES must be >= 0");
+            c->opt_fp6_pairs_min = value;
+            c->tiles_lb = c->tiles_le = ~0u;  // rebuild the lists at the next run
+            break;
         case WLD_OPT_SCREEN_FP6:
             if (value < 0 || value > 3) return fail(WLD_E_ARG, "WLD_OPT_SCREEN_FP6 takes 0 to 3");
             c->opt_fp6 = (int)value;
@@ -918,6 +928,7 @@ int wld_get_option(wld_ctx *c, int option, int64_t *value) {
         case WLD_OPT_HOST_BATCH_PAIRS: *value = (int64_t)c->opt_host_batch_pairs; break;
         case WLD_OPT_FUSED_SCAN: *value = c->opt_fused_scan; break;
         case WLD_OPT_TEST_GUARD: *value = c->opt_test_guard; break;
+        case WLD_OPT_FP6_PAIRS_MIN_TILES: *value = c->opt_fp6_pairs_min; break;
         case WLD_OPT_SCREEN_FP6: *value = c->opt_fp6; break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }

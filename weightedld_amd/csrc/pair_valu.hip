@@ -597,6 +597,9 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
 #ifndef WLD_ITEM_TRACE
 #define WLD_ITEM_TRACE 0
 #endif
+#ifndef WLD_ITEM_PRE
+#define WLD_ITEM_PRE 0
+#endif
 #if WLD_ITEM_TRACE
 constexpr uint32_t kTraceWaves = 65536;
 __device__ unsigned long long g_item_trace[kTraceWaves * 4];
@@ -679,6 +682,36 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
 #pragma unroll
                 for (int grp = 0; grp < 4; ++grp) A[grp] = ca[grp], B[grp] = cb[grp], Wt[grp] = cw[grp];
                 if (st + 1 < n_st) fetch(64 * (st + 1));  // (classes are consecutive: stage st at 64 st)
+#if WLD_ITEM_PRE
+                // (variant) every operand of a 16-position group formed before its 16
+                // MFMAs: no operand register is rewritten while an MFMA that reads
+                // it may still wait for the matrix pipe
+#pragma unroll
+                for (int grp = 0; grp < 4; ++grp) {
+                    const float we[4] = {Wt[grp].x, Wt[grp].y, Wt[grp].z, Wt[grp].w};
+                    const uint32_t ai = A[grp] & 0x01010101u, am = (A[grp] >> 1) & 0x01010101u;
+                    const uint32_t bi = B[grp] & 0x01010101u, bm = (B[grp] >> 1) & 0x01010101u;
+                    float u[4], v[4], fi[4], fm[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        u[e] = we[e] * cvt_ubyte<0>(ai, e);
+                        v[e] = we[e] * cvt_ubyte<0>(am, e);
+                        fi[e] = cvt_ubyte<1>(bi, e);
+                        fm[e] = cvt_ubyte<1>(bm, e);
+                    }
+                    // (all 16 live here: the compiler may not sink them between the MFMAs)
+                    asm volatile("" : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(v[0]), "+v"(v[1]),
+                                 "+v"(v[2]), "+v"(v[3]), "+v"(fi[0]), "+v"(fi[1]), "+v"(fi[2]), "+v"(fi[3]),
+                                 "+v"(fm[0]), "+v"(fm[1]), "+v"(fm[2]), "+v"(fm[3]));
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[e], fi[e], acc[0], 0, 0, 0);
+                        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[e], fi[e], acc[1], 0, 0, 0);
+                        acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[e], fm[e], acc[2], 0, 0, 0);
+                        acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[e], fm[e], acc[3], 0, 0, 0);
+                    }
+                }
+#else
 #pragma unroll
                 for (int grp = 0; grp < 4; ++grp) {
                     const float we[4] = {Wt[grp].x, Wt[grp].y, Wt[grp].z, Wt[grp].w};
@@ -698,6 +731,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                         acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fm, acc[3], 0, 0, 0);
                     }
                 }
+#endif
                 // end of a class: its chain joins the ordered horizontal sum
                 if (++in_cls == ref_cs) {
                     in_cls = 0;
