@@ -8,7 +8,9 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libweightedld.so")
+# WLD_LIB_PATH: an experimental build of the same library (tools/build_variant.sh)
+# for the GPU tests of a variant; default the in-tree build
+LIB_PATH = os.environ.get("WLD_LIB_PATH") or os.path.join(PKG_DIR, "libweightedld.so")
 
 WLD_OK = 0
 STATUS = {

@@ -597,8 +597,11 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
 #ifndef WLD_ITEM_TRACE
 #define WLD_ITEM_TRACE 0
 #endif
-#ifndef WLD_ITEM_PRE
-#define WLD_ITEM_PRE 0
+// WLD_ITEM_CPAIR 1 (variant): the lane classes two at a time, each with its
+// own accumulators (8 independent f32 chains per wave instead of 4; the same
+// sums: each class's chain from 0, joined to the horizontal sum in class order)
+#ifndef WLD_ITEM_CPAIR
+#define WLD_ITEM_CPAIR 0
 #endif
 #if WLD_ITEM_TRACE
 constexpr uint32_t kTraceWaves = 65536;
@@ -670,6 +673,63 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                 cw[2].x = __uint_as_float(b8.x);
                 cw[2].y = __uint_as_float(b8.y);
             };
+#if WLD_ITEM_CPAIR
+            // classes j and j + 1 side by side, stage s of each (stages of class j
+            // at j ref_cs ..); codes and weights of both loaded at the pair's
+            // stage top (no prefetch: the co-resident waves cover the latency)
+            for (uint32_t j = 0; j < 8; j += 2) {
+                v4f acc0[4], acc1[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc0[q] = acc1[q] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+                for (uint32_t sidx = 0; sidx < ref_cs; ++sidx) {
+                    const uint32_t k0 = 64 * (j * ref_cs + sidx), k1 = k0 + 64 * ref_cs;
+                    uint32_t A0[4], B0[4], A1[4], B1[4];
+                    float4 W0[4], W1[4];
+#pragma unroll
+                    for (int grp = 0; grp < 4; ++grp) {
+                        A0[grp] = *reinterpret_cast<const uint32_t *>(rowA + k0 + 16 * grp);
+                        B0[grp] = *reinterpret_cast<const uint32_t *>(rowB + k0 + 16 * grp);
+                        W0[grp] = *reinterpret_cast<const float4 *>(wg + k0 + 16 * grp);
+                        A1[grp] = *reinterpret_cast<const uint32_t *>(rowA + k1 + 16 * grp);
+                        B1[grp] = *reinterpret_cast<const uint32_t *>(rowB + k1 + 16 * grp);
+                        W1[grp] = *reinterpret_cast<const float4 *>(wg + k1 + 16 * grp);
+                    }
+#pragma unroll
+                    for (int grp = 0; grp < 4; ++grp) {
+                        const float we0[4] = {W0[grp].x, W0[grp].y, W0[grp].z, W0[grp].w};
+                        const float we1[4] = {W1[grp].x, W1[grp].y, W1[grp].z, W1[grp].w};
+                        const uint32_t ai0 = A0[grp] & 0x01010101u, am0 = (A0[grp] >> 1) & 0x01010101u;
+                        const uint32_t bi0 = B0[grp] & 0x01010101u, bm0 = (B0[grp] >> 1) & 0x01010101u;
+                        const uint32_t ai1 = A1[grp] & 0x01010101u, am1 = (A1[grp] >> 1) & 0x01010101u;
+                        const uint32_t bi1 = B1[grp] & 0x01010101u, bm1 = (B1[grp] >> 1) & 0x01010101u;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float u0 = we0[e] * cvt_ubyte<0>(ai0, e), v0 = we0[e] * cvt_ubyte<0>(am0, e);
+                            const float fi0 = cvt_ubyte<1>(bi0, e), fm0 = cvt_ubyte<1>(bm0, e);
+                            const float u1 = we1[e] * cvt_ubyte<0>(ai1, e), v1 = we1[e] * cvt_ubyte<0>(am1, e);
+                            const float fi1 = cvt_ubyte<1>(bi1, e), fm1 = cvt_ubyte<1>(bm1, e);
+                            acc0[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u0, fi0, acc0[0], 0, 0, 0);
+                            acc1[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u1, fi1, acc1[0], 0, 0, 0);
+                            acc0[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0, fi0, acc0[1], 0, 0, 0);
+                            acc1[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1, fi1, acc1[1], 0, 0, 0);
+                            acc0[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u0, fm0, acc0[2], 0, 0, 0);
+                            acc1[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u1, fm1, acc1[2], 0, 0, 0);
+                            acc0[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0, fm0, acc0[3], 0, 0, 0);
+                            acc1[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1, fm1, acc1[3], 0, 0, 0);
+                        }
+                    }
+                }
+                // class j's chain, then class j + 1's, onto the ordered horizontal sum
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) tot[e][q] += acc0[q][e];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) tot[e][q] += acc1[q][e];
+            }
+#else
             if (n_st) fetch(0);
             v4f acc[4];
             uint32_t in_cls = 0;  // this stage's index in its class (no modulo in the loop)
@@ -682,36 +742,6 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
 #pragma unroll
                 for (int grp = 0; grp < 4; ++grp) A[grp] = ca[grp], B[grp] = cb[grp], Wt[grp] = cw[grp];
                 if (st + 1 < n_st) fetch(64 * (st + 1));  // (classes are consecutive: stage st at 64 st)
-#if WLD_ITEM_PRE
-                // (variant) every operand of a 16-position group formed before its 16
-                // MFMAs: no operand register is rewritten while an MFMA that reads
-                // it may still wait for the matrix pipe
-#pragma unroll
-                for (int grp = 0; grp < 4; ++grp) {
-                    const float we[4] = {Wt[grp].x, Wt[grp].y, Wt[grp].z, Wt[grp].w};
-                    const uint32_t ai = A[grp] & 0x01010101u, am = (A[grp] >> 1) & 0x01010101u;
-                    const uint32_t bi = B[grp] & 0x01010101u, bm = (B[grp] >> 1) & 0x01010101u;
-                    float u[4], v[4], fi[4], fm[4];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        u[e] = we[e] * cvt_ubyte<0>(ai, e);
-                        v[e] = we[e] * cvt_ubyte<0>(am, e);
-                        fi[e] = cvt_ubyte<1>(bi, e);
-                        fm[e] = cvt_ubyte<1>(bm, e);
-                    }
-                    // (all 16 live here: the compiler may not sink them between the MFMAs)
-                    asm volatile("" : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(v[0]), "+v"(v[1]),
-                                 "+v"(v[2]), "+v"(v[3]), "+v"(fi[0]), "+v"(fi[1]), "+v"(fi[2]), "+v"(fi[3]),
-                                 "+v"(fm[0]), "+v"(fm[1]), "+v"(fm[2]), "+v"(fm[3]));
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[e], fi[e], acc[0], 0, 0, 0);
-                        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[e], fi[e], acc[1], 0, 0, 0);
-                        acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[e], fm[e], acc[2], 0, 0, 0);
-                        acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[e], fm[e], acc[3], 0, 0, 0);
-                    }
-                }
-#else
 #pragma unroll
                 for (int grp = 0; grp < 4; ++grp) {
                     const float we[4] = {Wt[grp].x, Wt[grp].y, Wt[grp].z, Wt[grp].w};
@@ -731,7 +761,6 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                         acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fm, acc[3], 0, 0, 0);
                     }
                 }
-#endif
                 // end of a class: its chain joins the ordered horizontal sum
                 if (++in_cls == ref_cs) {
                     in_cls = 0;
@@ -741,6 +770,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                         for (int q = 0; q < 4; ++q) tot[e][q] += acc[q][e];
                 }
             }
+#endif
             // the scalar tail (lib.rs:461-480), onto the horizontal sums in order
             // (ref_tail_n <= 7, uniform)
             // (one position per step: the byte queues shift down by 8 bits, the
