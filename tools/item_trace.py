@@ -5,7 +5,7 @@ per wave {HW_ID | XCC_ID << 32, start, sums done, end} of the last launch, in
 wall_clock64 ticks (100 MHz = 10 ns).  Prints the launch span, the phases per
 wave (sums, epilogue + compaction + scan ticket), the start/end spread, how
 many workgroups each CU ran, and the busy fraction of each SIMD over the span.
-    python tools/item_trace.py LIB.so [config=c2] [reps=20]"""
+    python tools/item_trace.py LIB.so [config=c2] [reps=20] [RAW.npy]"""
 import ctypes
 import json
 import os
@@ -44,6 +44,8 @@ out = (ctypes.c_ulonglong * n_words)()
 assert lib.wld_diag_item_trace(out, n_words, 0) == 0
 a = np.frombuffer(out, dtype=np.uint64).reshape(-1, 4)
 a = a[a[:, 3] != 0]
+if len(sys.argv) > 4:  # the raw records, for offline analysis
+    np.save(sys.argv[4], a)
 hw, t0, t1, t2 = a[:, 0], a[:, 1].astype(np.int64), a[:, 2].astype(np.int64), a[:, 3].astype(np.int64)
 base = t0.min()
 t0, t1, t2 = t0 - base, t1 - base, t2 - base
