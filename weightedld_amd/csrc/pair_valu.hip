@@ -603,6 +603,9 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
 #ifndef WLD_ITEM_CPAIR
 #define WLD_ITEM_CPAIR 0
 #endif
+#ifndef WLD_ITEM_NOPF
+#define WLD_ITEM_NOPF 0
+#endif
 #if WLD_ITEM_TRACE
 constexpr uint32_t kTraceWaves = 65536;
 __device__ unsigned long long g_item_trace[kTraceWaves * 4];
@@ -730,7 +733,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                     for (int q = 0; q < 4; ++q) tot[e][q] += acc1[q][e];
             }
 #else
-            if (n_st) fetch(0);
+            if (n_st && !WLD_ITEM_NOPF) fetch(0);
             v4f acc[4];
             uint32_t in_cls = 0;  // this stage's index in its class (no modulo in the loop)
             for (uint32_t st = 0; st < n_st; ++st) {
@@ -739,9 +742,17 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                     for (int q = 0; q < 4; ++q) acc[q] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
                 uint32_t A[4], B[4];
                 float4 Wt[4];
+#if WLD_ITEM_NOPF
+                // (variant) no prefetch: this stage's operands loaded at its top; the
+                // registers this frees buy more co-resident waves to cover the latency
+                fetch(64 * st);
+#pragma unroll
+                for (int grp = 0; grp < 4; ++grp) A[grp] = ca[grp], B[grp] = cb[grp], Wt[grp] = cw[grp];
+#else
 #pragma unroll
                 for (int grp = 0; grp < 4; ++grp) A[grp] = ca[grp], B[grp] = cb[grp], Wt[grp] = cw[grp];
                 if (st + 1 < n_st) fetch(64 * (st + 1));  // (classes are consecutive: stage st at 64 st)
+#endif
 #pragma unroll
                 for (int grp = 0; grp < 4; ++grp) {
                     const float we[4] = {Wt[grp].x, Wt[grp].y, Wt[grp].z, Wt[grp].w};
