@@ -1150,7 +1150,12 @@ constexpr int kF6PStage = kF6AStage + 2 * kF6BStage;
 #ifndef WLD_F6_RING
 #define WLD_F6_RING 2
 #endif
-__global__ __launch_bounds__(512, 4) void pair_fp6_screen2_kernel(const uint8_t *__restrict__ a6,
+// waves per SIMD the tile-pair kernel is compiled for: 4 (default, two
+// workgroups per CU, <= 128 VGPRs) or 6 (three per CU, <= 85 VGPRs)
+#ifndef WLD_FP6_PAIR_WPS
+#define WLD_FP6_PAIR_WPS 4
+#endif
+__global__ __launch_bounds__(512, WLD_FP6_PAIR_WPS) void pair_fp6_screen2_kernel(const uint8_t *__restrict__ a6,
                                                           const uint8_t *__restrict__ b6,
                                                           const uint64_t *__restrict__ ok_bits,
                                                           const uint32_t *__restrict__ pairs, uint32_t n_pairs,
