@@ -582,7 +582,7 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
     return r;
 }
 #ifndef WLD_REF_ITEM_WG
-#define WLD_REF_ITEM_WG 5  // workgroups per CU, full runs (<= 102 VGPRs; two spill, outside the loop)
+#define WLD_REF_ITEM_WG 6  // workgroups per CU, full runs (<= 85 VGPRs: 70 without the prefetch)
 #endif
 #ifndef WLD_REF_ITEML_WG
 #define WLD_REF_ITEML_WG 4  // ... the candidate loop (its loop state: <= 128 VGPRs)
@@ -603,8 +603,13 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
 #ifndef WLD_ITEM_CPAIR
 #define WLD_ITEM_CPAIR 0
 #endif
+// Full runs (not LOOP) load each stage's operands at its top instead of one
+// stage ahead: 70 instead of 96 VGPRs, six workgroups per CU instead of five,
+// and the co-resident waves cover the latency (C2 -2.5%, profiles/r05v/; the
+// matrix pipe fills only with many waves in their sums).  The
+// candidate loop keeps the prefetch (four workgroups per CU either way).
 #ifndef WLD_ITEM_NOPF
-#define WLD_ITEM_NOPF 0
+#define WLD_ITEM_NOPF 1
 #endif
 #if WLD_ITEM_TRACE
 constexpr uint32_t kTraceWaves = 65536;
@@ -733,7 +738,8 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                     for (int q = 0; q < 4; ++q) tot[e][q] += acc1[q][e];
             }
 #else
-            if (n_st && !WLD_ITEM_NOPF) fetch(0);
+            constexpr bool kNoPrefetch = WLD_ITEM_NOPF && !LOOP;
+            if (n_st && !kNoPrefetch) fetch(0);
             v4f acc[4];
             uint32_t in_cls = 0;  // this stage's index in its class (no modulo in the loop)
             for (uint32_t st = 0; st < n_st; ++st) {
@@ -742,17 +748,10 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                     for (int q = 0; q < 4; ++q) acc[q] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
                 uint32_t A[4], B[4];
                 float4 Wt[4];
-#if WLD_ITEM_NOPF
-                // (variant) no prefetch: this stage's operands loaded at its top; the
-                // registers this frees buy more co-resident waves to cover the latency
-                fetch(64 * st);
+                if constexpr (kNoPrefetch) fetch(64 * st);  // this stage's operands, at its top
 #pragma unroll
                 for (int grp = 0; grp < 4; ++grp) A[grp] = ca[grp], B[grp] = cb[grp], Wt[grp] = cw[grp];
-#else
-#pragma unroll
-                for (int grp = 0; grp < 4; ++grp) A[grp] = ca[grp], B[grp] = cb[grp], Wt[grp] = cw[grp];
-                if (st + 1 < n_st) fetch(64 * (st + 1));  // (classes are consecutive: stage st at 64 st)
-#endif
+                if (!kNoPrefetch && st + 1 < n_st) fetch(64 * (st + 1));  // (classes are consecutive: stage st at 64 st)
 #pragma unroll
                 for (int grp = 0; grp < 4; ++grp) {
                     const float we[4] = {Wt[grp].x, Wt[grp].y, Wt[grp].z, Wt[grp].w};
