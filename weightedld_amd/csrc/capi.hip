@@ -129,11 +129,13 @@ struct wld_ctx {
     bool opt_fused_scan = true;  // WLD_OPT_FUSED_SCAN: the chunk scan in the candidate launch's last workgroup
     int opt_test_guard = 0;      // WLD_OPT_TEST_GUARD (tests: a bucket count corrupted before the candidate launch)
     // WLD_OPT_FP6_PAIRS_MIN_TILES: the fp6 screen runs on tile pairs from this
-    // many tiles in the run's list, below it one tile per workgroup (rank 0's
-    // shard of C4: 1/8, 6,128 tiles, single 7% faster; 1/4, 12,256 tiles,
-    // single 5% faster; 1/2, 24,572 tiles, pairs 3% faster; whole C4 even;
-    // C5 pairs 4.8% faster: profiles/r05q, r05s, r05j)
-    int64_t opt_fp6_pairs_min = 16384;
+    // many tiles in the run's list, below it one tile per workgroup.  Alone
+    // (one pass at a time) single tiles screen rank 0's 1/8 and 1/4 shards of
+    // C4 5-7% faster (profiles/r05q, r05s), but in the N>1 step path, where
+    // the passes of three contexts overlap, the 1/4 shard steps 6% faster on
+    // pairs and the 1/8 shard is even within noise (profiles/r05x); C5 pairs
+    // 4.8% faster (profiles/r05j)
+    int64_t opt_fp6_pairs_min = 8192;
     int opt_fp6 = 1;             // WLD_OPT_SCREEN_FP6: 0 off, 1 auto, 2 whenever it applies, 3 auto without the sample run
     bool opt_ref_sums = true;  // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order (default)
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
