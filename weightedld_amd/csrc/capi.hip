@@ -280,8 +280,8 @@ uint32_t fp6_code(double x, double *rounded) {
 // rounding, plus the fixed point's 0.5 per sequence (exact mode) and lib.rs's
 // f32 summation (9 gamma_m sum w, ref_extra_residual) — both added, so one
 // R serves either mode.
-// Built on the first run that may screen on fp6 (not at load: with
-// WLD_OPT_SCREEN_FP6 0 it never is).
+// Built at load unless WLD_OPT_SCREEN_FP6 is 0, else on the first run that
+// may screen on fp6 after the option is set.
 int fp6_prepare(wld_ctx *c) {
     c->fp6_ok = c->fp6_better = false;
     c->fp6_tried = true;
@@ -337,6 +337,10 @@ int fp6_prepare(wld_ctx *c) {
     c->fp6_better = c->fp6_rel <= std::max(2.0 * c->i8_rel, 0.02);
     return WLD_OK;
 }
+
+int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le);
+int ensure_ref_layout(wld_ctx *c);
+uint32_t chunks_of(size_t L);
 
 int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint64_t *site_map,
                 const uint32_t *d_site_index = nullptr) {
@@ -439,6 +443,15 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     c->loaded = true;
     c->have_rows = false;
     c->tiles_lb = c->tiles_le = ~0u;
+    // what a first run would otherwise build: the fp6 screen's operands (not
+    // with WLD_OPT_SCREEN_FP6 0), lib.rs's lane-class layout (WLD_OPT_REF_SUMS),
+    // the whole set's tile lists; a fresh context's first pass then costs
+    // about a steady one (a run over a shard builds its own
+    // lists on its first pass)
+    if (c->opt_fp6 != 0) WLD_TRY(fp6_prepare(c));
+    if (c->opt_ref_sums) WLD_TRY(ensure_ref_layout(c));
+    WLD_TRY(build_tiles(c, 0, chunks_of(L)));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return WLD_OK;
 }
 
@@ -510,16 +523,24 @@ void rows_to_linear(uint32_t n, uint32_t rb, uint32_t re, uint32_t &lb, uint32_t
 // a counting sort by block over the (ta, tb)-sorted list, O(n) (a comparison
 // sort on the block key took ~3 ms per call on the GPU box's host at C4, twice
 // per first pass of a context: profiles/r05o/trace_first).
-std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t, uint32_t kS) {
+// Entries may carry flag bits outside `key` (the tile-pair list's single
+// flag): they ride along, the order is the keyed tiles'.
+std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t, uint32_t kS, uint32_t key = ~0u) {
     constexpr uint32_t kX = 8;
     std::vector<uint32_t> sorted(t);
-    if (!std::is_sorted(sorted.begin(), sorted.end())) std::sort(sorted.begin(), sorted.end());
+    auto keyed_less = [key](uint32_t x, uint32_t y) { return (x & key) < (y & key); };
+    if (!std::is_sorted(sorted.begin(), sorted.end(), keyed_less))
+        std::sort(sorted.begin(), sorted.end(), keyed_less);
     uint32_t nbr = 0, nbc = 0;
     for (uint32_t v : sorted) {
+        v &= key;
         nbr = std::max(nbr, (v >> 16) / kS + 1);
         nbc = std::max(nbc, (v & 0xFFFFu) / kS + 1);
     }
-    auto block_of = [&](uint32_t v) { return (size_t)((v >> 16) / kS) * nbc + (v & 0xFFFFu) / kS; };
+    auto block_of = [&](uint32_t v) {
+        v &= key;
+        return (size_t)((v >> 16) / kS) * nbc + (v & 0xFFFFu) / kS;
+    };
     std::vector<uint32_t> start((size_t)nbr * nbc + 1, 0);
     for (uint32_t v : sorted) ++start[block_of(v) + 1];
     for (size_t b = 1; b < start.size(); ++b) start[b] += start[b - 1];
@@ -564,33 +585,26 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
     if (c->tiles_lb == lb && c->tiles_le == le && c->n_tiles) return WLD_OK;
     const uint32_t T_used = (uint32_t)((c->L + kTile - 1) / kTile);
     const uint32_t n = chunk_rows_of(c->L);
+    // in (ta, tb) order directly (no sort): row by row, the chunk columns of
+    // the range (a contiguous run of the linear chunk sequence)
     std::vector<uint32_t> t;
-    for (uint32_t i = lb; i < le; ++i) {
-        uint32_t row, col;
-        chunk_of_linear_host(n, i, row, col);
-        for (uint32_t ta = row * kTilesPerChunk; ta < std::min<uint32_t>((row + 1) * kTilesPerChunk, T_used); ++ta)
+    for (uint32_t ta = 0; ta < T_used; ++ta) {
+        const uint32_t row = ta / kTilesPerChunk;
+        for (uint32_t col = row; col < n; ++col) {
+            const uint32_t li = chunk_linear(n, row, col);
+            if (li < lb || li >= le) continue;
             for (uint32_t tb = std::max(ta, col * kTilesPerChunk);
                  tb < std::min<uint32_t>((col + 1) * kTilesPerChunk, T_used); ++tb)
                 t.push_back((ta << 16) | tb);
+        }
     }
-    std::sort(t.begin(), t.end());
     const uint32_t kS = 24ull * kTile * c->NP <= (4ull << 20) ? 16u : 8u;
     // the fp6 screen's tile pairs (ordered as the tiles below, by first tile;
     // single tiles keep their flag through the ordering)
     std::vector<uint32_t> pl;
     if (fp6_uses_pairs() && T_used <= 0x7FFF && (int64_t)t.size() >= c->opt_fp6_pairs_min) {
         pl = fp6_pair_list(t);
-        if (!c->opt_tile_rows && pl.size() >= 2048) {
-            std::vector<uint32_t> plain(pl.size()), single;
-            for (size_t i = 0; i < pl.size(); ++i) {
-                plain[i] = pl[i] & ~0x8000u;
-                if (pl[i] & 0x8000u) single.push_back(plain[i]);
-            }
-            std::sort(single.begin(), single.end());
-            pl = xcd_order(plain, kS);
-            for (auto &v : pl)
-                if (v != kNoTile && std::binary_search(single.begin(), single.end(), v)) v |= 0x8000u;
-        }
+        if (!c->opt_tile_rows && pl.size() >= 2048) pl = xcd_order(pl, kS, ~0x8000u);
     }
     // only with many rounds of resident tiles: whole super-blocks per XCD
     // leave up to one super-block of imbalance (C2's 528 tiles: +14%)
