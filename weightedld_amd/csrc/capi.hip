@@ -581,6 +581,9 @@ std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t, uint32_t kS, uin
 
 // 64x64 tiles (tb >= ta) of the chunks [lb, le), sorted (ta, tb) so a row of
 // tiles shares its A columns in L2 as in a whole-row run
+#ifndef WLD_F6_KS
+#define WLD_F6_KS 0  // A/B builds only: the tile-pair list's super-block side (0: as the tile list's)
+#endif
 int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
     if (c->tiles_lb == lb && c->tiles_le == le && c->n_tiles) return WLD_OK;
     const uint32_t T_used = (uint32_t)((c->L + kTile - 1) / kTile);
@@ -604,7 +607,7 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
     std::vector<uint32_t> pl;
     if (fp6_uses_pairs() && T_used <= 0x7FFF && (int64_t)t.size() >= c->opt_fp6_pairs_min) {
         pl = fp6_pair_list(t);
-        if (!c->opt_tile_rows && pl.size() >= 2048) pl = xcd_order(pl, kS, ~0x8000u);
+        if (!c->opt_tile_rows && pl.size() >= 2048) pl = xcd_order(pl, WLD_F6_KS ? WLD_F6_KS : kS, ~0x8000u);
     }
     // only with many rounds of resident tiles: whole super-blocks per XCD
     // leave up to one super-block of imbalance (C2's 528 tiles: +14%)
