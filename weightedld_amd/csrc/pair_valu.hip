@@ -597,12 +597,6 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
 #ifndef WLD_ITEM_TRACE
 #define WLD_ITEM_TRACE 0
 #endif
-// WLD_ITEM_CPAIR 1 (variant): the lane classes two at a time, each with its
-// own accumulators (8 independent f32 chains per wave instead of 4; the same
-// sums: each class's chain from 0, joined to the horizontal sum in class order)
-#ifndef WLD_ITEM_CPAIR
-#define WLD_ITEM_CPAIR 0
-#endif
 // Full runs (not LOOP) load each stage's operands at its top instead of one
 // stage ahead: 70 instead of 96 VGPRs, six workgroups per CU instead of five,
 // and the co-resident waves cover the latency (C2 -2.5%, profiles/r05v/; the
@@ -610,6 +604,16 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
 // candidate loop keeps the prefetch (four workgroups per CU either way).
 #ifndef WLD_ITEM_NOPF
 #define WLD_ITEM_NOPF 1
+#endif
+// WLD_ITEM_ASHARE 1 (full runs): the four waves of an item share its 16 rows,
+// so each forms the A operands (w x in, w x major) of one 16-position group of
+// a stage and writes them to LDS, and every wave reads all four: a quarter of
+// the A-side converts and products per wave.  The f32 MFMA runs on the same
+// ALUs as the vector instructions (tools/probes/f32_mfma_rate_probe.hip:
+// ~1.5x the cycles per MFMA with the item's operand work beside it, even at
+// eight waves per SIMD), so vector instructions cost MFMA throughput directly.
+#ifndef WLD_ITEM_ASHARE
+#define WLD_ITEM_ASHARE 0
 #endif
 #if WLD_ITEM_TRACE
 constexpr uint32_t kTraceWaves = 65536;
@@ -623,6 +627,9 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
     uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, OrderArgs o, ScanArgs sa) {
     __shared__ unsigned long long sBits[kTile];  // compaction: passing b per a row
     __shared__ uint32_t sRowBase[kTile];
+    constexpr bool kAShare = WLD_ITEM_ASHARE && !LOOP;
+    // (kAShare) two stages of A operands: [stage & 1][group][element][lane] (u, v)
+    __shared__ float2 sAop[kAShare ? 2 * 16 * 64 : 1];
     const uint32_t tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
@@ -681,64 +688,66 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                 cw[2].x = __uint_as_float(b8.x);
                 cw[2].y = __uint_as_float(b8.y);
             };
-#if WLD_ITEM_CPAIR
-            // classes j and j + 1 side by side, stage s of each (stages of class j
-            // at j ref_cs ..); codes and weights of both loaded at the pair's
-            // stage top (no prefetch: the co-resident waves cover the latency)
-            for (uint32_t j = 0; j < 8; j += 2) {
-                v4f acc0[4], acc1[4];
+            constexpr bool kNoPrefetch = WLD_ITEM_NOPF && !LOOP;
+#if WLD_ITEM_ASHARE
+            if constexpr (kAShare) {
+                // this wave's share: group `wave` of each stage (rows of the item's
+                // row block, lane (r, g) its row r, elements 4 e + g)
+                const uint8_t *rowAs = rowA + 16 * wave;
+                const float *wgs = wg + 16 * wave;
+                uint32_t sa_c = 0, nb[4];
+                float4 sa_w = make_float4(0.f, 0.f, 0.f, 0.f);
+                auto fetch2 = [&](uint32_t k0) {
+                    sa_c = *reinterpret_cast<const uint32_t *>(rowAs + k0);
+                    sa_w = *reinterpret_cast<const float4 *>(wgs + k0);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) acc0[q] = acc1[q] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-                for (uint32_t sidx = 0; sidx < ref_cs; ++sidx) {
-                    const uint32_t k0 = 64 * (j * ref_cs + sidx), k1 = k0 + 64 * ref_cs;
-                    uint32_t A0[4], B0[4], A1[4], B1[4];
-                    float4 W0[4], W1[4];
+                    for (int grp = 0; grp < 4; ++grp) nb[grp] = *reinterpret_cast<const uint32_t *>(rowB + k0 + 16 * grp);
+                };
+                if (n_st) fetch2(0);
+                v4f acc[4];
+                uint32_t in_cls = 0;
+                for (uint32_t st = 0; st < n_st; ++st) {
+                    if (in_cls == 0)
 #pragma unroll
-                    for (int grp = 0; grp < 4; ++grp) {
-                        A0[grp] = *reinterpret_cast<const uint32_t *>(rowA + k0 + 16 * grp);
-                        B0[grp] = *reinterpret_cast<const uint32_t *>(rowB + k0 + 16 * grp);
-                        W0[grp] = *reinterpret_cast<const float4 *>(wg + k0 + 16 * grp);
-                        A1[grp] = *reinterpret_cast<const uint32_t *>(rowA + k1 + 16 * grp);
-                        B1[grp] = *reinterpret_cast<const uint32_t *>(rowB + k1 + 16 * grp);
-                        W1[grp] = *reinterpret_cast<const float4 *>(wg + k1 + 16 * grp);
+                        for (int q = 0; q < 4; ++q) acc[q] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+                    float2 *dst = sAop + (st & 1) * 1024 + wave * 256 + lane;
+                    {
+                        const uint32_t ai = sa_c & 0x01010101u, am = (sa_c >> 1) & 0x01010101u;
+                        const float we[4] = {sa_w.x, sa_w.y, sa_w.z, sa_w.w};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            dst[64 * e] = make_float2(we[e] * cvt_ubyte<0>(ai, e), we[e] * cvt_ubyte<0>(am, e));
                     }
+                    uint32_t B[4];
+#pragma unroll
+                    for (int grp = 0; grp < 4; ++grp) B[grp] = nb[grp];
+                    if (st + 1 < n_st) fetch2(64 * (st + 1));
+                    __syncthreads();  // the stage's four groups written (and the buffer's last readers done)
+                    const float2 *src = sAop + (st & 1) * 1024 + lane;
 #pragma unroll
                     for (int grp = 0; grp < 4; ++grp) {
-                        const float we0[4] = {W0[grp].x, W0[grp].y, W0[grp].z, W0[grp].w};
-                        const float we1[4] = {W1[grp].x, W1[grp].y, W1[grp].z, W1[grp].w};
-                        const uint32_t ai0 = A0[grp] & 0x01010101u, am0 = (A0[grp] >> 1) & 0x01010101u;
-                        const uint32_t bi0 = B0[grp] & 0x01010101u, bm0 = (B0[grp] >> 1) & 0x01010101u;
-                        const uint32_t ai1 = A1[grp] & 0x01010101u, am1 = (A1[grp] >> 1) & 0x01010101u;
-                        const uint32_t bi1 = B1[grp] & 0x01010101u, bm1 = (B1[grp] >> 1) & 0x01010101u;
+                        const uint32_t bi = B[grp] & 0x01010101u, bm = (B[grp] >> 1) & 0x01010101u;
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
-                            const float u0 = we0[e] * cvt_ubyte<0>(ai0, e), v0 = we0[e] * cvt_ubyte<0>(am0, e);
-                            const float fi0 = cvt_ubyte<1>(bi0, e), fm0 = cvt_ubyte<1>(bm0, e);
-                            const float u1 = we1[e] * cvt_ubyte<0>(ai1, e), v1 = we1[e] * cvt_ubyte<0>(am1, e);
-                            const float fi1 = cvt_ubyte<1>(bi1, e), fm1 = cvt_ubyte<1>(bm1, e);
-                            acc0[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u0, fi0, acc0[0], 0, 0, 0);
-                            acc1[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u1, fi1, acc1[0], 0, 0, 0);
-                            acc0[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0, fi0, acc0[1], 0, 0, 0);
-                            acc1[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1, fi1, acc1[1], 0, 0, 0);
-                            acc0[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u0, fm0, acc0[2], 0, 0, 0);
-                            acc1[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u1, fm1, acc1[2], 0, 0, 0);
-                            acc0[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v0, fm0, acc0[3], 0, 0, 0);
-                            acc1[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v1, fm1, acc1[3], 0, 0, 0);
+                            const float2 uv = src[256 * grp + 64 * e];
+                            const float fi = cvt_ubyte<1>(bi, e), fm = cvt_ubyte<1>(bm, e);
+                            acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(uv.x, fi, acc[0], 0, 0, 0);
+                            acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(uv.y, fi, acc[1], 0, 0, 0);
+                            acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(uv.x, fm, acc[2], 0, 0, 0);
+                            acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(uv.y, fm, acc[3], 0, 0, 0);
                         }
                     }
+                    if (++in_cls == ref_cs) {
+                        in_cls = 0;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) tot[e][q] += acc[q][e];
+                    }
                 }
-                // class j's chain, then class j + 1's, onto the ordered horizontal sum
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) tot[e][q] += acc0[q][e];
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) tot[e][q] += acc1[q][e];
-            }
-#else
-            constexpr bool kNoPrefetch = WLD_ITEM_NOPF && !LOOP;
+            } else
+#endif
+            {
             if (n_st && !kNoPrefetch) fetch(0);
             v4f acc[4];
             uint32_t in_cls = 0;  // this stage's index in its class (no modulo in the loop)
@@ -780,7 +789,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                         for (int q = 0; q < 4; ++q) tot[e][q] += acc[q][e];
                 }
             }
-#endif
+            }
             // the scalar tail (lib.rs:461-480), onto the horizontal sums in order
             // (ref_tail_n <= 7, uniform)
             // (one position per step: the byte queues shift down by 8 bits, the
@@ -905,7 +914,9 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
         const uint32_t tile = tiles[blockIdx.x >> 2], q = blockIdx.x & 3;
         // a diagonal tile's sub-blocks left of row block q's diagonal one hold
         // only pairs a > b: not computed (their waves idle to the epilogue)
-        const uint32_t cols = (tile >> 16) == (tile & 0xFFFFu) ? 0xFu & ~((1u << q) - 1u) : 0xFu;
+        // (kAShare: every wave takes part in each stage's A operands, so every
+        // wave computes a sub-block; the epilogue drops the a > b pairs)
+        const uint32_t cols = (tile >> 16) == (tile & 0xFFFFu) && !kAShare ? 0xFu & ~((1u << q) - 1u) : 0xFu;
         if (tile != kNoTile) compute_item(tile, cols << (4 * q), 1u << q);  // kNoTile: padding of an XCD-ordered list
         scan_tail(sa, gridDim.x);  // (every workgroup takes a ticket when the scan is fused)
 #if WLD_ITEM_TRACE
