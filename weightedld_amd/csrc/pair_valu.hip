@@ -582,7 +582,7 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
     return r;
 }
 #ifndef WLD_REF_ITEM_WG
-#define WLD_REF_ITEM_WG 6  // workgroups per CU, full runs (<= 85 VGPRs: 70 without the prefetch)
+#define WLD_REF_ITEM_WG 6  // workgroups per CU, full runs (<= 85 VGPRs: 72 with the shared A operands)
 #endif
 #ifndef WLD_REF_ITEML_WG
 #define WLD_REF_ITEML_WG 4  // ... the candidate loop (its loop state: <= 128 VGPRs)
@@ -612,8 +612,9 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
 // ALUs as the vector instructions (tools/probes/f32_mfma_rate_probe.hip:
 // ~1.5x the cycles per MFMA with the item's operand work beside it, even at
 // eight waves per SIMD), so vector instructions cost MFMA throughput directly.
+// C2 0.1184 -> 0.1114 ms (profiles/r05ad/; rows bit-identical, 191 tests).
 #ifndef WLD_ITEM_ASHARE
-#define WLD_ITEM_ASHARE 0
+#define WLD_ITEM_ASHARE 1
 #endif
 #if WLD_ITEM_TRACE
 constexpr uint32_t kTraceWaves = 65536;
