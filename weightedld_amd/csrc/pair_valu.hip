@@ -628,7 +628,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
     uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, OrderArgs o, ScanArgs sa) {
     __shared__ unsigned long long sBits[kTile];  // compaction: passing b per a row
     __shared__ uint32_t sRowBase[kTile];
-    constexpr bool kAShare = WLD_ITEM_ASHARE && !LOOP;
+    constexpr bool kAShare = WLD_ITEM_ASHARE != 0;
     // (kAShare) two stages of A operands: [stage & 1][group][element][lane] (u, v)
     __shared__ float2 sAop[kAShare ? 2 * 16 * 64 : 1];
     const uint32_t tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
@@ -655,8 +655,12 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
 #pragma unroll
             for (int q = 0; q < 4; ++q) tot[e][q] = 0.0f;
         uint32_t okA4 = 0, okB = 0;  // the epilogue's site flags
-        if (has) {
-            const uint8_t *rowA = rcodes + (size_t)(a0 + 16 * ui + r) * NPr + 4 * g;
+        // (kAShare: a wave without a sub-block still forms its share of the
+        // item's A operands and keeps the stage barriers; the item's 16 rows are
+        // its row block, ctz(owned))
+        if (has || kAShare) {
+            const uint32_t urow = kAShare ? (uint32_t)__builtin_ctz(owned) : ui;
+            const uint8_t *rowA = rcodes + (size_t)(a0 + 16 * urow + r) * NPr + 4 * g;
             const uint8_t *rowB = rcodes + (size_t)(b0 + 16 * un + r) * NPr + 4 * g;
             const float *wg = rw + 4 * g;
             const uint32_t cls = 64 * ref_cs, n_st = 8 * ref_cs;
@@ -701,8 +705,10 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                 auto fetch2 = [&](uint32_t k0) {
                     sa_c = *reinterpret_cast<const uint32_t *>(rowAs + k0);
                     sa_w = *reinterpret_cast<const float4 *>(wgs + k0);
+                    if (has)
 #pragma unroll
-                    for (int grp = 0; grp < 4; ++grp) nb[grp] = *reinterpret_cast<const uint32_t *>(rowB + k0 + 16 * grp);
+                        for (int grp = 0; grp < 4; ++grp)
+                            nb[grp] = *reinterpret_cast<const uint32_t *>(rowB + k0 + 16 * grp);
                 };
                 if (n_st) fetch2(0);
                 v4f acc[4];
@@ -725,6 +731,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                     if (st + 1 < n_st) fetch2(64 * (st + 1));
                     __syncthreads();  // the stage's four groups written (and the buffer's last readers done)
                     const float2 *src = sAop + (st & 1) * 1024 + lane;
+                    if (has)  // (uniform per wave)
 #pragma unroll
                     for (int grp = 0; grp < 4; ++grp) {
                         const uint32_t bi = B[grp] & 0x01010101u, bm = (B[grp] >> 1) & 0x01010101u;
@@ -798,6 +805,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
             // the epilogue's site flags (one dword: the lane's four a rows; one
             // byte: its b column) in the same round trip as the tail, not one
             // load per pair behind the sums
+            if (has) {
             okA4 = *reinterpret_cast<const uint32_t *>(site_ok + a0 + 16 * ui + 4 * g);
             okB = site_ok[b0 + 16 * un + r];
             if (ref_tail_n) fetch_tail();
@@ -822,6 +830,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                 qb1 >>= 8;
                 wlo = make_float4(wlo.y, wlo.z, wlo.w, whi.x);
                 whi = make_float4(whi.y, whi.z, whi.w, 0.0f);
+            }
             }
         }
         // ---- epilogue (lib.rs:482-520, 660) --------------------------------
@@ -915,9 +924,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
         const uint32_t tile = tiles[blockIdx.x >> 2], q = blockIdx.x & 3;
         // a diagonal tile's sub-blocks left of row block q's diagonal one hold
         // only pairs a > b: not computed (their waves idle to the epilogue)
-        // (kAShare: every wave takes part in each stage's A operands, so every
-        // wave computes a sub-block; the epilogue drops the a > b pairs)
-        const uint32_t cols = (tile >> 16) == (tile & 0xFFFFu) && !kAShare ? 0xFu & ~((1u << q) - 1u) : 0xFu;
+        const uint32_t cols = (tile >> 16) == (tile & 0xFFFFu) ? 0xFu & ~((1u << q) - 1u) : 0xFu;
         if (tile != kNoTile) compute_item(tile, cols << (4 * q), 1u << q);  // kNoTile: padding of an XCD-ordered list
         scan_tail(sa, gridDim.x);  // (every workgroup takes a ticket when the scan is fused)
 #if WLD_ITEM_TRACE
