@@ -628,7 +628,9 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
     uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, OrderArgs o, ScanArgs sa) {
     __shared__ unsigned long long sBits[kTile];  // compaction: passing b per a row
     __shared__ uint32_t sRowBase[kTile];
-    constexpr bool kAShare = WLD_ITEM_ASHARE != 0;
+    // (full runs only: a candidate item may pack sub-blocks of several row
+    // blocks, whose waves need different A operands)
+    constexpr bool kAShare = WLD_ITEM_ASHARE && !LOOP;
     // (kAShare) two stages of A operands: [stage & 1][group][element][lane] (u, v)
     __shared__ float2 sAop[kAShare ? 2 * 16 * 64 : 1];
     const uint32_t tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
@@ -655,9 +657,9 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
 #pragma unroll
             for (int q = 0; q < 4; ++q) tot[e][q] = 0.0f;
         uint32_t okA4 = 0, okB = 0;  // the epilogue's site flags
-        // (kAShare: a wave without a sub-block still forms its share of the
-        // item's A operands and keeps the stage barriers; the item's 16 rows are
-        // its row block, ctz(owned))
+        // (kAShare: a wave without a sub-block, left of a diagonal tile's
+        // diagonal, still forms its share of the item's A operands and keeps
+        // the stage barriers; the item's 16 rows are its row block, ctz(owned))
         if (has || kAShare) {
             const uint32_t urow = kAShare ? (uint32_t)__builtin_ctz(owned) : ui;
             const uint8_t *rowA = rcodes + (size_t)(a0 + 16 * urow + r) * NPr + 4 * g;
