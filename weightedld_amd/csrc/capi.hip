@@ -145,8 +145,6 @@ struct wld_ctx {
     size_t L = 0, N = 0, LP = 0, NP = 0;
     DevBuf raw, wraw, codes, w_pad, wstats, site_ok, site_map, planes, frag;
     DevBuf rcodes, rw;       // WLD_OPT_REF_SUMS: codes and weights in lane-class order (ref_layout_kernel)
-    DevBuf rbpl;             // ... and the b operands as f32 planes, for full runs on the item kernel
-    bool have_bpl = false;   // rbpl holds this load's planes
     // the fp6 screen (fp6_prepare): weight codes, packed operands, constants
     DevBuf w6, f6a, f6b;
     Fp6Screen f6{};
@@ -208,7 +206,7 @@ struct wld_ctx {
         // work queued on a borrowed stream (wld_set_stream) may still use the
         // buffers: it completes before they are freed
         if (stream && stream != own_stream) (void)hipStreamSynchronize(stream);
-        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &rcodes, &rw, &rbpl, &w6, &f6a, &f6b, &tiles, &cand, &f6_pairs, &fp6_probe_buf,
+        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &rcodes, &rw, &w6, &f6a, &f6b, &tiles, &cand, &f6_pairs, &fp6_probe_buf,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &chunk_left, &prog_n, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
@@ -670,7 +668,6 @@ OrderArgs order_args(wld_ctx *c) {
 // (pair_valu.hip), built once per load on first use
 int ensure_ref_layout(wld_ctx *c) {
     if (c->have_ref) return WLD_OK;
-    c->have_bpl = false;
     uint32_t tail = 0;
     ref_layout_dims(c->N, &c->ref_cls, &tail, &c->NPr);
     WLD_TRY(ensure(c->rcodes, c->LP * c->NPr));
@@ -678,15 +675,6 @@ int ensure_ref_layout(wld_ctx *c) {
     launch_ref_layout(ptr<uint8_t>(c->codes), ptr<float>(c->w_pad), c->LP, c->NP, c->N, ptr<uint8_t>(c->rcodes),
                       ptr<float>(c->rw), c->stream);
     HIP_TRY(hipGetLastError());
-    // full runs of up to 4 x 768 tiles go to the item kernel, which reads the b
-    // operands from f32 planes (8 bytes per site and position)
-    const uint64_t T = (c->L + kTile - 1) / kTile;
-    if (T * (T + 1) / 2 <= 4ull * kRefCandidateGrid) {
-        WLD_TRY(ensure(c->rbpl, std::max<size_t>(c->LP * c->NPr, 1) * sizeof(float2)));
-        launch_ref_bplanes(ptr<uint8_t>(c->rcodes), c->LP, c->NPr, ptr<float2>(c->rbpl), c->stream);
-        HIP_TRY(hipGetLastError());
-        c->have_bpl = true;
-    }
     c->have_ref = true;
     return WLD_OK;
 }
@@ -727,7 +715,6 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         rv = ValuLaunch{ptr<uint8_t>(c->rcodes), ptr<float>(c->rw), ptr<uint8_t>(c->site_ok), ptr<uint32_t>(c->tiles),
                         c->n_tiles, nullptr, (uint32_t)c->L, (uint32_t)c->NPr, n, thr, c->safe, false, true,
                         c->ref_cls, (uint32_t)(c->N % 8)};
-        rv.bplanes = c->have_bpl ? ptr<float2>(c->rbpl) : nullptr;
     }
     // reference order without a screen in front (no positive threshold, the
     // f32 kernel, dense stats, or the auto policy's full-kernel thresholds):

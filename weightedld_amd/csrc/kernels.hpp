@@ -150,9 +150,6 @@ struct ValuLaunch {
     // tile_count launches: the list's entries are 16-row blocks of candidate
     // tiles (pair_mfma.hip ScreenArgs::rb_items), counted by the buckets
     bool rb_items;
-    // REF full runs on the item kernel: the b operands as f32 planes
-    // (launch_ref_bplanes; null: converted from the codes)
-    const float2 *bplanes = nullptr;
 };
 // returns true when the run's chunk scan ran in the launch (v.scan given, the
 // item kernel of a full run); else the caller launches it
@@ -176,7 +173,6 @@ struct RefRowsLaunch {
 void launch_ref_rows(const RefRowsLaunch &r, const OrderArgs &o, hipStream_t s);
 // the lane-class layout of REF: cls positions per class, the tail stage, NPr
 void ref_layout_dims(size_t N, uint32_t *cls, uint32_t *tail, size_t *NPr);
-void launch_ref_bplanes(const uint8_t *rcodes, size_t LP, size_t NPr, float2 *out, hipStream_t s);
 void launch_ref_layout(const uint8_t *codes, const float *w_pad, size_t LP, size_t NP, size_t N, uint8_t *rcodes,
                        float *rw, hipStream_t s);
 

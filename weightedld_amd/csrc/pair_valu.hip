@@ -616,11 +616,6 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
 #ifndef WLD_ITEM_ASHARE
 #define WLD_ITEM_ASHARE 1
 #endif
-// (planes path) 1: a stage's b operands all loaded before its barrier (32
-// VGPRs); 0: each group's at its use, the compiler schedules them
-#ifndef WLD_ITEM_BPRE
-#define WLD_ITEM_BPRE 0
-#endif
 #if WLD_ITEM_TRACE
 constexpr uint32_t kTraceWaves = 65536;
 __device__ unsigned long long g_item_trace[kTraceWaves * 4];
@@ -630,8 +625,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
     const uint8_t *__restrict__ rcodes, const float *__restrict__ rw, const uint8_t *__restrict__ site_ok,
     const uint32_t *__restrict__ tiles, uint32_t n_tiles, const uint32_t *__restrict__ tile_bits,
     unsigned *tile_work, const unsigned *tile_buckets, uint32_t bucket_cap, uint32_t L, uint32_t NPr,
-    uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, OrderArgs o, ScanArgs sa,
-    const float2 *__restrict__ bpl) {
+    uint32_t ref_cs, uint32_t ref_tail_n, uint32_t n_chunk_rows, float thr, OrderArgs o, ScanArgs sa) {
     __shared__ unsigned long long sBits[kTile];  // compaction: passing b per a row
     __shared__ uint32_t sRowBase[kTile];
     // (full runs only: a candidate item may pack sub-blocks of several row
@@ -708,14 +702,15 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                 // row block, lane (r, g) its row r, elements 4 e + g)
                 const uint8_t *rowAs = rowA + 16 * wave;
                 const float *wgs = wg + 16 * wave;
-                // the b operands as f32 planes (bpl, required here): four {in,
-                // major} pairs of lane (r, g) per group at position 16 grp + 4 g
-                const float2 *rowBp = bpl + (size_t)(b0 + 16 * un + r) * NPr + 4 * g;
-                uint32_t sa_c = 0;
+                uint32_t sa_c = 0, nb[4];
                 float4 sa_w = make_float4(0.f, 0.f, 0.f, 0.f);
                 auto fetch2 = [&](uint32_t k0) {
                     sa_c = *reinterpret_cast<const uint32_t *>(rowAs + k0);
                     sa_w = *reinterpret_cast<const float4 *>(wgs + k0);
+                    if (has)
+#pragma unroll
+                        for (int grp = 0; grp < 4; ++grp)
+                            nb[grp] = *reinterpret_cast<const uint32_t *>(rowB + k0 + 16 * grp);
                 };
                 if (n_st) fetch2(0);
                 v4f acc[4];
@@ -732,37 +727,20 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                         for (int e = 0; e < 4; ++e)
                             dst[64 * e] = make_float2(we[e] * cvt_ubyte<0>(ai, e), we[e] * cvt_ubyte<0>(am, e));
                     }
-#if WLD_ITEM_BPRE
-                    // the planes' b operands of this stage, loaded before the barrier
-                    float4 bp[4][2];
-                    if (has)
+                    uint32_t B[4];
 #pragma unroll
-                        for (int grp = 0; grp < 4; ++grp) {
-                            const float4 *q = reinterpret_cast<const float4 *>(rowBp + 64 * st + 16 * grp);
-                            bp[grp][0] = q[0];
-                            bp[grp][1] = q[1];
-                        }
-#endif
+                    for (int grp = 0; grp < 4; ++grp) B[grp] = nb[grp];
                     if (st + 1 < n_st) fetch2(64 * (st + 1));
                     __syncthreads();  // the stage's four groups written (and the buffer's last readers done)
                     const float2 *src = sAop + (st & 1) * 1024 + lane;
                     if (has)  // (uniform per wave)
 #pragma unroll
                     for (int grp = 0; grp < 4; ++grp) {
-#if !WLD_ITEM_BPRE
-                        float4 bp[4][2];
-                        {
-                            const float4 *q = reinterpret_cast<const float4 *>(rowBp + 64 * st + 16 * grp);
-                            bp[grp][0] = q[0];
-                            bp[grp][1] = q[1];
-                        }
-#endif
-                        const float f[8] = {bp[grp][0].x, bp[grp][0].y, bp[grp][0].z, bp[grp][0].w,
-                                            bp[grp][1].x, bp[grp][1].y, bp[grp][1].z, bp[grp][1].w};
+                        const uint32_t bi = B[grp] & 0x01010101u, bm = (B[grp] >> 1) & 0x01010101u;
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
                             const float2 uv = src[256 * grp + 64 * e];
-                            const float fi = f[2 * e], fm = f[2 * e + 1];
+                            const float fi = cvt_ubyte<1>(bi, e), fm = cvt_ubyte<1>(bm, e);
                             acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(uv.x, fi, acc[0], 0, 0, 0);
                             acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(uv.y, fi, acc[1], 0, 0, 0);
                             acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(uv.x, fm, acc[2], 0, 0, 0);
@@ -1201,22 +1179,6 @@ void launch_ref_layout(const uint8_t *codes, const float *w_pad, size_t LP, size
                        (uint32_t)LP, (uint32_t)NP, (uint32_t)N, (uint32_t)NPr, cls, rcodes, rw);
 }
 
-// The b side's MFMA operands of the lane-class layout as f32 planes: per
-// (site, position) {in, major} as 0.0 / 1.0 (full-run items read them instead
-// of converting code bytes: the f32 MFMA shares the vector ALUs, so every
-// convert costs MFMA throughput)
-__global__ __launch_bounds__(256) void ref_bplanes_kernel(const uint8_t *__restrict__ rcodes, size_t n,
-                                                          float2 *__restrict__ out) {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t c = rcodes[i];
-    out[i] = make_float2((c & kCodeIn) ? 1.0f : 0.0f, (c & kCodeMaj) ? 1.0f : 0.0f);
-}
-void launch_ref_bplanes(const uint8_t *rcodes, size_t LP, size_t NPr, float2 *out, hipStream_t s) {
-    const size_t n = LP * NPr;
-    if (n) hipLaunchKernelGGL(ref_bplanes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rcodes, n, out);
-}
-
 namespace {
 template <bool DENSE, bool SAFE, bool MF, bool REF, bool LOOP>
 void launch_v(const ValuLaunch &v, uint32_t grid, uint32_t flush, uint32_t cs, const OrderArgs &o,
@@ -1246,18 +1208,18 @@ bool launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
                 hipLaunchKernelGGL(ref_item_kernel<true>, dim3(std::min<uint32_t>(4 * v.n_tiles, kRefItemGrid)),
                                    dim3(256), 0, s, v.codes, v.w, v.site_ok, v.tiles, v.n_tiles, v.tile_bits,
                                    v.tile_work, v.tile_buckets, v.bucket_cap, v.L, v.NP, cs, v.ref_tail_n,
-                                   v.n_chunk_rows, v.thr, o, v.scan, nullptr);
+                                   v.n_chunk_rows, v.thr, o, v.scan);
             else launch_v<false, false, true, true, true>(v, grid, flush, cs, o, dn, s);
         } else {
             // every tile of the run: with fewer tiles than four rounds of
             // resident workgroups (BASELINE config 2: 528 tiles), each tile's
             // four 16-row blocks are separate work items (f32 MFMA path)
             if (v.safe) launch_v<false, true, false, true, false>(v, grid, flush, cs, o, dn, s);
-            else if (v.n_tiles <= 4 * kRefCandidateGrid && (v.bplanes || !WLD_ITEM_ASHARE)) {
+            else if (v.n_tiles <= 4 * kRefCandidateGrid) {
                 // (the run's chunk scan in the last workgroup when given)
                 hipLaunchKernelGGL(ref_item_kernel<false>, dim3(4 * grid), dim3(256), 0, s, v.codes, v.w, v.site_ok,
                                    v.tiles, v.n_tiles, nullptr, nullptr, nullptr, 0u, v.L, v.NP, cs, v.ref_tail_n,
-                                   v.n_chunk_rows, v.thr, o, v.scan, v.bplanes);
+                                   v.n_chunk_rows, v.thr, o, v.scan);
                 return v.scan.ticket != nullptr;
             }
             else launch_v<false, false, true, true, false>(v, grid, flush, cs, o, dn, s);
