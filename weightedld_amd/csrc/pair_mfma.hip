@@ -876,17 +876,28 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
 #ifndef WLD_F6_B4
 #define WLD_F6_B4 1
 #endif
+// WLD_F6_BMIN 1 (fp4 B only): each B block in memory is followed by its
+// minor-bit plane (raw & 0x22222222, made once by frag6_kernel), which the
+// tile-pair kernel copies beside it into LDS instead of masking per wave (the
+// four waves of a half read the same B blocks); the single-tile kernel copies
+// only the code blocks and masks as before
+#ifndef WLD_F6_BMIN
+#define WLD_F6_BMIN 0
+#endif
+static_assert(!WLD_F6_BMIN || WLD_F6_B4, "the minor-bit plane is for fp4 B codes");
 constexpr int kF6ABytes = 3072;                         // per 16-site block: A, two channels
-constexpr int kF6BBytes = WLD_F6_B4 ? 1024 : 1536;      // ... and B
+constexpr int kF6BBytes = WLD_F6_B4 ? 1024 : 1536;      // ... and B (its codes; LDS, single-tile kernel)
+constexpr int kF6BMem = kF6BBytes * (WLD_F6_BMIN ? 2 : 1);  // a B block in memory (+ its minor plane)
 constexpr int kF6AStage = 4 * kF6ABytes;                // a tile's A image per 128 sequences
-constexpr int kF6BStage = 4 * kF6BBytes;                // ... and B image
+constexpr int kF6BStage = 4 * kF6BBytes;                // ... and B image (LDS, single-tile kernel)
+constexpr int kF6BStageMem = 4 * kF6BMem;               // ... B image in memory (and the pair kernel's LDS)
 constexpr int kF6Stage = kF6AStage + kF6BStage;
 constexpr uint32_t kF6Major = 8, kF6Minor = 16;         // 6-bit b codes: e2m3 1.0 / 2.0, e3m2 0.5 / 2.0
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 
 size_t fp6_a_bytes(size_t LP, size_t NP) { return LP / 64 * ((NP + 127) / 128) * kF6AStage; }
-size_t fp6_b_bytes(size_t LP, size_t NP) { return LP / 64 * ((NP + 127) / 128) * kF6BStage; }
+size_t fp6_b_bytes(size_t LP, size_t NP) { return LP / 64 * ((NP + 127) / 128) * kF6BStageMem; }
 
 // one thread per (64-site tile, 128-sequence block, 16-site block, lane)
 __global__ __launch_bounds__(256) void frag6_kernel(const uint8_t *__restrict__ codes, const uint8_t *__restrict__ w6,
@@ -921,12 +932,17 @@ __global__ __launch_bounds__(256) void frag6_kernel(const uint8_t *__restrict__ 
         }
     }
     uint8_t *pa = a6 + tk * kF6AStage + blk * kF6ABytes, *pm = pa + 1536;
-    uint8_t *pb = b6 + tk * kF6BStage + blk * kF6BBytes;
+    uint8_t *pb = b6 + tk * kF6BStageMem + blk * kF6BMem;
     *reinterpret_cast<uint4 *>(pa + 16 * lane) = make_uint4(ai[0], ai[1], ai[2], ai[3]);
     *reinterpret_cast<uint2 *>(pa + 1024 + 8 * lane) = make_uint2(ai[4], ai[5]);
     *reinterpret_cast<uint4 *>(pm + 16 * lane) = make_uint4(am[0], am[1], am[2], am[3]);
     *reinterpret_cast<uint2 *>(pm + 1024 + 8 * lane) = make_uint2(am[4], am[5]);
     *reinterpret_cast<uint4 *>(pb + 16 * lane) = make_uint4(b[0], b[1], b[2], b[3]);
+    if (WLD_F6_BMIN) {
+        constexpr uint32_t kMinor = 0x22222222u;
+        *reinterpret_cast<uint4 *>(pb + 1024 + 16 * lane) =
+            make_uint4(b[0] & kMinor, b[1] & kMinor, b[2] & kMinor, b[3] & kMinor);
+    }
     if (!WLD_F6_B4) *reinterpret_cast<uint2 *>(pb + 1024 + 8 * lane) = make_uint2(b[4], b[5]);
 }
 
@@ -967,6 +983,15 @@ __device__ __forceinline__ void f6_block_mfma(v4f (&acc)[2][2], const v8i &ai, c
         acc[1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, b, acc[1][0], 2, 2, 0, kOne, 0, kOne);
         acc[1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, b, acc[1][1], 2, 3, 0, kOne, 0, kOne);
     }
+}
+// ... with the minor-bit plane read from LDS (WLD_F6_BMIN) instead of masked
+[[maybe_unused]] __device__ __forceinline__ void f6_block_mfma2(v4f (&acc)[2][2], const v8i &ai, const v8i &am, const v8i &b,
+                                               const v8i &bmin) {
+    constexpr int kOne = 0x7F7F7F7F;
+    acc[0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, b, acc[0][0], 2, 4, 0, kOne, 0, kOne);
+    acc[0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc[0][1], 2, 4, 0, kOne, 0, kOne);
+    acc[1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, b, acc[1][0], 2, 4, 0, kOne, 0, kOne);
+    acc[1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, bmin, acc[1][1], 2, 4, 0, kOne, 0, kOne);
 }
 // t1 of pair e of a B block's accumulators, mlo its smallest marginal
 __device__ __forceinline__ float f6_terms(const v4f (&acc)[2][2], int e, float R2, float thr_c, float E,
@@ -1048,14 +1073,14 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     const uint32_t tile = ei < n_tiles ? tiles[ei] : kNoTile;
     if (tile == kNoTile) return;  // (uniform: the whole workgroup)
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
-    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB = b6 + (size_t)tb * NK * kF6BStage;
-    // a stage's 1-KB pieces (A image, then B image): wave w copies w, w + 4, ...
+    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB = b6 + (size_t)tb * NK * kF6BStageMem;
+    // a stage's 1-KB pieces (A image, then the B code blocks): wave w copies w, w + 4, ...
     auto issue = [&](uint32_t kb, uint32_t buf) {
         const uint32_t gb = lds + buf * kF6Stage;
-        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b = sB + (size_t)kb * kF6BStage;
+        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b = sB + (size_t)kb * kF6BStageMem;
 #pragma unroll
         for (uint32_t p = wave; p < kF6Stage / 1024; p += 4)
-            glds16_s(p < kF6AStage / 1024 ? a + p * 1024 : b + (p * 1024 - kF6AStage), lane16, gb + p * 1024);
+            glds16_s(p < kF6AStage / 1024 ? a + p * 1024 : b + (p - kF6AStage / 1024) * kF6BMem, lane16, gb + p * 1024);
     };
     issue(0, 0);
     // the give-up test: read by thread 0 while the first stage is in flight,
@@ -1143,13 +1168,14 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
 constexpr uint32_t kF6Single = 0x8000u;
 // s_waitcnt immediate (gfx9 encoding): lgkmcnt(0), vmcnt and expcnt at their maxima
 [[maybe_unused]] constexpr int kWaitLgkm0 = 0xC07F;
-constexpr int kF6PStage = kF6AStage + 2 * kF6BStage;
+constexpr int kF6PStage = kF6AStage + 2 * kF6BStageMem;
 // stage buffers of the tile-pair kernel: 2 (default: one stage in flight while
 // one is computed) or 3 (WLD_F6_RING 3: two stages in flight, counted vmcnt;
 // 120 KB of LDS for the CU's two workgroups)
 #ifndef WLD_F6_RING
 #define WLD_F6_RING 2
 #endif
+static_assert(!WLD_F6_BMIN || (!WLD_F6_PIPE && WLD_F6_RING == 2), "the minor-bit planes: the default stage loop only");
 // waves per SIMD the tile-pair kernel is compiled for: 4 (default, two
 // workgroups per CU, <= 128 VGPRs) or 6 (three per CU, <= 85 VGPRs)
 #ifndef WLD_FP6_PAIR_WPS
@@ -1174,19 +1200,19 @@ __global__ __launch_bounds__(512, WLD_FP6_PAIR_WPS) void pair_fp6_screen2_kernel
     const uint32_t ta = entry >> 16, tb0 = entry & 0x7FFFu;
     const bool single = (entry & kF6Single) != 0, idle = single && half;  // (uniform per wave)
     const uint32_t tb = tb0 + (idle ? 0u : half);
-    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB0 = b6 + (size_t)tb0 * NK * kF6BStage;
-    const uint8_t *sB1 = single ? sB0 : sB0 + (size_t)NK * kF6BStage;
+    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB0 = b6 + (size_t)tb0 * NK * kF6BStageMem;
+    const uint8_t *sB1 = single ? sB0 : sB0 + (size_t)NK * kF6BStageMem;
     // a stage's 1-KB pieces (A image, B image of tb, B image of tb + 1): wave w copies w, w + 8, ...
     auto issue = [&](uint32_t kb, uint32_t buf) {
         const uint32_t gb = lds + buf * kF6PStage;
-        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b0 = sB0 + (size_t)kb * kF6BStage,
-                      *b1 = sB1 + (size_t)kb * kF6BStage;
+        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b0 = sB0 + (size_t)kb * kF6BStageMem,
+                      *b1 = sB1 + (size_t)kb * kF6BStageMem;
 #pragma unroll
         for (uint32_t p = wave; p < kF6PStage / 1024; p += 8) {
             const uint32_t off = p * 1024;
             glds16_s(off < kF6AStage ? a + off
-                                     : off < kF6AStage + kF6BStage ? b0 + (off - kF6AStage)
-                                                                   : b1 + (off - kF6AStage - kF6BStage),
+                                     : off < kF6AStage + kF6BStageMem ? b0 + (off - kF6AStage)
+                                                                      : b1 + (off - kF6AStage - kF6BStageMem),
                      lane16, gb + off);
         }
     };
@@ -1209,7 +1235,7 @@ __global__ __launch_bounds__(512, WLD_FP6_PAIR_WPS) void pair_fp6_screen2_kernel
         for (int x = 0; x < 2; ++x)
 #pragma unroll
             for (int y = 0; y < 2; ++y) acc[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-    const uint32_t boff = kF6AStage + (idle ? 0u : half) * kF6BStage;  // this half's B image in a stage
+    const uint32_t boff = kF6AStage + (idle ? 0u : half) * kF6BStageMem;  // this half's B image in a stage
 #if WLD_F6_PIPE
     // The stage loop, software-pipelined: stage kb's operands are in registers
     // when its MFMAs start (read from LDS during stage kb - 1), so no wave
@@ -1312,7 +1338,13 @@ __global__ __launch_bounds__(512, WLD_FP6_PAIR_WPS) void pair_fp6_screen2_kernel
         const uint8_t *g = smem + buf * kF6PStage;
         const v8i ai = f6_ld24(g + wq * kF6ABytes, lane), am = f6_ld24(g + wq * kF6ABytes + 1536, lane);
 #pragma unroll
-        for (int n = 0; n < 4; ++n) f6_block_mfma(acc[n], ai, am, f6_ldb(g + boff + n * kF6BBytes, lane));
+        for (int n = 0; n < 4; ++n) {
+            if constexpr (WLD_F6_BMIN)
+                f6_block_mfma2(acc[n], ai, am, f6_ldb(g + boff + n * kF6BMem, lane),
+                               f6_ldb(g + boff + n * kF6BMem + 1024, lane));
+            else
+                f6_block_mfma(acc[n], ai, am, f6_ldb(g + boff + n * kF6BMem, lane));
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
         buf ^= 1;
     }
