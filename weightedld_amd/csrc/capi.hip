@@ -188,6 +188,7 @@ struct wld_ctx {
     // no host round trip between scan and gather; gather_cap: the output
     // rows the enqueued gather may write (0: none enqueued)
     bool spec_gather = false;
+    int ev_end = 4;            // the event that ends a pass's scan: 4, or 3 when the scan ran inside the pair launch
     uint64_t gather_cap = 0;
     wld_run_stats stats{};
     // per-chunk progress (wld_run_host with a callback): the run's chunk
@@ -1242,7 +1243,10 @@ int enqueue_pass(wld_ctx *c) {
     } else if (!lin_count && r.count_out) {
         HIP_TRY(hipMemsetAsync(r.count_out, 0, sizeof(unsigned long long), c->stream));
     }
-    HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+    // (a scan fused into the pair launch ends with it: ev[3] marks both, one
+    // event record fewer per pass)
+    c->ev_end = scan_fused ? 3 : 4;
+    if (!scan_fused) HIP_TRY(hipEventRecord(c->ev[4], c->stream));
     c->gather_cap = 0;
     if (c->spec_gather && lin_count) {
         // outputs for a quarter more rows than the last run's (the scan's
@@ -1377,7 +1381,7 @@ int drain_progress(wld_ctx *c, uint32_t lin_begin, uint32_t n_chunks) {
         }
     };
     for (;;) {
-        const hipError_t q = hipEventQuery(c->ev[4]);  // the pass's end (the stream may hold later work)
+        const hipError_t q = hipEventQuery(c->ev[c->ev_end]);  // the pass's end (the stream may hold later work)
         drain();
         if (q == hipSuccess) break;
         if (q != hipErrorNotReady) HIP_TRY(q);
@@ -1437,7 +1441,7 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
         }
         // the pass's end, not the stream's: on a shared stream (wld_set_stream)
         // the next context's run may already be queued behind it
-        HIP_TRY(hipEventSynchronize(c->ev[c->gather_cap ? 5 : 4]));
+        HIP_TRY(hipEventSynchronize(c->ev[c->gather_cap ? 5 : c->ev_end]));
         WLD_TRY(check_guard(c, c->gather_cap ? "pair phase or reference-order gather" : "pair phase"));
         c->run_dirty = false;  // the pass completed: its scan cleaned the run state
         h[0] = __atomic_load_n(&c->h_cnt[0], __ATOMIC_ACQUIRE);
@@ -1464,7 +1468,7 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     // chunk totals the rows kept)
     if (c->ref_pairs_pass ? h[0] < h[1] : h[0] != h[1])
         return fail(WLD_E_HIP, "internal: staging cursor %llu vs chunk total %llu", h[0], h[1]);
-    int order_end = c->gather_cap ? 5 : 4;  // with no rows (and no gather enqueued) it ends at the scan
+    int order_end = c->gather_cap ? 5 : c->ev_end;  // with no rows (and no gather enqueued) it ends at the scan
     if (rows && lin_count && rows > c->gather_cap) {  // not gathered behind the scan
         WLD_TRY(ensure_outputs(c, rows));
         launch_gather(order_args(c), ptr<uint32_t>(c->chunk_base), r.lin_begin, lin_count, n, (uint32_t)c->L, rows,

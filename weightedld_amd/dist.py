@@ -278,7 +278,12 @@ class PipelinedShardStep:
                 self.steps[k].stream.wait_event(self.done[prev])
             elif self.serialize == "pair":
                 self.steps[k].ctx.run_after(self.steps[prev].ctx)
-        self.steps[k].enqueue(thr, chunk_begin, chunk_end, self.done[k])
+        # the step's end event only where a later submit may wait on it (a
+        # wait_event on an older record of the same event only orders less:
+        # the contexts share nothing the kernels write); one record fewer per
+        # step in the common case
+        need_done = self.serialize is True or any(st.rows_seen for st in self.steps)
+        self.steps[k].enqueue(thr, chunk_begin, chunk_end, self.done[k] if need_done else None)
         self.i += 1
         self.pending.append(k)
         return self.steps[self.pending.popleft()].finish() if len(self.pending) > D - 1 else None
