@@ -235,6 +235,7 @@ int set_dev(wld_ctx *c) {
 
 float event_ms(hipEvent_t a, hipEvent_t b) {
     float ms = 0.0f;
+    if (a == b) return 0.0f;  // (a phase that ended where it began: no API call)
     if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
         (void)hipGetLastError();
         return -1.0f;
