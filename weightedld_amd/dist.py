@@ -173,6 +173,7 @@ class ShardStep:
         else:
             self.stream = _HostStream()
         self.rows_seen = False  # some rank had rows in the last finished step
+        self._no_rows = None
         # the gathered counts go to pinned host memory by an async copy queued
         # behind the all_gather; finish() waits on its event and reads them (no
         # synchronous device-to-host read per step: the host's share of a short
@@ -219,7 +220,9 @@ class ShardStep:
         self.rows_seen = max(counts) > 0
         n = self.ctx.run_wait()  # returns at once: the stream is idle
         if max(counts) == 0:
-            return n, (g.cnt.new_zeros((5, 0), dtype=torch.int32) if g.rank == 0 else None)
+            if self._no_rows is None:  # (one empty result, not an allocation per step)
+                self._no_rows = g.cnt.new_zeros((5, 0), dtype=torch.int32)
+            return n, (self._no_rows if g.rank == 0 else None)
         packed = pack_rows_device(self.ctx, n, self.device)
         if self.host:
             packed = packed.cpu()
