@@ -16,7 +16,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-s
 HIP_SRCS := $(CSRC)/encode.hip $(CSRC)/prepass.hip $(CSRC)/pair_valu.hip $(CSRC)/pair_mfma.hip \
             $(CSRC)/order.hip $(CSRC)/capi.hip
 CXX_SRCS := $(CSRC)/host.cpp
-HDRS := include/weightedld.h $(CSRC)/common.hpp $(CSRC)/kernels.hpp $(CSRC)/pair_common.hpp
+HDRS := include/weightedld.h $(CSRC)/common.hpp $(CSRC)/kernels.hpp $(CSRC)/pair_common.hpp $(CSRC)/tile_order.hpp
 OBJDIR := build/obj
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(CXX_SRCS))
 
