@@ -1337,10 +1337,10 @@ int check_guard(wld_ctx *c, const char *phase) {
     if (!g) return WLD_OK;
     c->run_dirty = true;
     c->have_rows = false;
-    return fail(WLD_E_STATE, "internal: the %s refused an out-of-range index (guard 0x%x: %s%s%s%s%s); no rows", phase,
+    return fail(WLD_E_STATE, "internal: the %s refused an out-of-range index (guard 0x%x: %s%s%s%s%s%s); no rows", phase,
                 g, g & kGuardEntry ? "candidate entry " : "", g & kGuardTile ? "tile " : "",
                 g & kGuardPair ? "staged pair " : "", g & kGuardSlice ? "candidate slice " : "",
-                g & kGuardGather ? "gather destination" : "");
+                g & kGuardGather ? "gather destination" : "", g & kGuardSpin ? " stage wait" : "");
 }
 
 // Phase 2: one host wait, the overflow re-run if needed, then (only when rows

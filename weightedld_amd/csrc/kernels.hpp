@@ -53,7 +53,8 @@ enum : unsigned {
     kGuardTile = 2u,    // a listed tile with ta > tb or tb past the set's last tile
     kGuardPair = 4u,    // a staged candidate pair with a >= b or b past the set
     kGuardSlice = 8u,   // a candidate slice outside staging or with a bad tile
-    kGuardGather = 16u  // a gather destination past the run's row count, or a source past staging
+    kGuardGather = 16u, // a gather destination past the run's row count, or a source past staging
+    kGuardSpin = 32u    // a wave of a producer/consumer screen waited past its bound (WLD_F6_PC)
 };
 __device__ inline void report_guard(const OrderArgs &o, unsigned bit) {
     if (o.guard) __hip_atomic_store(o.guard, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

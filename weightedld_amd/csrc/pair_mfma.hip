@@ -1369,6 +1369,179 @@ __global__ __launch_bounds__(512, WLD_FP6_PAIR_WPS) void pair_fp6_screen2_kernel
     if (!idle) screen_verdict(mine ? (uint32_t)sMask[half] : 0u, ta, tb, ltid, n_chunk_rows, o, sc);
 }
 
+// Producer/consumer form of the tile-pair screen (WLD_F6_PC 1, experimental):
+// eight MFMA waves as above plus a ninth that only copies stages into a ring
+// of three LDS buffers.  No stage barrier: the copier publishes each landed
+// stage in an LDS counter (sLoaded) and refills a buffer once all eight MFMA
+// waves' counts of finished stages (sDone) have passed it, so a fast wave runs up to two stages
+// ahead of a slow one instead of meeting it at every stage.  Every wait is
+// bounded: a wave that waits past kPcSpin polls reports kGuardSpin (the host
+// fails the run, no rows) and goes on to the epilogue, whose barriers every
+// wave reaches.
+#ifndef WLD_F6_PC
+#define WLD_F6_PC 0
+#endif
+#if WLD_F6_PC
+constexpr uint32_t kPcSlots = 3, kPcPieces = kF6PStage / 1024, kPcSpin = 1u << 20;
+static_assert(kPcPieces == 20, "the copier's vmcnt immediates count 20 pieces a stage");
+// wait until *ctr >= target (workgroup-uniform value); false past the bound
+__device__ __forceinline__ bool pc_wait(const uint32_t *ctr, uint32_t target) {
+    for (uint32_t n = 0; n < kPcSpin; ++n) {
+        const uint32_t v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__builtin_amdgcn_readfirstlane(v) >= target) {
+            asm volatile("" ::: "memory");  // (no LDS read of the stage moves above the poll)
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+// wait until every MFMA wave's count of finished stages (done[0..7]) >= target
+__device__ __forceinline__ bool pc_wait_all(const uint32_t *done, uint32_t target) {
+    for (uint32_t n = 0; n < kPcSpin; ++n) {
+        uint32_t m = ~0u;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            const uint32_t v = __hip_atomic_load(done + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            m = v < m ? v : m;
+        }
+        if (__builtin_amdgcn_readfirstlane(m) >= target) {
+            asm volatile("" ::: "memory");  // (no copy into the freed buffer moves above the poll)
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+__global__ __launch_bounds__(576, 5) void pair_fp6_screen_pc_kernel(const uint8_t *__restrict__ a6,
+                                                                   const uint8_t *__restrict__ b6,
+                                                                   const uint64_t *__restrict__ ok_bits,
+                                                                   const uint32_t *__restrict__ pairs, uint32_t n_pairs,
+                                                                   uint32_t NK, uint32_t L, uint32_t n_chunk_rows,
+                                                                   float thr, OrderArgs o, ScreenArgs sc) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kPcSlots * kF6PStage];
+    __shared__ unsigned long long sMask[2];
+    __shared__ uint32_t sBail, sCand[2], sLoaded, sDone[8];
+    if (!sc.probe && blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool copier = wave == 8;
+    const uint32_t half = copier ? 0u : wave >> 2, wq = wave & 3, ltid = tid & 255;
+    const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
+    const uint32_t ei = sc.probe ? blockIdx.x * sc.probe_stride + blockIdx.x % sc.probe_stride : blockIdx.x;
+    const uint32_t entry = ei < n_pairs ? pairs[ei] : kNoTile;
+    if (entry == kNoTile) return;  // (uniform: the whole workgroup)
+    const uint32_t ta = entry >> 16, tb0 = entry & 0x7FFFu;
+    const bool single = (entry & kF6Single) != 0, idle = single && half;  // (uniform per wave)
+    const bool worker = !copier && !idle;                                 // decides a tile
+    const uint32_t tb = tb0 + (idle ? 0u : half);
+    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB0 = b6 + (size_t)tb0 * NK * kF6BStageMem;
+    const uint8_t *sB1 = single ? sB0 : sB0 + (size_t)NK * kF6BStageMem;
+    // the copier's stage: its 20 1-KB pieces (A image, B image of tb, B image of tb + 1)
+    auto issue = [&](uint32_t kb) {
+        const uint32_t gb = lds + (kb % kPcSlots) * kF6PStage;
+        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b0 = sB0 + (size_t)kb * kF6BStageMem,
+                      *b1 = sB1 + (size_t)kb * kF6BStageMem;
+        // (rolled loops: the copier's addresses stay in a few SGPRs)
+#pragma unroll 1
+        for (uint32_t off = 0; off < kF6AStage; off += 1024) glds16_s(a + off, lane16, gb + off);
+#pragma unroll 1
+        for (uint32_t off = 0; off < kF6BStageMem; off += 1024) {
+            glds16_s(b0 + off, lane16, gb + kF6AStage + off);
+            glds16_s(b1 + off, lane16, gb + kF6AStage + kF6BStageMem + off);
+        }
+    };
+    if (copier)
+        for (uint32_t kb = 0; kb < kPcSlots && kb < NK; ++kb) issue(kb);
+    if (tid == 0) {  // the give-up test (as the single-tile kernel)
+        uint32_t v = 0;
+        if (sc.bail) {
+            const unsigned cc = __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v = cc > sc.bail ? ((cc & kAbandonBit) ? 2u : 1u) : 0u;
+        }
+        sBail = v;
+        sLoaded = 0u;
+    }
+    if (tid < 8) sDone[tid] = 0u;
+    if (tid < 2) sCand[tid] = 0u, sMask[tid] = 0ull;
+    __syncthreads();  // the counters are set before the copier publishes
+    if (sBail) {      // (uniform) give the pass up: the copier drains its copies, every wave leaves
+        if (tid == 0 && sBail == 1) {
+            atomicOr(sc.cand_count, kAbandonBit);
+            atomicOr(sc.cand_buckets, kAbandonBit);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+    }
+    const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
+    v4f acc[4][2][2];
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) acc[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+    bool stalled = false;
+    if (copier) {
+        // publish stage kb once its copies landed (the copies issued after it
+        // may stay in flight: 20 pieces a stage), then refill the buffer of
+        // stage kb - 1 with stage kb + 2 once every MFMA wave freed it
+        for (uint32_t kb = 0; kb < NK && !stalled; ++kb) {
+            const uint32_t last = kb == 0 ? (NK - 1 < 2u ? NK - 1 : 2u) : (NK - 1 < kb + 1 ? NK - 1 : kb + 1);
+            const uint32_t after = last - kb;  // stages in flight behind kb (0, 1 or 2)
+            if (after == 2)
+                asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+            else if (after == 1)
+                asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_store(&sLoaded, kb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (kb >= 1 && kb + 2 < NK) {
+                if (!pc_wait_all(sDone, kb)) {
+                    stalled = true;
+                    break;
+                }
+                issue(kb + 2);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing in flight when the workgroup ends
+    } else {
+        const uint32_t boff = kF6AStage + (idle ? 0u : half) * kF6BStageMem;  // this half's B image in a stage
+        for (uint32_t kb = 0; kb < NK; ++kb) {
+            if (!pc_wait(&sLoaded, kb + 1)) {
+                stalled = true;
+                break;
+            }
+            const uint8_t *g = smem + (kb % kPcSlots) * kF6PStage;
+            const v8i ai = f6_ld24(g + wq * kF6ABytes, lane), am = f6_ld24(g + wq * kF6ABytes + 1536, lane);
+#pragma unroll
+            for (int n = 0; n < 4; ++n) f6_block_mfma(acc[n], ai, am, f6_ldb(g + boff + n * kF6BBytes, lane));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the buffer done
+            // (every lane stores the same word: no branch the MFMAs could sink past)
+            __hip_atomic_store(&sDone[wave], kb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    if (stalled && lane == 0) report_guard(o, kGuardSpin);
+    const F6Epi ep{ta, tb, wq, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
+    const bool cand = worker && ep.any(acc);
+    if (cand) sCand[half] = 1u;  // (benign race: every writer stores 1)
+    __syncthreads();
+    const bool mine = sCand[half] != 0;  // (uniform per half)
+    if (sc.probe) {  // the sample run: count, decide nothing
+        if (ltid == 0 && worker) {
+            if (mine) atomicAdd(sc.probe, 1u);
+            atomicAdd(sc.probe + 1, 1u);
+        }
+        return;
+    }
+    if (mine && worker) {
+        const unsigned mk = ep.blocks(acc);
+        if (mk) atomicOr(&sMask[half], (unsigned long long)mk);
+    }
+    __syncthreads();
+    if (worker) screen_verdict(mine ? (uint32_t)sMask[half] : 0u, ta, tb, ltid, n_chunk_rows, o, sc);
+}
+#endif
+
 void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b6,
                   hipStream_t s) {
     const size_t n = LP / 16 * ((NP + 127) / 128) * 64;
@@ -1554,6 +1727,12 @@ void launch_fp6_screen(const MfmaLaunch &m, const uint64_t *ok_bits, const Order
                        uint32_t stride, hipStream_t s) {
     if (fp6_uses_pairs() && m.f6_pairs) {
         // (a tile pair per workgroup, the XCD-ordered pair list)
+#if WLD_F6_PC
+        hipLaunchKernelGGL(pair_fp6_screen_pc_kernel, dim3((m.f6_n_pairs + stride - 1) / stride), dim3(576), 0, s,
+                           m.fp6->a6, m.fp6->b6, ok_bits, m.f6_pairs, m.f6_n_pairs, m.fp6->NK, m.L, m.n_chunk_rows,
+                           m.thr, o, sc);
+        return;
+#endif
         hipLaunchKernelGGL(pair_fp6_screen2_kernel, dim3((m.f6_n_pairs + stride - 1) / stride), dim3(512), 0, s,
                            m.fp6->a6, m.fp6->b6, ok_bits, m.f6_pairs, m.f6_n_pairs, m.fp6->NK, m.L, m.n_chunk_rows,
                            m.thr, o, sc);
