@@ -686,10 +686,10 @@ def main():
         achieved = alg_ops / (dom_ms * 1e-3) / 1e12
         if fp6:
             # tile pairs (two tiles sharing one A image per workgroup) from
-            # WLD_OPT_FP6_PAIRS_MIN_TILES tiles (default 8192) while the pair
+            # WLD_OPT_FP6_PAIRS_MIN_TILES tiles (default 0) while the pair
             # list's 15-bit tile index holds the sites
             pairs_min = ctx.get_option("fp6_pairs_min_tiles")
-            kname = ("pair_fp6_screen2_kernel<tile pairs, fp6 x fp4 16x16x128>"
+            kname = ("pair_fp6_screen2w_kernel<tile pairs, 32x64 per wave, fp6 x fp4 16x16x128>"
                      if (L + 63) // 64 <= 0x7FFF and n_tiles >= pairs_min
                      else "pair_fp6_screen_kernel<fp6 x fp4 16x16x128>")
         elif screen_kind == 4:

@@ -230,7 +230,7 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *   WLD_OPT_FP6_PAIRS_MIN_TILES  the fp6 screen computes two tiles of a row
  *                      per workgroup (one shared A operand stream) when the
  *                      run's tile list has at least this many tiles (default
- *                      8192), else one tile per workgroup.  Same rows.
+ *                      0: always), else one tile per workgroup.  Same rows.
  *   WLD_OPT_TEST_GUARD 0 (default); 1 (tests only): before each candidate
  *                      launch the last candidate bucket's count is set one
  *                      past its capacity, so the launch meets an entry outside

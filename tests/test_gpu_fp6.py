@@ -66,9 +66,13 @@ def test_fp6_screen_rows_bit_identical(W, kind, weights):
     else:
         w = np.ones(N, dtype=np.float32)
     ctxs = {}
-    for name, fp6 in (("fp6", 2), ("i8", 0)):
+    # fp6 on the single-tile kernel (a list under fp6_pairs_min_tiles) and on
+    # the tile-pair kernel (fp6_pairs_min_tiles 0, the default), and the i8 screen
+    for name, fp6, pairs_min in (("fp6", 2, 1 << 30), ("fp6pairs", 2, 0), ("i8", 0, None)):
         c = W.Context(0)
         c.set_option("screen_fp6", fp6)
+        if pairs_min is not None:
+            c.set_option("fp6_pairs_min_tiles", pairs_min)
         c.load(buf, w)
         ctxs[name] = c
     for thr in (0.05, 0.2, 0.01, 0.5):
@@ -80,9 +84,10 @@ def test_fp6_screen_rows_bit_identical(W, kind, weights):
             out[name] = (c.rows(), st)
             assert n == len(ref["site_a"])
             _bits_equal(out[name][0], ref)
-        st6 = out["fp6"][1]
-        if st6["screened"] == 1:
-            assert st6["screen_fp6"] == 1, st6
+        for k in ("fp6", "fp6pairs"):
+            st6 = out[k][1]
+            if st6["screened"] == 1:
+                assert st6["screen_fp6"] == 1, st6
         assert out["i8"][1]["screen_fp6"] == 0
     for c in ctxs.values():
         c.close()
@@ -230,14 +235,18 @@ def test_fp6_default_on_bench_data_and_ineligible_weights(W):
     c.close()
 
 
+@pytest.mark.parametrize("pairs", [False, True])
 @pytest.mark.parametrize("N", [64, 100, 128, 190, 1000, 2049])
-def test_fp6_sequence_counts(W, N):
-    """NP not a multiple of 128 (a zero-padded last fp6 block), tiny N."""
+def test_fp6_sequence_counts(W, N, pairs):
+    """NP not a multiple of 128 (a zero-padded last fp6 block), tiny N; on the
+    single-tile (forced) and tile-pair kernels (L 700: 11 tile rows, so the
+    pair list holds single entries beside pairs)."""
     L = 700
     buf = synth(L, N, 31 + N)
     w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
     c = W.Context(0)
     c.set_option("screen_fp6", 2)
+    c.set_option("fp6_pairs_min_tiles", 0 if pairs else 1 << 30)
     c.load(buf, w)
     for thr in (0.02, 0.1):
         c.run(thr)

@@ -136,7 +136,7 @@ struct wld_ctx {
     // the passes of three contexts overlap, the 1/4 shard steps 6% faster on
     // pairs and the 1/8 shard is even within noise (profiles/r05x); C5 pairs
     // 4.8% faster (profiles/r05j)
-    int64_t opt_fp6_pairs_min = 8192;
+    int64_t opt_fp6_pairs_min = 0;  // (tile pairs at every list size: profiles/r05ar/)
     int opt_fp6 = 1;             // WLD_OPT_SCREEN_FP6: 0 off, 1 auto, 2 whenever it applies, 3 auto without the sample run
     bool opt_ref_sums = true;  // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order (default)
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;

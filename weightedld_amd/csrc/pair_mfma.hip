@@ -1369,6 +1369,123 @@ __global__ __launch_bounds__(512, WLD_FP6_PAIR_WPS) void pair_fp6_screen2_kernel
     if (!idle) screen_verdict(mine ? (uint32_t)sMask[half] : 0u, ta, tb, ltid, n_chunk_rows, o, sc);
 }
 
+// Wide-wave form of the tile-pair screen (WLD_F6_WIDE 1, the default; 0 the
+// eight-wave kernel above): four waves, wave w computing rows 32 (w & 1) ..
+// + 31 (two 16-row blocks) x 64 columns of tile tb + (w >> 1): each B block
+// read and masked once for two A row blocks, so per MFMA half the B reads and
+// masks and 5/7 of the LDS bytes of the eight-wave kernel; 128 accumulator
+// registers per lane (166 VGPRs), three workgroups per CU (the same two 20-KB
+// stage buffers each).  C4 -12%, C5 -10% (profiles/r05ap/).
+#ifndef WLD_F6_WIDE
+#define WLD_F6_WIDE 1
+#endif
+#if WLD_F6_WIDE
+__global__ __launch_bounds__(256, 3) void pair_fp6_screen2w_kernel(const uint8_t *__restrict__ a6,
+                                                                  const uint8_t *__restrict__ b6,
+                                                                  const uint64_t *__restrict__ ok_bits,
+                                                                  const uint32_t *__restrict__ pairs, uint32_t n_pairs,
+                                                                  uint32_t NK, uint32_t L, uint32_t n_chunk_rows,
+                                                                  float thr, OrderArgs o, ScreenArgs sc) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6PStage];
+    __shared__ unsigned long long sMask[2];
+    __shared__ uint32_t sBail, sCand[2];
+    if (!sc.probe && blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t half = wave >> 1, rp = wave & 1, ltid = tid & 127;
+    const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
+    const uint32_t ei = sc.probe ? blockIdx.x * sc.probe_stride + blockIdx.x % sc.probe_stride : blockIdx.x;
+    const uint32_t entry = ei < n_pairs ? pairs[ei] : kNoTile;
+    if (entry == kNoTile) return;  // (uniform: the whole workgroup)
+    const uint32_t ta = entry >> 16, tb0 = entry & 0x7FFFu;
+    const bool single = (entry & kF6Single) != 0, idle = single && half;  // (uniform per wave)
+    const uint32_t tb = tb0 + (idle ? 0u : half);
+    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB0 = b6 + (size_t)tb0 * NK * kF6BStageMem;
+    const uint8_t *sB1 = single ? sB0 : sB0 + (size_t)NK * kF6BStageMem;
+    // a stage's 1-KB pieces (A image, B image of tb, B image of tb + 1): wave w copies w, w + 4, ...
+    auto issue = [&](uint32_t kb, uint32_t buf) {
+        const uint32_t gb = lds + buf * kF6PStage;
+        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b0 = sB0 + (size_t)kb * kF6BStageMem,
+                      *b1 = sB1 + (size_t)kb * kF6BStageMem;
+#pragma unroll
+        for (uint32_t p = wave; p < kF6PStage / 1024; p += 4) {
+            const uint32_t off = p * 1024;
+            glds16_s(off < kF6AStage ? a + off
+                                     : off < kF6AStage + kF6BStageMem ? b0 + (off - kF6AStage)
+                                                                      : b1 + (off - kF6AStage - kF6BStageMem),
+                     lane16, gb + off);
+        }
+    };
+    issue(0, 0);
+    if (tid == 0) {  // the give-up test (as the single-tile kernel)
+        uint32_t v = 0;
+        if (sc.bail) {
+            const unsigned cc = __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v = cc > sc.bail ? ((cc & kAbandonBit) ? 2u : 1u) : 0u;
+        }
+        sBail = v;
+    }
+    if (tid < 2) sCand[tid] = 0u, sMask[tid] = 0ull;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
+    v4f acc[2][4][2][2];  // [row block 2 rp + j][b block n][channel_a][X, Y]
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y) acc[j][n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+    const uint32_t boff = kF6AStage + (idle ? 0u : half) * kF6BStageMem;  // this half's B image in a stage
+    const uint32_t aoff = 2 * rp * kF6ABytes;                             // this wave's two A row blocks
+    uint32_t buf = 0;
+    for (uint32_t kb = 0; kb < NK; ++kb) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of the stage landed
+        __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
+        asm volatile("" ::: "memory");
+        if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
+            if (tid == 0 && sBail == 1) {
+                atomicOr(sc.cand_count, kAbandonBit);
+                atomicOr(sc.cand_buckets, kAbandonBit);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            return;
+        }
+        if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
+        const uint8_t *g = smem + buf * kF6PStage;
+        const v8i ai0 = f6_ld24(g + aoff, lane), am0 = f6_ld24(g + aoff + 1536, lane);
+        const v8i ai1 = f6_ld24(g + aoff + kF6ABytes, lane), am1 = f6_ld24(g + aoff + kF6ABytes + 1536, lane);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const v8i b = f6_ldb(g + boff + n * kF6BBytes, lane);
+            f6_block_mfma(acc[0][n], ai0, am0, b);
+            f6_block_mfma(acc[1][n], ai1, am1, b);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
+        buf ^= 1;
+    }
+    const F6Epi ep0{ta, tb, 2 * rp, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
+    const F6Epi ep1{ta, tb, 2 * rp + 1, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
+    const bool cand = !idle && (ep0.any(acc[0]) || ep1.any(acc[1]));
+    if (cand) sCand[half] = 1u;  // (benign race: every writer stores 1)
+    __syncthreads();
+    const bool mine = sCand[half] != 0;  // (uniform per half)
+    if (sc.probe) {  // the sample run: count, decide nothing
+        if (ltid == 0 && !idle) {
+            if (mine) atomicAdd(sc.probe, 1u);
+            atomicAdd(sc.probe + 1, 1u);
+        }
+        return;
+    }
+    if (mine && !idle) {
+        const unsigned mk = ep0.blocks(acc[0]) | ep1.blocks(acc[1]);
+        if (mk) atomicOr(&sMask[half], (unsigned long long)mk);
+    }
+    __syncthreads();
+    if (!idle) screen_verdict(mine ? (uint32_t)sMask[half] : 0u, ta, tb, ltid, n_chunk_rows, o, sc);
+}
+#endif
+
 // Producer/consumer form of the tile-pair screen (WLD_F6_PC 1, experimental):
 // eight MFMA waves as above plus a ninth that only copies stages into a ring
 // of three LDS buffers.  No stage barrier: the copier publishes each landed
@@ -1729,6 +1846,12 @@ void launch_fp6_screen(const MfmaLaunch &m, const uint64_t *ok_bits, const Order
         // (a tile pair per workgroup, the XCD-ordered pair list)
 #if WLD_F6_PC
         hipLaunchKernelGGL(pair_fp6_screen_pc_kernel, dim3((m.f6_n_pairs + stride - 1) / stride), dim3(576), 0, s,
+                           m.fp6->a6, m.fp6->b6, ok_bits, m.f6_pairs, m.f6_n_pairs, m.fp6->NK, m.L, m.n_chunk_rows,
+                           m.thr, o, sc);
+        return;
+#endif
+#if WLD_F6_WIDE
+        hipLaunchKernelGGL(pair_fp6_screen2w_kernel, dim3((m.f6_n_pairs + stride - 1) / stride), dim3(256), 0, s,
                            m.fp6->a6, m.fp6->b6, ok_bits, m.f6_pairs, m.f6_n_pairs, m.fp6->NK, m.L, m.n_chunk_rows,
                            m.thr, o, sc);
         return;
