@@ -130,6 +130,73 @@ def vcf_like(L, n_hap=5008, seed=0x1000, p_missing=0.002, p_rare=0.5):
     return out
 
 
+def planted_ld(L, N, seed=0x91A7, n_tiles=400, max_per_tile=3):
+    """The headline's seeded background (synth) with planted linkage: the
+    workload where the screen must reject nearly every tile yet keep the few
+    that hold rows.  About n_tiles 64x64 tiles each get 1..max_per_tile site
+    pairs (a, b), b's column a copy of a's with a fraction p of its entries
+    replaced by a permutation of a's (p in {0 .. 0.78}: r2 from 1 down to about
+    the 0.05 threshold, some just below it).  Every planted site is used once.
+    The tiles include, deliberately: diagonal tiles (rows of both parities,
+    i.e. first halves of tile-pair entries and single entries, tile 0 and the
+    padded last tile), the padded last tile column (single entries), tiles
+    (ta, tb) with tb even and odd (both halves of a tile pair), the rest
+    uniform over the triangle (every XCD queue); a deliberately chosen tile's
+    first pair has p <= 0.3, so it holds a row.  Returns (buf, planted) with
+    planted = [(a, b, p)]."""
+    buf = synth(L, N)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    T = (L + 63) // 64
+    tiles = []
+    diag = set(rng.choice(np.arange(1, T - 1), size=min(T - 2, 40), replace=False).tolist()) | {0, 1, T - 2, T - 1}
+    tiles += [(t, t) for t in sorted(diag)]
+    tiles += [(int(t), T - 1) for t in rng.choice(T - 1, size=min(T - 1, 30), replace=False)]
+    for parity in (0, 1):
+        k = 0
+        while k < 30:
+            ta = int(rng.integers(0, T - 2))
+            tb = int(rng.integers(ta + 1, T - 1))
+            if tb % 2 == parity:
+                tiles.append((ta, tb))
+                k += 1
+    while len(set(tiles)) < n_tiles:
+        ta, tb = sorted(int(x) for x in rng.integers(0, T, size=2))
+        tiles.append((ta, tb))
+    deliberate = set(tiles)
+    # the deliberate tiles first, in the order chosen (the padded last tile's
+    # 32 sites go to the diagonal tile before the last column), then the rest
+    tiles = list(dict.fromkeys(tiles))
+    used = np.zeros(L, dtype=bool)
+    planted = []
+    levels = np.array([0.0, 0.1, 0.2, 0.3, 0.45, 0.6, 0.7, 0.75, 0.78])
+
+    def free_site(t, exclude=-1):
+        lo, hi = 64 * t, min(L, 64 * t + 64)
+        cand = [s for s in range(lo, hi) if not used[s] and s != exclude]
+        return int(rng.choice(cand)) if cand else -1
+
+    for ta, tb in tiles:
+        for k in range(int(rng.integers(1, max_per_tile + 1))):
+            a = free_site(ta)
+            if a < 0:
+                break
+            used[a] = True
+            b = free_site(tb)
+            if b < 0:
+                used[a] = False
+                break
+            used[b] = True
+            a, b = min(a, b), max(a, b)
+            # (a deliberately chosen tile's first pair well above the threshold)
+            p = float(rng.choice(levels[:4] if k == 0 and (ta, tb) in deliberate else levels))
+            col = buf[a].copy()
+            m = rng.random(N) < p
+            col[m] = rng.permutation(buf[a])[m]
+            buf[b] = col
+            planted.append((a, b, p))
+    return buf, planted
+
+
 def pairs_in_rows(L, rb, re_):
     a0, a1 = min(L, rb * 256), min(L, re_ * 256)
     return (a1 - a0) * (L - 1) - (a1 - 1 + a0) * (a1 - a0) // 2 if a1 > a0 else 0
@@ -193,30 +260,44 @@ def cpu_baseline(buf, w, thr, target_s=15.0, max_s=30.0):
                       "chunk scheduling), gcc -O3 -march=native" % (what, p, t), "host_cpus": share}
 
 
-def fp6_rows_check(ctx, buf, w, L, N, thr):
-    """The fp6 screen forced (WLD_OPT_SCREEN_FP6 2: it completes, never
-    handing over to i8) over the whole workload at thr, its rows against the
-    oracle's bit for bit; the context's options are restored after."""
+def fp6_planted_check(W, dev_index, L, N, thr):
+    """The headline screen where it can fail: the same size
+    and threshold as the timed workload, with planted linkage (planted_ld:
+    ~770 rows over ~380 tiles on every XCD queue, both halves of tile-pair
+    entries, single entries, diagonal and padded tiles), the fp6 screen forced
+    (WLD_OPT_SCREEN_FP6 2) and in auto, each pass's rows against the oracle's
+    bit for bit, with the candidate counts.  Outside the timed region."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import _oracle as O  # checker only
     O.use_native()
+    buf, planted = planted_ld(L, N)
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
     t0 = time.perf_counter()
     ref = O.all_pairs(buf, w, np.float32(thr), n_threads=host_cpu_share()[0])
     oracle_s = time.perf_counter() - t0
-    keep = ctx.get_option("screen_fp6")
-    ctx.set_option("screen_fp6", 2)
-    n = ctx.run_chunks(thr, 0, ctx.chunks(L))
-    st = ctx.stats()
-    g = ctx.rows()
-    ctx.set_option("screen_fp6", keep)
-    equal = n == len(ref["r2"]) and all(
-        np.array_equal(np.asarray(getattr(g, f)).astype(np.uint32), np.asarray(ref[f]).astype(np.uint32))
-        for f in ("site_a", "site_b")) and all(
-        np.array_equal(np.asarray(getattr(g, f), dtype=np.float32).view(np.uint32),
-                       np.asarray(ref[f], dtype=np.float32).view(np.uint32)) for f in ("d", "d_prime", "r2"))
-    return {"thr": thr, "gpu_rows": n, "oracle_rows": int(len(ref["r2"])), "equal": bool(equal),
-            "screen_fp6": st["screen_fp6"], "candidate_tiles": st["candidate_tiles"], "tiles": st["tiles"],
-            "oracle_s": oracle_s}
+    out = {"data": "bench.planted_ld (seeded background + %d planted pairs)" % len(planted), "thr": thr,
+           "oracle_rows": int(len(ref["r2"])),
+           "tiles_holding_rows": len(set(zip((ref["site_a"] // 64).tolist(), (ref["site_b"] // 64).tolist()))),
+           "oracle_s": oracle_s}
+    for mode, opt in (("forced", 2), ("auto", None)):
+        c = W.Context(dev_index)
+        if opt is not None:
+            c.set_option("screen_fp6", opt)
+        c.load(buf, w)
+        n = c.run(thr)
+        st = c.stats()
+        g = c.rows()
+        equal = n == len(ref["r2"]) and all(
+            np.array_equal(np.asarray(getattr(g, f)).astype(np.uint32), np.asarray(ref[f]).astype(np.uint32))
+            for f in ("site_a", "site_b")) and all(
+            np.array_equal(np.asarray(getattr(g, f), dtype=np.float32).view(np.uint32),
+                           np.asarray(ref[f], dtype=np.float32).view(np.uint32)) for f in ("d", "d_prime", "r2"))
+        out[mode] = {"gpu_rows": n, "equal": bool(equal), "screen_fp6": st["screen_fp6"],
+                     "candidate_tiles": st["candidate_tiles"], "candidate_blocks": st["candidate_blocks"],
+                     "tiles": st["tiles"], "pair_kernel_ms": st["pair_kernel_ms"]}
+        c.close()
+    out["equal"] = out["forced"]["equal"] and out["auto"]["equal"] and out["forced"]["screen_fp6"] == 1
+    return out
 
 
 def host_cpu_share():
@@ -467,7 +548,7 @@ def main():
     # RCCL count all_gather ordered after them on that stream, one host wait;
     # rows (if any) then gathered to rank 0 in reference order (shards
     # concatenate in descending rank order: chunk rows descend)
-    shard_step = wdist.ShardStep(ctx, rank, world, device, host_collectives=host_coll) if dist_on else None
+    shard_step = None  # (set below: the pipeline's first step when there is one)
     # N>1 timed steps: two contexts on the same resident inputs, step i's
     # kernel queued on the device behind step i-1's while step i-1's count
     # exchange / host read / row gather complete (PipelinedShardStep)
@@ -499,6 +580,11 @@ def main():
                                         # archive/profiles_r01_r03/r03i/)
                                         serialize_kernels={"0": False, "1": True}.get(serialize, "pair"),
                                         host_collectives=host_coll)
+    if dist_on:
+        # single steps on ctx (stats sampling, unscreened and checked steps) go
+        # through the pipeline's own step object for ctx: one stream per context
+        shard_step = pipe.steps[0] if pipe is not None else wdist.ShardStep(ctx, rank, world, device,
+                                                                              host_collectives=host_coll)
 
     def nrows(res):
         return int(res[1].shape[1]) if res is not None and res[1] is not None else 0
@@ -887,11 +973,11 @@ def main():
         assert out["rows_check"]["one_sided_outside_1e-5_of_thr"] == 0, out["rows_check"]
         assert not args.ref_sums or len(one_sided) == 0, out["rows_check"]
         assert not whole or rows == len(kg), (rows, len(kg))
-        if fp6 and whole and world == 1 and len(kr) < 1000 and args.ref_sums:
+        if fp6 and whole and world == 1 and len(kr) < 1000 and args.ref_sums and args.config == "c4":
             # the check above is vacuous where no row passes (C4 at 0.05): the
-            # fp6 screen forced on the whole workload at a threshold where
-            # rows do pass, every row against the oracle (same rows, order, bits)
-            out["rows_check_fp6"] = fp6_rows_check(ctx, buf, weights, L, N, min(thr, 0.01))
+            # same size and threshold with planted linkage, the fp6 screen
+            # forced and auto, every row against the oracle (rows, order, bits)
+            out["rows_check_fp6"] = fp6_planted_check(W, dev_index, L, N, thr)
             assert out["rows_check_fp6"]["equal"], out["rows_check_fp6"]
     print(json.dumps(out), flush=True)
     close_all()

@@ -4,7 +4,7 @@
 // device starts from v_rcp_f64) must equal the IEEE f32 quotient x / T for
 // every pair tried.  Random significands over wide exponent ranges, x and T
 // near each other, x / T near 1, subnormal quotients, integer-valued sums,
-// powers of two.  Prints the mismatch count; exits 1 on any.
+// powers of two, subnormal T.  Prints the mismatch count; exits 1 on any.
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -25,7 +25,7 @@ int main(int argc, char **argv) {
     long bad = 0, tried = 0;
     auto check = [&](float x, float t) {
         if (!(t != 0.0f) || !std::isfinite(t) || !std::isfinite(x)) return;
-        const double r = wld::recip_f64((double)t, (double)(1.0f / t));
+        const double r = wld::recip_f64((double)t, wld::recip_seed_host(t));
         const float q = (float)((double)x * r), ref = x / t;
         ++tried;
         uint32_t a, b;
@@ -39,7 +39,7 @@ int main(int argc, char **argv) {
     std::uniform_int_distribution<uint32_t> mant(0, (1u << 23) - 1), ex(1, 254), small(0, 60);
     for (long i = 0; i < n; ++i) {
         const uint32_t mt = mant(rng), mx = mant(rng);
-        switch (i % 6) {
+        switch (i % 7) {
         case 0:  // anything
             check(bits(ex(rng) << 23 | mx), bits(ex(rng) << 23 | mt));
             break;
@@ -58,6 +58,9 @@ int main(int argc, char **argv) {
             break;
         case 4:  // subnormal quotients
             check(bits((1 + small(rng)) << 23 | mx), bits((100 + small(rng)) << 23 | mt));
+            break;
+        case 6:  // subnormal T (quotients up to overflow)
+            check(bits(ex(rng) % 160 << 23 | mx), bits(mt ? mt : 1u));
             break;
         default:  // powers of two and all-ones significands
             check(bits(ex(rng) << 23 | ((i & 8) ? 0x7FFFFFu : 0u)), bits(ex(rng) << 23 | ((i & 16) ? 0x7FFFFFu : mt)));

@@ -124,3 +124,26 @@ def test_launcher_two_ranks_rows_equal_oracle_every_step():
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
     assert cb["host_cpus"]["affinity"] >= cb["cores"] and cb["host_cpus"]["threads_from"]
     assert out["rows_check"]["one_sided"] == 0
+
+
+@pytest.mark.gpu
+def test_launcher_eight_ranks_rows_equal_oracle_every_step():
+    """the driver's N=8 launch path, run once before its SCALE
+    run does: `bench.py --gpus 8` spawns eight ranks (here all on the box's
+    one GPU, counts and rows over gloo host tensors: a functional check, not a
+    performance line); BASELINE config 2 at threshold 0, each rank's 1/8
+    chunk range, the pipelined N>1 step loop; both checked steps' gathered
+    rows equal the oracle's bit for bit in reference order, and the line says
+    n_gpus 8."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--collectives", "gloo", "--config", "c2",
+                        "--steps", "3", "--warmup", "1", "--settle-s", "0", "--check-steps", "2",
+                        "--cpu-seconds", "1"], cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["config"]["launch"] == "bench.py spawned 8 ranks"
+    sc = out["steps_check"]
+    assert sc["steps"] == 2 and sc["equal_to_oracle"] == 2 and sc["rows_per_step"] > 1_900_000
+    print("eight ranks: %.3f ms/step (one shared GPU), steps_check %s" % (out["ms_per_step"], sc))

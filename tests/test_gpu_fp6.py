@@ -289,3 +289,97 @@ def test_fp6_forced_full_size_rows(W, cfg):
     print("fp6 forced full size %s: (thr, rows, candidate tiles, tiles) %s" % (cfg, counts))
     assert max(n for _, n, _, _ in counts) >= (1000 if cfg == "c4" else 10000), counts
     c.close()
+
+
+def _planted(cfg):
+    import bench
+    N, L, thr, _ = bench.CONFIGS[cfg]
+    buf, planted = bench.planted_ld(L, N)
+    import weightedld_amd as W
+    w = W.henikoff_weights(W.SiteSet.from_buffer(buf))
+    return buf, w, np.float32(thr), planted
+
+
+@pytest.fixture(scope="module")
+def planted_c4():
+    buf, w, thr, planted = _planted("c4")
+    return buf, w, thr, planted, O.all_pairs(buf, w, thr)
+
+
+@pytest.mark.parametrize("mode", ["forced", "auto"])
+def test_fp6_planted_full_size_c4(W, planted_c4, mode):
+    """the headline screen where it rejects nearly every tile
+    yet must keep the few that hold rows.  BASELINE config 4 at full size and
+    its threshold 0.05, the bench's seeded background with planted linkage
+    (bench.planted_ld: ~750 passing pairs over ~380 tiles on every XCD queue,
+    both halves of tile-pair entries, single entries, diagonal tiles and the
+    padded last tile row and column; r2 from 1 down to just above 0.05, and
+    planted pairs just below it).  fp6 forced (WLD_OPT_SCREEN_FP6 2) and auto
+    (the sample run decides): the pass runs on fp6, candidates are <= 2% of
+    the tiles, and the rows, their order and every bit of d, d', r2 equal the
+    oracle's (lib.rs:647-669, :660), twice on one context."""
+    buf, w, thr, planted, ref = planted_c4
+    L = buf.shape[0]
+    rt = set(zip((ref["site_a"] // 64).tolist(), (ref["site_b"] // 64).tolist()))
+    assert len(ref["r2"]) >= 500 and len(rt) >= 300, (len(ref["r2"]), len(rt))
+    T = (L + 63) // 64
+    assert any(a == b for a, b in rt) and any(b == T - 1 for _, b in rt) and (T - 1, T - 1) in rt
+    c = W.Context(0)
+    if mode == "forced":
+        c.set_option("screen_fp6", 2)
+    c.load(buf, w)
+    seen = []
+    for _ in range(2):
+        n = c.run(float(thr))
+        st = c.stats()
+        seen.append((n, st["candidate_tiles"], st["candidate_blocks"], st["tiles"], st["fp6_sampled"]))
+        assert st["screened"] == 1 and st["screen_fp6"] == 1, st
+        assert st["candidate_tiles"] * 50 <= st["tiles"], st
+        assert st["candidate_tiles"] >= len(rt), (st, len(rt))
+        assert n == len(ref["r2"])
+        _bits_equal(c.rows(), ref)
+    print("planted C4 %s: rows %d over %d tiles; (rows, candidate tiles, candidate sub-blocks, tiles, sampled) %s"
+          % (mode, len(ref["r2"]), len(rt), seen))
+    c.close()
+
+
+def test_fp6_planted_full_size_c5(W):
+    """The same at BASELINE config 5's size (5000 x 50000, thr 0.05), where
+    the full oracle does not fit a test's time: the forced-fp6 and auto rows
+    equal, bit for bit, those of the unscreened run (every tile through the
+    kernel in lib.rs's summation order, WLD_OPT_SCREEN 0 — the path the
+    oracle pins at every smaller size), and every planted pair's d, d', r2
+    equal the oracle's single_weighted_ld_pair (lib.rs:390-521); every
+    planted pair with r2 > thr is a row."""
+    buf, w, thr, planted = _planted("c5")
+    ref_c = W.Context(0)
+    ref_c.set_option("screen", 0)
+    ref_c.load(buf, w)
+    n_ref = ref_c.run(float(thr))
+    ref = _store_dict(ref_c.rows())
+    ref_c.close()
+    rows = {(int(a), int(b)): i for i, (a, b) in enumerate(zip(ref["site_a"], ref["site_b"]))}
+    hits = 0
+    for a, b, _ in planted:
+        d, dp, r2 = O.single_pair(buf[a], buf[b], w)
+        if np.float32(r2) > thr:
+            i = rows[(a, b)]
+            got = np.array([ref["d"][i], ref["d_prime"][i], ref["r2"][i]], dtype=np.float32)
+            assert np.array_equal(got.view(np.uint32), np.array([d, dp, r2], dtype=np.float32).view(np.uint32))
+            hits += 1
+    rt = set(zip((ref["site_a"] // 64).tolist(), (ref["site_b"] // 64).tolist()))
+    assert hits >= 500 and len(rt) >= 300, (hits, len(rt))
+    for mode in ("forced", "auto"):
+        c = W.Context(0)
+        if mode == "forced":
+            c.set_option("screen_fp6", 2)
+        c.load(buf, w)
+        n = c.run(float(thr))
+        st = c.stats()
+        assert st["screened"] == 1 and st["screen_fp6"] == 1, st
+        assert st["candidate_tiles"] * 50 <= st["tiles"], st
+        assert n == n_ref
+        _bits_equal(c.rows(), ref)
+        print("planted C5 %s: rows %d (planted %d) over %d tiles; candidate tiles %d of %d"
+              % (mode, n, hits, len(rt), st["candidate_tiles"], st["tiles"]))
+        c.close()

@@ -172,7 +172,7 @@ struct wld_ctx {
 
     // run state
     DevBuf tiles, cand, seg_cnt, seg_off, chunk_total, chunk_base, counters;
-    DevBuf f6_pairs;          // the fp6 screen's tile-pair list of the tile list (fp6_uses_pairs)
+    DevBuf f6_pairs;          // the fp6 screen's tile-pair list of the tile list (pair_fp6_screen2w_kernel)
     uint32_t f6_n_pairs = 0;
     std::vector<uint64_t> chunk_pairs_pre;  // prefix sums of the loaded set's per-chunk pair counts (linear order)
     DevBuf st_a, st_b, st_d, st_dp, st_r2;
@@ -457,15 +457,24 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     // lists on its first pass)
     if (c->opt_fp6 != 0) WLD_TRY(fp6_prepare(c));
     if (c->opt_ref_sums) WLD_TRY(ensure_ref_layout(c));
-    WLD_TRY(build_tiles(c, 0, chunks_of(L)));
-    {  // a run's pair count in O(1) (the per-chunk loop took microseconds per run)
+    {  // a run's pair count in O(1) (the per-chunk loop took microseconds per run);
+       // up to 2^24 chunks (128 MB of prefix; ~1.48M sites), beyond that per run
         const uint32_t m = chunks_of(L), nr = chunk_rows_of(L);
-        c->chunk_pairs_pre.assign((size_t)m + 1, 0);
-        for (uint32_t i = 0; i < m; ++i) {
+        c->chunk_pairs_pre.assign(m <= (1u << 24) ? (size_t)m + 1 : 0, 0);
+        for (uint32_t i = 0; i < m && m <= (1u << 24); ++i) {
             uint32_t row, col;
             chunk_of_linear_host(nr, i, row, col);
             c->chunk_pairs_pre[i + 1] = c->chunk_pairs_pre[i] + pairs_in_chunk(L, row, col);
         }
+    }
+    // the whole set's tile lists only where a whole-set run is possible (<=
+    // 2^32 pairs, run_enqueue's limit; about 92,700 sites) and the lists stay
+    // small (<= 2^22 tiles: 512 MB of candidate-list space at most); larger
+    // sets run only as shards, whose first run builds its own lists
+    {
+        const uint64_t T_used = (L + kTile - 1) / kTile;
+        if ((uint64_t)L * (L - 1) / 2 <= 0xFFFFFFFFull && T_used * (T_used + 1) / 2 <= (1ull << 22))
+            WLD_TRY(build_tiles(c, 0, chunks_of(L)));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     return WLD_OK;
@@ -526,21 +535,18 @@ void rows_to_linear(uint32_t n, uint32_t rb, uint32_t re, uint32_t &lb, uint32_t
 // xcd_order and range_tiles: tile_order.hpp
 using tile_order::xcd_order;
 
-#ifndef WLD_F6_KS
-#define WLD_F6_KS 0  // A/B builds only: the tile-pair list's super-block side (0: as the tile list's)
-#endif
 int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
     if (c->tiles_lb == lb && c->tiles_le == le && c->n_tiles) return WLD_OK;
     const uint32_t T_used = (uint32_t)((c->L + kTile - 1) / kTile);
     const uint32_t n = chunk_rows_of(c->L);
     std::vector<uint32_t> t = tile_order::range_tiles(n, T_used, lb, le);  // (ta, tb) order
-    const uint32_t kS = 24ull * kTile * c->NP <= (4ull << 20) ? 16u : 8u;
+    const uint32_t kS = tile_order::super_block_side((uint32_t)c->NP);
     // the fp6 screen's tile pairs (ordered as the tiles below, by first tile;
     // single tiles keep their flag through the ordering)
     std::vector<uint32_t> pl;
-    if (fp6_uses_pairs() && T_used <= 0x7FFF && (int64_t)t.size() >= c->opt_fp6_pairs_min) {
-        pl = fp6_pair_list(t);
-        if (!c->opt_tile_rows && pl.size() >= 2048) pl = xcd_order(pl, WLD_F6_KS ? WLD_F6_KS : kS, ~0x8000u);
+    if (T_used <= 0x7FFF && (int64_t)t.size() >= c->opt_fp6_pairs_min) {
+        pl = tile_order::fp6_pair_list(t);
+        if (!c->opt_tile_rows && pl.size() >= 2048) pl = xcd_order(pl, kS, ~0x8000u);
     }
     // only with many rounds of resident tiles: whole super-blocks per XCD
     // leave up to one super-block of imbalance (C2's 528 tiles: +14%)
@@ -1192,12 +1198,20 @@ int enqueue_pass(wld_ctx *c) {
 // candidates the threshold (and any lower one) goes to the i8 screen, else it
 // (and any higher one) stays on fp6 with no further sample.  Small lists
 // (fewer than 2,048 tiles) take the pass itself as the test, as before.
-int fp6_sample(wld_ctx *c, float thr) {
+// Only where the pass would run the one-plane screen (launch_pairs: the
+// screen policy, no dense stats); on the context's own stream when the
+// caller lent it one and the fp6 operands were built before this run (the
+// probe reads only them), so the read-back does not wait for the caller's
+// earlier work on the borrowed stream.
+int fp6_sample(wld_ctx *c, float thr, bool operands_fresh) {
     if (c->opt_fp6 != 1 || !c->fp6_ok || !c->fp6_better || !(thr > c->fp6_bad_thr) || thr >= c->fp6_good_thr)
         return WLD_OK;
     if (c->kernel != WLD_KERNEL_MFMA || !c->use_frag || !c->opt_prefilter || !(thr > 0.0f) || c->opt_screen == 0 ||
         c->n_tiles < 2048)
         return WLD_OK;
+    if (!(c->opt_screen == 2 || c->opt_screen == 3 || (c->opt_screen == 1 && thr > c->screen_bad_thr)))
+        return WLD_OK;  // no one-plane screen at this threshold: nothing to decide
+    const hipStream_t s = !operands_fresh && c->own_stream ? c->own_stream : c->stream;
     WLD_TRY(ensure(c->fp6_probe_buf, 2 * sizeof(unsigned)));
     MfmaLaunch m{};
     m.wplanes = ptr<int8_t>(c->planes);
@@ -1214,11 +1228,11 @@ int fp6_sample(wld_ctx *c, float thr) {
     m.f6_n_pairs = c->f6_n_pairs;
     const uint32_t entries = m.f6_pairs ? m.f6_n_pairs : m.n_tiles;
     const uint32_t stride = std::max<uint32_t>(1, std::min<uint32_t>(64, entries / 256));
-    launch_fp6_probe(m, ptr<unsigned>(c->fp6_probe_buf), stride, c->stream);
+    launch_fp6_probe(m, ptr<unsigned>(c->fp6_probe_buf), stride, s);
     HIP_TRY(hipGetLastError());
     unsigned h[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(h, c->fp6_probe_buf.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpyAsync(h, c->fp6_probe_buf.p, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
     c->fp6_sampled = true;
     if ((uint64_t)h[0] * 16 > h[1])
         c->fp6_bad_thr = std::max(c->fp6_bad_thr, thr);
@@ -1236,10 +1250,11 @@ int run_enqueue(wld_ctx *c, float thr, uint32_t lin_begin, uint32_t lin_end, uns
     const uint32_t n = chunk_rows_of(c->L);
     c->have_rows = false;
     c->pend.active = false;
-    if (!c->fp6_tried && c->opt_fp6 != 0) WLD_TRY(fp6_prepare(c));
+    const bool fp6_fresh = !c->fp6_tried && c->opt_fp6 != 0;
+    if (fp6_fresh) WLD_TRY(fp6_prepare(c));
     WLD_TRY(build_tiles(c, lin_begin, lin_end));
     c->fp6_sampled = false;
-    WLD_TRY(fp6_sample(c, thr));
+    WLD_TRY(fp6_sample(c, thr, fp6_fresh));
     const uint64_t pairs = c->chunk_pairs_pre.size() > lin_end
                                ? c->chunk_pairs_pre[lin_end] - c->chunk_pairs_pre[lin_begin]
                                : pairs_in_chunks(c->L, lin_begin, lin_end);
@@ -1337,10 +1352,10 @@ int check_guard(wld_ctx *c, const char *phase) {
     if (!g) return WLD_OK;
     c->run_dirty = true;
     c->have_rows = false;
-    return fail(WLD_E_STATE, "internal: the %s refused an out-of-range index (guard 0x%x: %s%s%s%s%s%s); no rows", phase,
+    return fail(WLD_E_STATE, "internal: the %s refused an out-of-range index (guard 0x%x: %s%s%s%s%s); no rows", phase,
                 g, g & kGuardEntry ? "candidate entry " : "", g & kGuardTile ? "tile " : "",
                 g & kGuardPair ? "staged pair " : "", g & kGuardSlice ? "candidate slice " : "",
-                g & kGuardGather ? "gather destination" : "", g & kGuardSpin ? " stage wait" : "");
+                g & kGuardGather ? "gather destination" : "");
 }
 
 // Phase 2: one host wait, the overflow re-run if needed, then (only when rows

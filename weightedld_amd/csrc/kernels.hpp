@@ -53,8 +53,7 @@ enum : unsigned {
     kGuardTile = 2u,    // a listed tile with ta > tb or tb past the set's last tile
     kGuardPair = 4u,    // a staged candidate pair with a >= b or b past the set
     kGuardSlice = 8u,   // a candidate slice outside staging or with a bad tile
-    kGuardGather = 16u, // a gather destination past the run's row count, or a source past staging
-    kGuardSpin = 32u    // a wave of a producer/consumer screen waited past its bound (WLD_F6_PC)
+    kGuardGather = 16u  // a gather destination past the run's row count, or a source past staging
 };
 __device__ inline void report_guard(const OrderArgs &o, unsigned bit) {
     if (o.guard) __hip_atomic_store(o.guard, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -218,11 +217,6 @@ struct Fp6Screen {
 };
 size_t fp6_a_bytes(size_t LP, size_t NP);
 size_t fp6_b_bytes(size_t LP, size_t NP);
-// the fp6 screen runs on tile pairs (pair_fp6_screen2_kernel: one A image for
-// two column tiles) rather than single tiles
-bool fp6_uses_pairs();
-// the pair list of a (ta, tb)-sorted tile list (pair_mfma.hip)
-std::vector<uint32_t> fp6_pair_list(const std::vector<uint32_t> &sorted_tiles);
 // w6: NP fp6 (e2m3) codes of the rounded weights (0 for padding)
 void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b6,
                   hipStream_t s);
@@ -266,7 +260,7 @@ struct MfmaLaunch {
     const Fp6Screen *fp6;
     // ... gives up past this many candidate tiles (0: never; kAbandonBit)
     uint32_t fp6_bail;
-    // ... its tile-pair list (fp6_uses_pairs; XCD-ordered, kNoTile padded)
+    // ... its tile-pair list (pair_fp6_screen2w_kernel; XCD-ordered, kNoTile padded)
     const uint32_t *f6_pairs;
     uint32_t f6_n_pairs;
 };

@@ -35,6 +35,11 @@ __host__ __device__ __forceinline__ double recip_f64(double t, double r0) {
     e = fma(-t, r, 1.0);
     return fma(r, e, r);
 }
+// The host's estimate: the f32 reciprocal, a subnormal t first scaled into
+// the normal range (1.0f / t overflows to inf there)
+__host__ __forceinline__ double recip_seed_host(float t) {
+    return fabsf(t) < 0x1p-126f ? (double)(1.0f / (t * 0x1p64f)) * 0x1p64 : (double)(1.0f / t);
+}
 __host__ __device__ __forceinline__ void ld_epilogue(float total_weight, float PA, float PB, float ld3, float &d_out,
                                                      float &dp_out, float &r2_out) {
     float ld_obs0, ld_obs1, ld_obs2, ld_obs3 = ld3;
@@ -47,7 +52,7 @@ __host__ __device__ __forceinline__ void ld_epilogue(float total_weight, float P
 #if defined(__HIP_DEVICE_COMPILE__)
         const double r = recip_f64((double)total_weight, __builtin_amdgcn_rcp((double)total_weight));
 #else
-        const double r = recip_f64((double)total_weight, (double)(1.0f / total_weight));
+        const double r = recip_f64((double)total_weight, recip_seed_host(total_weight));
 #endif
         PA = (float)((double)PA * r);
         PB = (float)((double)PB * r);

@@ -867,37 +867,22 @@ __global__ __launch_bounds__(64 * GroupShape<NPL>::kWaves, GroupShape<NPL>::kWgP
 // pieces) into a double-buffered 18 KB stage; wave w computes a rows 16w..
 // against the four column blocks (16 MFMAs per stage), then the screen
 // epilogue.
-// B operand format (WLD_F6_B4): 1 (default) the b codes as fp4 (e2m1) nibbles
-// of minor + 2 major (1.0 / 2.0; 16 B per lane and block), the minor channel
-// by one mask per dword (raw & 0x2222...), accumulators X / Y of the X/Y form
-// (r2_screen_terms_xy2); 0: 6-bit codes read twice, as e2m3 and as e3m2 (the
-// F / G form above, r2_screen_terms_fg; no mask, but 1.5x the B bytes and a
-// slower MFMA: 19.6 against 18.1 cycles in tools/probes/fp6_dual_probe.hip)
-#ifndef WLD_F6_B4
-#define WLD_F6_B4 1
-#endif
-// WLD_F6_BMIN 1 (fp4 B only): each B block in memory is followed by its
-// minor-bit plane (raw & 0x22222222, made once by frag6_kernel), which the
-// tile-pair kernel copies beside it into LDS instead of masking per wave (the
-// four waves of a half read the same B blocks); the single-tile kernel copies
-// only the code blocks and masks as before
-#ifndef WLD_F6_BMIN
-#define WLD_F6_BMIN 0
-#endif
-static_assert(!WLD_F6_BMIN || WLD_F6_B4, "the minor-bit plane is for fp4 B codes");
+// B operand: the b codes as fp4 (e2m1) nibbles of minor + 2 major (1.0 /
+// 2.0; 16 B per lane and block), the minor channel by one mask per dword (raw
+// & 0x2222...), accumulators X / Y (r2_screen_terms_xy2).  (Round 5 measured
+// the alternatives and removed them: 6-bit codes read twice as e2m3 / e3m2,
+// slower per MFMA and 1.5x the B bytes; a minor-bit plane copied into LDS
+// beside B, a larger stage; DESIGN.md Appendix A.)
 constexpr int kF6ABytes = 3072;                         // per 16-site block: A, two channels
-constexpr int kF6BBytes = WLD_F6_B4 ? 1024 : 1536;      // ... and B (its codes; LDS, single-tile kernel)
-constexpr int kF6BMem = kF6BBytes * (WLD_F6_BMIN ? 2 : 1);  // a B block in memory (+ its minor plane)
+constexpr int kF6BBytes = 1024;                         // ... and B (fp4 codes)
 constexpr int kF6AStage = 4 * kF6ABytes;                // a tile's A image per 128 sequences
-constexpr int kF6BStage = 4 * kF6BBytes;                // ... and B image (LDS, single-tile kernel)
-constexpr int kF6BStageMem = 4 * kF6BMem;               // ... B image in memory (and the pair kernel's LDS)
+constexpr int kF6BStage = 4 * kF6BBytes;                // ... and B image
 constexpr int kF6Stage = kF6AStage + kF6BStage;
-constexpr uint32_t kF6Major = 8, kF6Minor = 16;         // 6-bit b codes: e2m3 1.0 / 2.0, e3m2 0.5 / 2.0
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 
 size_t fp6_a_bytes(size_t LP, size_t NP) { return LP / 64 * ((NP + 127) / 128) * kF6AStage; }
-size_t fp6_b_bytes(size_t LP, size_t NP) { return LP / 64 * ((NP + 127) / 128) * kF6BStageMem; }
+size_t fp6_b_bytes(size_t LP, size_t NP) { return LP / 64 * ((NP + 127) / 128) * kF6BStage; }
 
 // one thread per (64-site tile, 128-sequence block, 16-site block, lane)
 __global__ __launch_bounds__(256) void frag6_kernel(const uint8_t *__restrict__ codes, const uint8_t *__restrict__ w6,
@@ -911,7 +896,7 @@ __global__ __launch_bounds__(256) void frag6_kernel(const uint8_t *__restrict__ 
     const uint32_t kb = (uint32_t)(tk % NK);
     const uint8_t *row = codes + (tile * 64 + blk * 16 + (lane & 15)) * (size_t)NP;
     const uint32_t k0 = 128 * kb + 32 * (lane >> 4);
-    uint32_t ai[6] = {0, 0, 0, 0, 0, 0}, am[6] = {0, 0, 0, 0, 0, 0}, b[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t ai[6] = {0, 0, 0, 0, 0, 0}, am[6] = {0, 0, 0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
     for (uint32_t j = 0; j < 32; ++j) {
         const uint32_t k = k0 + j;
         const uint32_t c = k < NP ? row[k] : 0u, v = k < NP ? w6[k] : 0u;
@@ -923,27 +908,16 @@ __global__ __launch_bounds__(256) void frag6_kernel(const uint8_t *__restrict__ 
             ai[d + 1] |= vi >> (32 - o);
             am[d + 1] |= vm >> (32 - o);
         }
-        if (WLD_F6_B4) {  // fp4 nibble j: 0, 2 (1.0: minor), 4 (2.0: major)
-            b[j >> 3] |= ((c & kCodeIn) ? ((c & kCodeMaj) ? 4u : 2u) : 0u) << (4 * (j & 7));
-        } else {
-            const uint32_t vb = (c & kCodeIn) ? ((c & kCodeMaj) ? kF6Major : kF6Minor) : 0u;
-            b[d] |= vb << o;
-            if (o > 26) b[d + 1] |= vb >> (32 - o);
-        }
+        // fp4 nibble j: 0, 2 (1.0: minor), 4 (2.0: major)
+        b[j >> 3] |= ((c & kCodeIn) ? ((c & kCodeMaj) ? 4u : 2u) : 0u) << (4 * (j & 7));
     }
     uint8_t *pa = a6 + tk * kF6AStage + blk * kF6ABytes, *pm = pa + 1536;
-    uint8_t *pb = b6 + tk * kF6BStageMem + blk * kF6BMem;
+    uint8_t *pb = b6 + tk * kF6BStage + blk * kF6BBytes;
     *reinterpret_cast<uint4 *>(pa + 16 * lane) = make_uint4(ai[0], ai[1], ai[2], ai[3]);
     *reinterpret_cast<uint2 *>(pa + 1024 + 8 * lane) = make_uint2(ai[4], ai[5]);
     *reinterpret_cast<uint4 *>(pm + 16 * lane) = make_uint4(am[0], am[1], am[2], am[3]);
     *reinterpret_cast<uint2 *>(pm + 1024 + 8 * lane) = make_uint2(am[4], am[5]);
     *reinterpret_cast<uint4 *>(pb + 16 * lane) = make_uint4(b[0], b[1], b[2], b[3]);
-    if (WLD_F6_BMIN) {
-        constexpr uint32_t kMinor = 0x22222222u;
-        *reinterpret_cast<uint4 *>(pb + 1024 + 16 * lane) =
-            make_uint4(b[0] & kMinor, b[1] & kMinor, b[2] & kMinor, b[3] & kMinor);
-    }
-    if (!WLD_F6_B4) *reinterpret_cast<uint2 *>(pb + 1024 + 8 * lane) = make_uint2(b[4], b[5]);
 }
 
 namespace {
@@ -956,38 +930,17 @@ __device__ __forceinline__ v8i f6_ld24(const uint8_t *p, uint32_t lane) {
     asm volatile("" ::: "memory");
     return v8i{(int)x.x, (int)x.y, (int)x.z, (int)x.w, (int)y.x, (int)y.y, 0, 0};
 }
-// a 16-site block's B operand (either format)
+// a 16-site block's B operand (fp4 codes)
 __device__ __forceinline__ v8i f6_ldb(const uint8_t *p, uint32_t lane) {
-    if constexpr (WLD_F6_B4) {
-        const uint4 x = *reinterpret_cast<const uint4 *>(p + 16 * lane);
-        return v8i{(int)x.x, (int)x.y, (int)x.z, (int)x.w, 0, 0, 0, 0};
-    } else {
-        return f6_ld24(p, lane);
-    }
+    const uint4 x = *reinterpret_cast<const uint4 *>(p + 16 * lane);
+    return v8i{(int)x.x, (int)x.y, (int)x.z, (int)x.w, 0, 0, 0, 0};
 }
 // one B block's four MFMAs against the wave's A channels (in: ai, major: am):
-// acc[channel_a][0 / 1] = X / Y (fp4 B: raw, minor bit) or F / G (6-bit B:
-// e2m3, e3m2 reading)
+// acc[channel_a][0 / 1] = X / Y (B raw: minor + 2 major, B's minor bit)
 __device__ __forceinline__ void f6_block_mfma(v4f (&acc)[2][2], const v8i &ai, const v8i &am, const v8i &b) {
-    constexpr int kOne = 0x7F7F7F7F;  // unit E8M0 block scales
-    if constexpr (WLD_F6_B4) {
-        constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
-        const v8i bmin = {b[0] & kMinor, b[1] & kMinor, b[2] & kMinor, b[3] & kMinor, 0, 0, 0, 0};
-        acc[0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, b, acc[0][0], 2, 4, 0, kOne, 0, kOne);
-        acc[0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc[0][1], 2, 4, 0, kOne, 0, kOne);
-        acc[1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, b, acc[1][0], 2, 4, 0, kOne, 0, kOne);
-        acc[1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, bmin, acc[1][1], 2, 4, 0, kOne, 0, kOne);
-    } else {
-        acc[0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, b, acc[0][0], 2, 2, 0, kOne, 0, kOne);
-        acc[0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, b, acc[0][1], 2, 3, 0, kOne, 0, kOne);
-        acc[1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, b, acc[1][0], 2, 2, 0, kOne, 0, kOne);
-        acc[1][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, b, acc[1][1], 2, 3, 0, kOne, 0, kOne);
-    }
-}
-// ... with the minor-bit plane read from LDS (WLD_F6_BMIN) instead of masked
-[[maybe_unused]] __device__ __forceinline__ void f6_block_mfma2(v4f (&acc)[2][2], const v8i &ai, const v8i &am, const v8i &b,
-                                               const v8i &bmin) {
-    constexpr int kOne = 0x7F7F7F7F;
+    constexpr int kOne = 0x7F7F7F7F;    // unit E8M0 block scales
+    constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
+    const v8i bmin = {b[0] & kMinor, b[1] & kMinor, b[2] & kMinor, b[3] & kMinor, 0, 0, 0, 0};
     acc[0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, b, acc[0][0], 2, 4, 0, kOne, 0, kOne);
     acc[0][1] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, bmin, acc[0][1], 2, 4, 0, kOne, 0, kOne);
     acc[1][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(am, b, acc[1][0], 2, 4, 0, kOne, 0, kOne);
@@ -996,10 +949,7 @@ __device__ __forceinline__ void f6_block_mfma(v4f (&acc)[2][2], const v8i &ai, c
 // t1 of pair e of a B block's accumulators, mlo its smallest marginal
 __device__ __forceinline__ float f6_terms(const v4f (&acc)[2][2], int e, float R2, float thr_c, float E,
                                           float &mlo) {
-    if constexpr (WLD_F6_B4)
-        return r2_screen_terms_xy2(acc[0][0][e], acc[0][1][e], acc[1][0][e], acc[1][1][e], R2, thr_c, E, mlo);
-    else
-        return r2_screen_terms_fg(acc[0][0][e], acc[0][1][e], acc[1][0][e], acc[1][1][e], R2, thr_c, E, mlo);
+    return r2_screen_terms_xy2(acc[0][0][e], acc[0][1][e], acc[1][0][e], acc[1][1][e], R2, thr_c, E, mlo);
 }
 
 // The screen epilogue of one wave's 16 rows x 64 columns (acc[n] = b block n),
@@ -1052,11 +1002,9 @@ struct F6Epi {
 };
 }  // namespace
 
-#ifndef WLD_FP6_WG
-#define WLD_FP6_WG 4  // workgroups per CU
-#endif
-// one 64x64 tile per 4-wave workgroup (WLD_FP6_PAIRS 0)
-__global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const uint8_t *__restrict__ a6,
+// one 64x64 tile per 4-wave workgroup, four per CU (tile lists past 2^15
+// tile columns, and WLD_OPT_FP6_PAIRS_MIN_TILES's smaller lists)
+__global__ __launch_bounds__(256, 4) void pair_fp6_screen_kernel(const uint8_t *__restrict__ a6,
                                                                   const uint8_t *__restrict__ b6,
                                                                   const uint64_t *__restrict__ ok_bits,
                                                                   const uint32_t *__restrict__ tiles, uint32_t n_tiles,
@@ -1073,14 +1021,14 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     const uint32_t tile = ei < n_tiles ? tiles[ei] : kNoTile;
     if (tile == kNoTile) return;  // (uniform: the whole workgroup)
     const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
-    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB = b6 + (size_t)tb * NK * kF6BStageMem;
+    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB = b6 + (size_t)tb * NK * kF6BStage;
     // a stage's 1-KB pieces (A image, then the B code blocks): wave w copies w, w + 4, ...
     auto issue = [&](uint32_t kb, uint32_t buf) {
         const uint32_t gb = lds + buf * kF6Stage;
-        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b = sB + (size_t)kb * kF6BStageMem;
+        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b = sB + (size_t)kb * kF6BStage;
 #pragma unroll
         for (uint32_t p = wave; p < kF6Stage / 1024; p += 4)
-            glds16_s(p < kF6AStage / 1024 ? a + p * 1024 : b + (p - kF6AStage / 1024) * kF6BMem, lane16, gb + p * 1024);
+            glds16_s(p < kF6AStage / 1024 ? a + p * 1024 : b + (p - kF6AStage / 1024) * kF6BBytes, lane16, gb + p * 1024);
     };
     issue(0, 0);
     // the give-up test: read by thread 0 while the first stage is in flight,
@@ -1150,239 +1098,22 @@ __global__ __launch_bounds__(256, WLD_FP6_WG) void pair_fp6_screen_kernel(const 
     }
 }
 
-// Tile pairs (WLD_FP6_PAIRS 1, the default): one 8-wave workgroup per entry
-// of the pair list, tiles (ta, tb) and (ta, tb + 1) (kF6Single: tile (ta, tb)
-// alone), two workgroups per CU.  Both tiles' rows are the same 64 sites, so
-// one A image per stage serves both: per 128 sequences the workgroup copies
-// A (12 KB) and the two B images, 3/4 of the two single tiles' bytes with fp6
-// B and 5/8 with fp4 B — the stage copies, not the MFMAs, bound the
-// single-tile kernel.  Waves 0-3 compute tile tb, waves 4-7
-// tile tb + 1 (the second B image), each as the single-tile kernel's wave;
-// each half decides its own tile.  A single entry's second half computes on
-// the first B image and decides nothing (it keeps the workgroup's barriers).
-// (WLD_F6_PIPE 1: the stage loop with next-stage operands read into registers
-// during this stage's MFMAs; needs ~30 more VGPRs: spills at 4 waves per SIMD)
-#ifndef WLD_F6_PIPE
-#define WLD_F6_PIPE 0
-#endif
 constexpr uint32_t kF6Single = 0x8000u;
-// s_waitcnt immediate (gfx9 encoding): lgkmcnt(0), vmcnt and expcnt at their maxima
-[[maybe_unused]] constexpr int kWaitLgkm0 = 0xC07F;
-constexpr int kF6PStage = kF6AStage + 2 * kF6BStageMem;
-// stage buffers of the tile-pair kernel: 2 (default: one stage in flight while
-// one is computed) or 3 (WLD_F6_RING 3: two stages in flight, counted vmcnt;
-// 120 KB of LDS for the CU's two workgroups)
-#ifndef WLD_F6_RING
-#define WLD_F6_RING 2
-#endif
-static_assert(!WLD_F6_BMIN || (!WLD_F6_PIPE && WLD_F6_RING == 2), "the minor-bit planes: the default stage loop only");
-// waves per SIMD the tile-pair kernel is compiled for: 4 (default, two
-// workgroups per CU, <= 128 VGPRs) or 6 (three per CU, <= 85 VGPRs)
-#ifndef WLD_FP6_PAIR_WPS
-#define WLD_FP6_PAIR_WPS 4
-#endif
-__global__ __launch_bounds__(512, WLD_FP6_PAIR_WPS) void pair_fp6_screen2_kernel(const uint8_t *__restrict__ a6,
-                                                          const uint8_t *__restrict__ b6,
-                                                          const uint64_t *__restrict__ ok_bits,
-                                                          const uint32_t *__restrict__ pairs, uint32_t n_pairs,
-                                                          uint32_t NK, uint32_t L, uint32_t n_chunk_rows, float thr,
-                                                          OrderArgs o, ScreenArgs sc) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[WLD_F6_RING * kF6PStage];
-    __shared__ unsigned long long sMask[2];
-    __shared__ uint32_t sBail, sCand[2];
-    if (!sc.probe && blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t half = wave >> 2, wq = wave & 3, ltid = tid & 255;
-    const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
-    const uint32_t ei = sc.probe ? blockIdx.x * sc.probe_stride + blockIdx.x % sc.probe_stride : blockIdx.x;
-    const uint32_t entry = ei < n_pairs ? pairs[ei] : kNoTile;
-    if (entry == kNoTile) return;  // (uniform: the whole workgroup)
-    const uint32_t ta = entry >> 16, tb0 = entry & 0x7FFFu;
-    const bool single = (entry & kF6Single) != 0, idle = single && half;  // (uniform per wave)
-    const uint32_t tb = tb0 + (idle ? 0u : half);
-    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB0 = b6 + (size_t)tb0 * NK * kF6BStageMem;
-    const uint8_t *sB1 = single ? sB0 : sB0 + (size_t)NK * kF6BStageMem;
-    // a stage's 1-KB pieces (A image, B image of tb, B image of tb + 1): wave w copies w, w + 8, ...
-    auto issue = [&](uint32_t kb, uint32_t buf) {
-        const uint32_t gb = lds + buf * kF6PStage;
-        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b0 = sB0 + (size_t)kb * kF6BStageMem,
-                      *b1 = sB1 + (size_t)kb * kF6BStageMem;
-#pragma unroll
-        for (uint32_t p = wave; p < kF6PStage / 1024; p += 8) {
-            const uint32_t off = p * 1024;
-            glds16_s(off < kF6AStage ? a + off
-                                     : off < kF6AStage + kF6BStageMem ? b0 + (off - kF6AStage)
-                                                                      : b1 + (off - kF6AStage - kF6BStageMem),
-                     lane16, gb + off);
-        }
-    };
-    issue(0, 0);
-    if (tid == 0) {  // the give-up test (as the single-tile kernel)
-        uint32_t v = 0;
-        if (sc.bail) {
-            const unsigned cc = __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v = cc > sc.bail ? ((cc & kAbandonBit) ? 2u : 1u) : 0u;
-        }
-        sBail = v;
-    }
-    if (tid < 2) sCand[tid] = 0u, sMask[tid] = 0ull;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
-    v4f acc[4][2][2];
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int x = 0; x < 2; ++x)
-#pragma unroll
-            for (int y = 0; y < 2; ++y) acc[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-    const uint32_t boff = kF6AStage + (idle ? 0u : half) * kF6BStageMem;  // this half's B image in a stage
-#if WLD_F6_PIPE
-    // The stage loop, software-pipelined: stage kb's operands are in registers
-    // when its MFMAs start (read from LDS during stage kb - 1), so no wave
-    // waits on LDS latency after a barrier; the copies of stage kb + 2 go into
-    // the buffer stage kb was read from (free once every wave has passed the
-    // barrier of stage kb); the copies of stage kb + 1 were issued one stage
-    // earlier and are waited for at stage kb's top.
-    struct Ops {
-        v8i ai, am, b[4];
-    };
-    auto ld_ops = [&](uint32_t buf, Ops &r) {
-        const uint8_t *g = smem + buf * kF6PStage;
-        r.ai = f6_ld24(g + wq * kF6ABytes, lane);
-        r.am = f6_ld24(g + wq * kF6ABytes + 1536, lane);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) r.b[n] = f6_ldb(g + boff + n * kF6BBytes, lane);
-    };
-    Ops r0, r1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of stage 0 landed
-    __builtin_amdgcn_s_barrier();                     // ... and every other wave's
-    asm volatile("" ::: "memory");
-    if (sBail) {  // (uniform) give the pass up: leave
-        if (tid == 0 && sBail == 1) {
-            atomicOr(sc.cand_count, kAbandonBit);
-            atomicOr(sc.cand_buckets, kAbandonBit);
-        }
-        return;
-    }
-    if (NK > 1) issue(1, 1);
-    ld_ops(0, r0);
-    // stage kb (its operands in cur; nxt receives stage kb + 1's)
-    auto stage = [&](uint32_t kb, const Ops &cur, Ops &nxt) {
-        if (kb + 1 < NK) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of stage kb + 1 landed
-            __builtin_amdgcn_s_barrier();                     // ... every wave's; every read of stage kb's buffer done
-            asm volatile("" ::: "memory");
-            if (kb + 2 < NK) issue(kb + 2, kb & 1);
-            ld_ops((kb + 1) & 1, nxt);
-        }
-#pragma unroll
-        for (int n = 0; n < 4; ++n) f6_block_mfma(acc[n], cur.ai, cur.am, cur.b[n]);
-        // stage kb + 1's reads done before the next barrier; as the builtin (not
-        // asm) the compiler sees it, so it puts no wait of its own in front of
-        // the next stage's MFMAs (it would wait for the reads issued there)
-        __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
-    };
-    for (uint32_t kb = 0; kb < NK; kb += 2) {
-        stage(kb, r0, r1);
-        if (kb + 1 < NK) stage(kb + 1, r1, r0);
-    }
-#elif WLD_F6_RING == 3
-    // three buffers, stages kb + 1 and kb + 2 in flight while kb is computed:
-    // at stage kb's top this wave's copies of kb have landed once no more than
-    // its copies of kb + 1 are outstanding (pieces p = wave, wave + 8, wave +
-    // 16 of 20: three for waves 0-3, two for 4-7)
-    if (NK > 1) issue(1, 1);
-    uint32_t buf = 0;
-    for (uint32_t kb = 0; kb < NK; ++kb) {
-        if (kb + 1 < NK) {
-            if (wave < 4)
-                asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();  // every wave's copies of stage kb landed; stage kb - 1's buffer is free
-        asm volatile("" ::: "memory");
-        if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
-            if (tid == 0 && sBail == 1) {
-                atomicOr(sc.cand_count, kAbandonBit);
-                atomicOr(sc.cand_buckets, kAbandonBit);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            return;
-        }
-        if (kb + 2 < NK) issue(kb + 2, buf == 0 ? 2u : buf - 1u);
-        const uint8_t *g = smem + buf * kF6PStage;
-        const v8i ai = f6_ld24(g + wq * kF6ABytes, lane), am = f6_ld24(g + wq * kF6ABytes + 1536, lane);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) f6_block_mfma(acc[n], ai, am, f6_ldb(g + boff + n * kF6BBytes, lane));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
-        buf = buf == 2 ? 0u : buf + 1u;
-    }
-#else
-    uint32_t buf = 0;
-    for (uint32_t kb = 0; kb < NK; ++kb) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of the stage landed
-        __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
-        asm volatile("" ::: "memory");
-        if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
-            if (tid == 0 && sBail == 1) {
-                atomicOr(sc.cand_count, kAbandonBit);
-                atomicOr(sc.cand_buckets, kAbandonBit);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            return;
-        }
-        if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
-        const uint8_t *g = smem + buf * kF6PStage;
-        const v8i ai = f6_ld24(g + wq * kF6ABytes, lane), am = f6_ld24(g + wq * kF6ABytes + 1536, lane);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            if constexpr (WLD_F6_BMIN)
-                f6_block_mfma2(acc[n], ai, am, f6_ldb(g + boff + n * kF6BMem, lane),
-                               f6_ldb(g + boff + n * kF6BMem + 1024, lane));
-            else
-                f6_block_mfma(acc[n], ai, am, f6_ldb(g + boff + n * kF6BMem, lane));
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
-        buf ^= 1;
-    }
-#endif
-    const F6Epi ep{ta, tb, wq, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
-    const bool cand = !idle && ep.any(acc);
-    if (cand) sCand[half] = 1u;  // (benign race: every writer stores 1)
-    __syncthreads();
-    const bool mine = sCand[half] != 0;  // (uniform per half)
-    if (sc.probe) {  // the sample run: count, decide nothing
-        if (ltid == 0 && !idle) {
-            if (mine) atomicAdd(sc.probe, 1u);
-            atomicAdd(sc.probe + 1, 1u);
-        }
-        return;
-    }
-    if (mine && !idle) {
-        const unsigned mk = ep.blocks(acc);
-        if (mk) atomicOr(&sMask[half], (unsigned long long)mk);
-    }
-    __syncthreads();
-    if (!idle) screen_verdict(mine ? (uint32_t)sMask[half] : 0u, ta, tb, ltid, n_chunk_rows, o, sc);
-}
+constexpr int kF6PStage = kF6AStage + 2 * kF6BStage;
 
-// Wide-wave form of the tile-pair screen (WLD_F6_WIDE 1, the default; 0 the
-// eight-wave kernel above): four waves, wave w computing rows 32 (w & 1) ..
-// + 31 (two 16-row blocks) x 64 columns of tile tb + (w >> 1): each B block
-// read and masked once for two A row blocks, so per MFMA half the B reads and
-// masks and 5/7 of the LDS bytes of the eight-wave kernel; 128 accumulator
-// registers per lane (166 VGPRs), three workgroups per CU (the same two 20-KB
-// stage buffers each).  C4 -12%, C5 -10% (profiles/r05ap/).
-#ifndef WLD_F6_WIDE
-#define WLD_F6_WIDE 1
-#endif
-#ifndef WLD_F6_DIAG
-#define WLD_F6_DIAG 0
-#endif
-#if WLD_F6_WIDE
+// Tile pairs: one 4-wave workgroup per entry of the pair list, tiles (ta, tb)
+// and (ta, tb + 1) (kF6Single: tile (ta, tb) alone), three workgroups per CU.
+// Both tiles' rows are the same 64 sites, so one A image per stage serves
+// both: per 128 sequences the workgroup LDS-DMAs A (12 KB) and the two B
+// images (2 x 4 KB) into one of two 20-KB stage buffers.  Wide waves: wave w
+// computes rows 32 (w & 1) .. + 31 (two 16-row blocks) x 64 columns of tile
+// tb + (w >> 1), so each B block is read and masked once for two A row blocks
+// (per MFMA 0.31 KB of LDS reads); 128 accumulator registers per lane.  Each
+// half decides its own tile; a single entry's second half computes on the
+// first B image and decides nothing (it keeps the workgroup's barriers).
+// (Round 5 measured and removed the alternatives: eight waves of 16 x 64,
+// three stage buffers, a producer/consumer split, register-staged operands;
+// DESIGN.md Appendix A.)
 __global__ __launch_bounds__(256, 3) void pair_fp6_screen2w_kernel(const uint8_t *__restrict__ a6,
                                                                   const uint8_t *__restrict__ b6,
                                                                   const uint64_t *__restrict__ ok_bits,
@@ -1402,19 +1133,19 @@ __global__ __launch_bounds__(256, 3) void pair_fp6_screen2w_kernel(const uint8_t
     const uint32_t ta = entry >> 16, tb0 = entry & 0x7FFFu;
     const bool single = (entry & kF6Single) != 0, idle = single && half;  // (uniform per wave)
     const uint32_t tb = tb0 + (idle ? 0u : half);
-    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB0 = b6 + (size_t)tb0 * NK * kF6BStageMem;
-    const uint8_t *sB1 = single ? sB0 : sB0 + (size_t)NK * kF6BStageMem;
+    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB0 = b6 + (size_t)tb0 * NK * kF6BStage;
+    const uint8_t *sB1 = single ? sB0 : sB0 + (size_t)NK * kF6BStage;
     // a stage's 1-KB pieces (A image, B image of tb, B image of tb + 1): wave w copies w, w + 4, ...
     auto issue = [&](uint32_t kb, uint32_t buf) {
         const uint32_t gb = lds + buf * kF6PStage;
-        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b0 = sB0 + (size_t)kb * kF6BStageMem,
-                      *b1 = sB1 + (size_t)kb * kF6BStageMem;
+        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b0 = sB0 + (size_t)kb * kF6BStage,
+                      *b1 = sB1 + (size_t)kb * kF6BStage;
 #pragma unroll
         for (uint32_t p = wave; p < kF6PStage / 1024; p += 4) {
             const uint32_t off = p * 1024;
             glds16_s(off < kF6AStage ? a + off
-                                     : off < kF6AStage + kF6BStageMem ? b0 + (off - kF6AStage)
-                                                                      : b1 + (off - kF6AStage - kF6BStageMem),
+                                     : off < kF6AStage + kF6BStage ? b0 + (off - kF6AStage)
+                                                                      : b1 + (off - kF6AStage - kF6BStage),
                      lane16, gb + off);
         }
     };
@@ -1439,7 +1170,7 @@ __global__ __launch_bounds__(256, 3) void pair_fp6_screen2w_kernel(const uint8_t
             for (int x = 0; x < 2; ++x)
 #pragma unroll
                 for (int y = 0; y < 2; ++y) acc[j][n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-    const uint32_t boff = kF6AStage + (idle ? 0u : half) * kF6BStageMem;  // this half's B image in a stage
+    const uint32_t boff = kF6AStage + (idle ? 0u : half) * kF6BStage;  // this half's B image in a stage
     const uint32_t aoff = 2 * rp * kF6ABytes;                             // this wave's two A row blocks
     uint32_t buf = 0;
     for (uint32_t kb = 0; kb < NK; ++kb) {
@@ -1469,11 +1200,7 @@ __global__ __launch_bounds__(256, 3) void pair_fp6_screen2w_kernel(const uint8_t
     }
     const F6Epi ep0{ta, tb, 2 * rp, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
     const F6Epi ep1{ta, tb, 2 * rp + 1, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
-#if WLD_F6_DIAG  // (timing builds only: the epilogue's share; one compare keeps the MFMAs live)
-    const bool cand = !idle && acc[0][0][0][0][0] + acc[1][3][1][1][3] > 1e30f;
-#else
     const bool cand = !idle && (ep0.any(acc[0]) || ep1.any(acc[1]));
-#endif
     if (cand) sCand[half] = 1u;  // (benign race: every writer stores 1)
     __syncthreads();
     const bool mine = sCand[half] != 0;  // (uniform per half)
@@ -1491,210 +1218,12 @@ __global__ __launch_bounds__(256, 3) void pair_fp6_screen2w_kernel(const uint8_t
     __syncthreads();
     if (!idle) screen_verdict(mine ? (uint32_t)sMask[half] : 0u, ta, tb, ltid, n_chunk_rows, o, sc);
 }
-#endif
-
-// Producer/consumer form of the tile-pair screen (WLD_F6_PC 1, experimental):
-// eight MFMA waves as above plus a ninth that only copies stages into a ring
-// of three LDS buffers.  No stage barrier: the copier publishes each landed
-// stage in an LDS counter (sLoaded) and refills a buffer once all eight MFMA
-// waves' counts of finished stages (sDone) have passed it, so a fast wave runs up to two stages
-// ahead of a slow one instead of meeting it at every stage.  Every wait is
-// bounded: a wave that waits past kPcSpin polls reports kGuardSpin (the host
-// fails the run, no rows) and goes on to the epilogue, whose barriers every
-// wave reaches.
-#ifndef WLD_F6_PC
-#define WLD_F6_PC 0
-#endif
-#if WLD_F6_PC
-constexpr uint32_t kPcSlots = 3, kPcPieces = kF6PStage / 1024, kPcSpin = 1u << 20;
-static_assert(kPcPieces == 20, "the copier's vmcnt immediates count 20 pieces a stage");
-// wait until *ctr >= target (workgroup-uniform value); false past the bound
-__device__ __forceinline__ bool pc_wait(const uint32_t *ctr, uint32_t target) {
-    for (uint32_t n = 0; n < kPcSpin; ++n) {
-        const uint32_t v = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (__builtin_amdgcn_readfirstlane(v) >= target) {
-            asm volatile("" ::: "memory");  // (no LDS read of the stage moves above the poll)
-            return true;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return false;
-}
-// wait until every MFMA wave's count of finished stages (done[0..7]) >= target
-__device__ __forceinline__ bool pc_wait_all(const uint32_t *done, uint32_t target) {
-    for (uint32_t n = 0; n < kPcSpin; ++n) {
-        uint32_t m = ~0u;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            const uint32_t v = __hip_atomic_load(done + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            m = v < m ? v : m;
-        }
-        if (__builtin_amdgcn_readfirstlane(m) >= target) {
-            asm volatile("" ::: "memory");  // (no copy into the freed buffer moves above the poll)
-            return true;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return false;
-}
-__global__ __launch_bounds__(576, 5) void pair_fp6_screen_pc_kernel(const uint8_t *__restrict__ a6,
-                                                                   const uint8_t *__restrict__ b6,
-                                                                   const uint64_t *__restrict__ ok_bits,
-                                                                   const uint32_t *__restrict__ pairs, uint32_t n_pairs,
-                                                                   uint32_t NK, uint32_t L, uint32_t n_chunk_rows,
-                                                                   float thr, OrderArgs o, ScreenArgs sc) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kPcSlots * kF6PStage];
-    __shared__ unsigned long long sMask[2];
-    __shared__ uint32_t sBail, sCand[2], sLoaded, sDone[8];
-    if (!sc.probe && blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool copier = wave == 8;
-    const uint32_t half = copier ? 0u : wave >> 2, wq = wave & 3, ltid = tid & 255;
-    const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
-    const uint32_t ei = sc.probe ? blockIdx.x * sc.probe_stride + blockIdx.x % sc.probe_stride : blockIdx.x;
-    const uint32_t entry = ei < n_pairs ? pairs[ei] : kNoTile;
-    if (entry == kNoTile) return;  // (uniform: the whole workgroup)
-    const uint32_t ta = entry >> 16, tb0 = entry & 0x7FFFu;
-    const bool single = (entry & kF6Single) != 0, idle = single && half;  // (uniform per wave)
-    const bool worker = !copier && !idle;                                 // decides a tile
-    const uint32_t tb = tb0 + (idle ? 0u : half);
-    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB0 = b6 + (size_t)tb0 * NK * kF6BStageMem;
-    const uint8_t *sB1 = single ? sB0 : sB0 + (size_t)NK * kF6BStageMem;
-    // the copier's stage: its 20 1-KB pieces (A image, B image of tb, B image of tb + 1)
-    auto issue = [&](uint32_t kb) {
-        const uint32_t gb = lds + (kb % kPcSlots) * kF6PStage;
-        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b0 = sB0 + (size_t)kb * kF6BStageMem,
-                      *b1 = sB1 + (size_t)kb * kF6BStageMem;
-        // (rolled loops: the copier's addresses stay in a few SGPRs)
-#pragma unroll 1
-        for (uint32_t off = 0; off < kF6AStage; off += 1024) glds16_s(a + off, lane16, gb + off);
-#pragma unroll 1
-        for (uint32_t off = 0; off < kF6BStageMem; off += 1024) {
-            glds16_s(b0 + off, lane16, gb + kF6AStage + off);
-            glds16_s(b1 + off, lane16, gb + kF6AStage + kF6BStageMem + off);
-        }
-    };
-    if (copier)
-        for (uint32_t kb = 0; kb < kPcSlots && kb < NK; ++kb) issue(kb);
-    if (tid == 0) {  // the give-up test (as the single-tile kernel)
-        uint32_t v = 0;
-        if (sc.bail) {
-            const unsigned cc = __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v = cc > sc.bail ? ((cc & kAbandonBit) ? 2u : 1u) : 0u;
-        }
-        sBail = v;
-        sLoaded = 0u;
-    }
-    if (tid < 8) sDone[tid] = 0u;
-    if (tid < 2) sCand[tid] = 0u, sMask[tid] = 0ull;
-    __syncthreads();  // the counters are set before the copier publishes
-    if (sBail) {      // (uniform) give the pass up: the copier drains its copies, every wave leaves
-        if (tid == 0 && sBail == 1) {
-            atomicOr(sc.cand_count, kAbandonBit);
-            atomicOr(sc.cand_buckets, kAbandonBit);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        return;
-    }
-    const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
-    v4f acc[4][2][2];
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int x = 0; x < 2; ++x)
-#pragma unroll
-            for (int y = 0; y < 2; ++y) acc[n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-    bool stalled = false;
-    if (copier) {
-        // publish stage kb once its copies landed (the copies issued after it
-        // may stay in flight: 20 pieces a stage), then refill the buffer of
-        // stage kb - 1 with stage kb + 2 once every MFMA wave freed it
-        for (uint32_t kb = 0; kb < NK && !stalled; ++kb) {
-            const uint32_t last = kb == 0 ? (NK - 1 < 2u ? NK - 1 : 2u) : (NK - 1 < kb + 1 ? NK - 1 : kb + 1);
-            const uint32_t after = last - kb;  // stages in flight behind kb (0, 1 or 2)
-            if (after == 2)
-                asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-            else if (after == 1)
-                asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) __hip_atomic_store(&sLoaded, kb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (kb >= 1 && kb + 2 < NK) {
-                if (!pc_wait_all(sDone, kb)) {
-                    stalled = true;
-                    break;
-                }
-                issue(kb + 2);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing in flight when the workgroup ends
-    } else {
-        const uint32_t boff = kF6AStage + (idle ? 0u : half) * kF6BStageMem;  // this half's B image in a stage
-        for (uint32_t kb = 0; kb < NK; ++kb) {
-            if (!pc_wait(&sLoaded, kb + 1)) {
-                stalled = true;
-                break;
-            }
-            const uint8_t *g = smem + (kb % kPcSlots) * kF6PStage;
-            const v8i ai = f6_ld24(g + wq * kF6ABytes, lane), am = f6_ld24(g + wq * kF6ABytes + 1536, lane);
-#pragma unroll
-            for (int n = 0; n < 4; ++n) f6_block_mfma(acc[n], ai, am, f6_ldb(g + boff + n * kF6BBytes, lane));
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the buffer done
-            // (every lane stores the same word: no branch the MFMAs could sink past)
-            __hip_atomic_store(&sDone[wave], kb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    }
-    if (stalled && lane == 0) report_guard(o, kGuardSpin);
-    const F6Epi ep{ta, tb, wq, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
-    const bool cand = worker && ep.any(acc);
-    if (cand) sCand[half] = 1u;  // (benign race: every writer stores 1)
-    __syncthreads();
-    const bool mine = sCand[half] != 0;  // (uniform per half)
-    if (sc.probe) {  // the sample run: count, decide nothing
-        if (ltid == 0 && worker) {
-            if (mine) atomicAdd(sc.probe, 1u);
-            atomicAdd(sc.probe + 1, 1u);
-        }
-        return;
-    }
-    if (mine && worker) {
-        const unsigned mk = ep.blocks(acc);
-        if (mk) atomicOr(&sMask[half], (unsigned long long)mk);
-    }
-    __syncthreads();
-    if (worker) screen_verdict(mine ? (uint32_t)sMask[half] : 0u, ta, tb, ltid, n_chunk_rows, o, sc);
-}
-#endif
 
 void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b6,
                   hipStream_t s) {
     const size_t n = LP / 16 * ((NP + 127) / 128) * 64;
     hipLaunchKernelGGL(frag6_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, codes, w6, (uint32_t)LP,
                        (uint32_t)NP, a6, b6);
-}
-
-#ifndef WLD_FP6_PAIRS
-#define WLD_FP6_PAIRS 1
-#endif
-bool fp6_uses_pairs() { return WLD_FP6_PAIRS != 0; }
-
-// The pair list of a tile list (sorted by (ta, tb)): tiles (ta, tb) and (ta,
-// tb + 1) with tb even form an entry ta << 16 | tb; any other tile is an entry
-// of its own (kF6Single set).  Within a 256-site chunk row the pairs never
-// cross a chunk (four tiles per chunk).  Returned in the tile list's order of
-// first tiles.
-std::vector<uint32_t> fp6_pair_list(const std::vector<uint32_t> &sorted_tiles) {
-    std::vector<uint32_t> out;
-    for (size_t i = 0; i < sorted_tiles.size(); ++i) {
-        const uint32_t t = sorted_tiles[i];
-        if ((t & 1u) == 0 && i + 1 < sorted_tiles.size() && sorted_tiles[i + 1] == t + 1) {
-            out.push_back(t);
-            ++i;
-        } else {
-            out.push_back(t | kF6Single);
-        }
-    }
-    return out;
 }
 
 // Site-major variant (one tile per workgroup, codes read straight into
@@ -1849,21 +1378,9 @@ void fp6_screen_args(const MfmaLaunch &m, ScreenArgs &sc) {
 // sc.probe every stride-th one
 void launch_fp6_screen(const MfmaLaunch &m, const uint64_t *ok_bits, const OrderArgs &o, const ScreenArgs &sc,
                        uint32_t stride, hipStream_t s) {
-    if (fp6_uses_pairs() && m.f6_pairs) {
+    if (m.f6_pairs) {
         // (a tile pair per workgroup, the XCD-ordered pair list)
-#if WLD_F6_PC
-        hipLaunchKernelGGL(pair_fp6_screen_pc_kernel, dim3((m.f6_n_pairs + stride - 1) / stride), dim3(576), 0, s,
-                           m.fp6->a6, m.fp6->b6, ok_bits, m.f6_pairs, m.f6_n_pairs, m.fp6->NK, m.L, m.n_chunk_rows,
-                           m.thr, o, sc);
-        return;
-#endif
-#if WLD_F6_WIDE
         hipLaunchKernelGGL(pair_fp6_screen2w_kernel, dim3((m.f6_n_pairs + stride - 1) / stride), dim3(256), 0, s,
-                           m.fp6->a6, m.fp6->b6, ok_bits, m.f6_pairs, m.f6_n_pairs, m.fp6->NK, m.L, m.n_chunk_rows,
-                           m.thr, o, sc);
-        return;
-#endif
-        hipLaunchKernelGGL(pair_fp6_screen2_kernel, dim3((m.f6_n_pairs + stride - 1) / stride), dim3(512), 0, s,
                            m.fp6->a6, m.fp6->b6, ok_bits, m.f6_pairs, m.f6_n_pairs, m.fp6->NK, m.L, m.n_chunk_rows,
                            m.thr, o, sc);
     } else {

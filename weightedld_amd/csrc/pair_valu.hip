@@ -587,25 +587,13 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
 #ifndef WLD_REF_ITEML_WG
 #define WLD_REF_ITEML_WG 4  // ... the candidate loop (its loop state: <= 128 VGPRs)
 #endif
-#ifndef WLD_ITEM_DIAG
-#define WLD_ITEM_DIAG 0  // diagnostic builds only (tools/build_variant.sh): 1 no compaction, 2 no epilogue
-#endif
-// WLD_ITEM_TRACE (diagnostic builds only): the full-run item kernel records,
-// per wave, {HW_ID | XCC_ID << 32, start, sums done, end} (wall_clock64, 100
-// MHz) of its last launch; wld_diag_item_trace copies them out
-// (tools/item_trace.py)
-#ifndef WLD_ITEM_TRACE
-#define WLD_ITEM_TRACE 0
-#endif
 // Full runs (not LOOP) load each stage's operands at its top instead of one
 // stage ahead: 70 instead of 96 VGPRs, six workgroups per CU instead of five,
 // and the co-resident waves cover the latency (C2 -2.5%, profiles/r05v/; the
 // matrix pipe fills only with many waves in their sums).  The
 // candidate loop keeps the prefetch (four workgroups per CU either way).
-#ifndef WLD_ITEM_NOPF
-#define WLD_ITEM_NOPF 1
-#endif
-// WLD_ITEM_ASHARE 1 (full runs): the four waves of an item share its 16 rows,
+constexpr bool kItemNoPrefetch = true;
+// kItemAShare (full runs): the four waves of an item share its 16 rows,
 // so each forms the A operands (w x in, w x major) of one 16-position group of
 // a stage and writes them to LDS, and every wave reads all four: a quarter of
 // the A-side converts and products per wave.  The f32 MFMA runs on the same
@@ -613,13 +601,7 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
 // ~1.5x the cycles per MFMA with the item's operand work beside it, even at
 // eight waves per SIMD), so vector instructions cost MFMA throughput directly.
 // C2 0.1184 -> 0.1114 ms (profiles/r05ad/; rows bit-identical, 191 tests).
-#ifndef WLD_ITEM_ASHARE
-#define WLD_ITEM_ASHARE 1
-#endif
-#if WLD_ITEM_TRACE
-constexpr uint32_t kTraceWaves = 65536;
-__device__ unsigned long long g_item_trace[kTraceWaves * 4];
-#endif
+constexpr bool kItemAShare = true;
 template <bool LOOP>
 __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) void ref_item_kernel(
     const uint8_t *__restrict__ rcodes, const float *__restrict__ rw, const uint8_t *__restrict__ site_ok,
@@ -630,16 +612,12 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
     __shared__ uint32_t sRowBase[kTile];
     // (full runs only: a candidate item may pack sub-blocks of several row
     // blocks, whose waves need different A operands)
-    constexpr bool kAShare = WLD_ITEM_ASHARE && !LOOP;
+    constexpr bool kAShare = kItemAShare && !LOOP;
     // (kAShare) two stages of A operands: [stage & 1][group][element][lane] (u, v)
     __shared__ float2 sAop[kAShare ? 2 * 16 * 64 : 1];
     const uint32_t tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-#if WLD_ITEM_TRACE
-    const unsigned long long t_start = wall_clock64();
-    unsigned long long t_sums = 0;
-#endif
     auto compute_item = [&](uint32_t tile, uint32_t bits, uint32_t owned) {
         const uint32_t ta = tile >> 16, tb = tile & 0xFFFFu;
         const uint32_t a0 = ta * kTile, b0 = tb * kTile;
@@ -695,8 +673,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                 cw[2].x = __uint_as_float(b8.x);
                 cw[2].y = __uint_as_float(b8.y);
             };
-            constexpr bool kNoPrefetch = WLD_ITEM_NOPF && !LOOP;
-#if WLD_ITEM_ASHARE
+            constexpr bool kNoPrefetch = kItemNoPrefetch && !LOOP;
             if constexpr (kAShare) {
                 // this wave's share: group `wave` of each stage (rows of the item's
                 // row block, lane (r, g) its row r, elements 4 e + g)
@@ -755,9 +732,7 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                             for (int q = 0; q < 4; ++q) tot[e][q] += acc[q][e];
                     }
                 }
-            } else
-#endif
-            {
+            } else {
             if (n_st && !kNoPrefetch) fetch(0);
             v4f acc[4];
             uint32_t in_cls = 0;  // this stage's index in its class (no modulo in the loop)
@@ -836,23 +811,6 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
             }
         }
         // ---- epilogue (lib.rs:482-520, 660) --------------------------------
-#if WLD_ITEM_TRACE
-        t_sums = wall_clock64();
-#endif
-#if WLD_ITEM_DIAG & 2  // diagnostic build (timing only): the sums, no epilogue, nothing stored
-        {
-            float keep = 0.0f;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) keep += tot[e][q];
-            asm volatile("" ::"v"(keep), "v"(okA4), "v"(okB));
-            if (tid < kTile && ((owned >> (tid >> 4)) & 1u)) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
-            __syncthreads();
-            if (tid == 0) tile_done(o, ta, tb, n_chunk_rows, (uint32_t)__popc(owned));
-            return;
-        }
-#endif
         uint32_t passmask = 0;  // bit e
         float res[4][3];
 #pragma unroll
@@ -868,15 +826,6 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
         // ---- compaction: the tile's 64x64 pass bits, rows in b order ---------
         const bool own_row = tid < kTile && ((owned >> (tid >> 4)) & 1u);
         const uint32_t quarters = (uint32_t)__popc(owned);
-#if WLD_ITEM_DIAG & 1  // diagnostic build (timing only): the epilogue, no compaction, nothing stored
-        {
-            float keep = 0.0f;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) keep += res[e][0] + res[e][1] + res[e][2];
-            asm volatile("" ::"v"(passmask), "v"(keep));
-            passmask = 0;
-        }
-#endif
         if (!__syncthreads_or(passmask != 0)) {
             if (own_row) o.seg_cnt[(size_t)(a0 + tid) * o.T + tb] = 0;
             if (tid == 0) tile_done(o, ta, tb, n_chunk_rows, quarters);
@@ -929,18 +878,6 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
         const uint32_t cols = (tile >> 16) == (tile & 0xFFFFu) ? 0xFu & ~((1u << q) - 1u) : 0xFu;
         if (tile != kNoTile) compute_item(tile, cols << (4 * q), 1u << q);  // kNoTile: padding of an XCD-ordered list
         scan_tail(sa, gridDim.x);  // (every workgroup takes a ticket when the scan is fused)
-#if WLD_ITEM_TRACE
-        const size_t wi = (size_t)blockIdx.x * 4 + wave;
-        if (lane == 0 && wi < kTraceWaves) {
-            unsigned hw, xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            g_item_trace[4 * wi] = hw | (unsigned long long)xcc << 32;
-            g_item_trace[4 * wi + 1] = t_start;
-            g_item_trace[4 * wi + 2] = t_sums;
-            g_item_trace[4 * wi + 3] = wall_clock64();
-        }
-#endif
     } else {
         // the screen's items, heaviest bucket first; the first by workgroup id
         // (rounds dealt in snake order, heavy beside light on a CU), the next
@@ -1242,15 +1179,3 @@ bool launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
 }
 
 }  // namespace wld
-
-#if WLD_ITEM_TRACE
-extern "C" int wld_diag_item_trace(unsigned long long *out, size_t n_words, int reset) {
-    if (reset) {
-        void *p = nullptr;
-        if (hipGetSymbolAddress(&p, HIP_SYMBOL(wld::g_item_trace)) != hipSuccess) return -1;
-        return hipMemset(p, 0, sizeof(wld::g_item_trace)) == hipSuccess ? 0 : -1;
-    }
-    n_words = n_words < sizeof(wld::g_item_trace) / 8 ? n_words : sizeof(wld::g_item_trace) / 8;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(wld::g_item_trace), n_words * 8) == hipSuccess ? 0 : -1;
-}
-#endif

@@ -56,7 +56,8 @@ inline std::vector<uint32_t> range_tiles(uint32_t n, uint32_t T_used, uint32_t l
 // per first pass of a context: profiles/r05o/trace_first).
 // Entries may carry flag bits outside `key` (the tile-pair list's single
 // flag): they ride along, the order is the keyed tiles'.
-std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t, uint32_t kS, uint32_t key = ~0u) {
+inline uint32_t super_block_side(uint32_t NP) { return 24ull * 64 * NP <= (4ull << 20) ? 16u : 8u; }
+inline std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t, uint32_t kS, uint32_t key = ~0u) {
     constexpr uint32_t kX = 8;
     std::vector<uint32_t> sorted(t);
     auto keyed_less = [key](uint32_t x, uint32_t y) { return (x & key) < (y & key); };
@@ -110,7 +111,24 @@ std::vector<uint32_t> xcd_order(const std::vector<uint32_t> &t, uint32_t kS, uin
     return out;
 }
 
-// 64x64 tiles (tb >= ta) of the chunks [lb, le), sorted (ta, tb) so a row of
-// tiles shares its A columns in L2 as in a whole-row run
+// The fp6 screen's pair list of a tile list (sorted by (ta, tb)): tiles (ta,
+// tb) and (ta, tb + 1) with tb even form an entry ta << 16 | tb; any other
+// tile is an entry of its own (kSingleEntry set).  Within a 256-site chunk
+// row the pairs never cross a chunk (four tiles per chunk).  Returned in the
+// tile list's order of first tiles.
+constexpr uint32_t kSingleEntry = 0x8000u;  // (= pair_mfma.hip kF6Single)
+inline std::vector<uint32_t> fp6_pair_list(const std::vector<uint32_t> &sorted_tiles) {
+    std::vector<uint32_t> out;
+    for (size_t i = 0; i < sorted_tiles.size(); ++i) {
+        const uint32_t t = sorted_tiles[i];
+        if ((t & 1u) == 0 && i + 1 < sorted_tiles.size() && sorted_tiles[i + 1] == t + 1) {
+            out.push_back(t);
+            ++i;
+        } else {
+            out.push_back(t | kSingleEntry);
+        }
+    }
+    return out;
+}
 }  // namespace tile_order
 }  // namespace wld

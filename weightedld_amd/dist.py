@@ -167,9 +167,16 @@ class ShardStep:
         # profiles/r04i/: the context was destroyed by its finalizer at
         # interpreter shutdown, in no set order against the torch event and
         # pinned-memory block recorded on the stream it destroyed.)
+        # One stream per context: a second step object on the same context
+        # (the bench's ShardStep beside its PipelinedShardStep) reuses the
+        # stream the first bound, so every step on that context, its count
+        # collective and its pinned copy stay ordered on one stream.
         if device.type == "cuda":
-            self.stream = torch.cuda.Stream(device=device)
-            ctx.set_stream(self.stream.cuda_stream)
+            self.stream = getattr(ctx, "_shard_step_stream", None)
+            if self.stream is None:
+                self.stream = torch.cuda.Stream(device=device)
+                ctx.set_stream(self.stream.cuda_stream)
+                ctx._shard_step_stream = self.stream
         else:
             self.stream = _HostStream()
         self.rows_seen = False  # some rank had rows in the last finished step
@@ -270,6 +277,7 @@ class PipelinedShardStep:
         self.serialize = serialize_kernels  # False: step i's kernel may start in step i-1's tail
         self.i = 0
         self.pending = collections.deque()  # contexts of the enqueued, unfinished steps, oldest first
+        self.recorded = [False] * len(ctxs)  # done[k] recorded after context k's latest enqueued step
 
     def submit(self, thr, chunk_begin, chunk_end):
         D = len(self.steps)
@@ -278,6 +286,12 @@ class PipelinedShardStep:
         if self.pending:
             prev = self.pending[-1]
             if any(st.rows_seen for st in self.steps) or (self.serialize and self.serialize != "pair"):
+                if not self.recorded[prev]:
+                    # prev was enqueued without its end event (no rank had
+                    # rows then); nothing has been queued on its stream since,
+                    # so a record now marks exactly the end of prev's step
+                    self.done[prev].record(self.steps[prev].stream)
+                    self.recorded[prev] = True
                 self.steps[k].stream.wait_event(self.done[prev])
             elif self.serialize == "pair":
                 self.steps[k].ctx.run_after(self.steps[prev].ctx)
@@ -287,6 +301,7 @@ class PipelinedShardStep:
         # step in the common case
         need_done = self.serialize is True or any(st.rows_seen for st in self.steps)
         self.steps[k].enqueue(thr, chunk_begin, chunk_end, self.done[k] if need_done else None)
+        self.recorded[k] = need_done
         self.i += 1
         self.pending.append(k)
         return self.steps[self.pending.popleft()].finish() if len(self.pending) > D - 1 else None
