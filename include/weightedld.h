@@ -231,6 +231,13 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
  *                      per workgroup (one shared A operand stream) when the
  *                      run's tile list has at least this many tiles (default
  *                      0: always), else one tile per workgroup.  Same rows.
+ *   WLD_OPT_I8_PAIRS   1 (default): the i8 one-plane screen (nonnegative
+ *                      weights, at most 16,384 sequences) runs on the fp6
+ *                      screen's tile-pair list with wide waves, its operands
+ *                      (the top weight digit times the site indicators, and
+ *                      the codes) pre-multiplied once per load (3 bytes per
+ *                      site and sequence); 0: one tile per workgroup, the
+ *                      operands formed per stage.  Same rows.
  *   WLD_OPT_TEST_GUARD 0 (default); 1 (tests only): before each candidate
  *                      launch the last candidate bucket's count is set one
  *                      past its capacity, so the launch meets an entry outside
@@ -252,6 +259,7 @@ int wld_set_kernel(wld_ctx *ctx, int kernel);
 #define WLD_OPT_SCREEN_FP6 13
 #define WLD_OPT_TEST_GUARD 14
 #define WLD_OPT_FP6_PAIRS_MIN_TILES 15
+#define WLD_OPT_I8_PAIRS 16
 int wld_set_option(wld_ctx *ctx, int option, int64_t value);
 int wld_get_option(wld_ctx *ctx, int option, int64_t *value);
 

@@ -26,7 +26,7 @@ KERNEL_AUTO, KERNEL_VALU, KERNEL_MFMA = 0, 1, 2
 # wld_set_option ids (include/weightedld.h)
 OPTIONS = {"prefilter": 1, "screen": 2, "tile_order": 3, "all_planes": 4, "mfma_layout": 5, "valu_plain": 6,
            "staging_rows": 7, "host_batch_pairs": 8, "ref_sums": 11, "fused_scan": 12, "screen_fp6": 13,
-           "test_guard": 14, "fp6_pairs_min_tiles": 15}
+           "test_guard": 14, "fp6_pairs_min_tiles": 15, "i8_pairs": 16}
 
 
 class WldError(RuntimeError):

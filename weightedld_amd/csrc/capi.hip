@@ -137,6 +137,7 @@ struct wld_ctx {
     // pairs and the 1/8 shard is even within noise (profiles/r05x); C5 pairs
     // 4.8% faster (profiles/r05j)
     int64_t opt_fp6_pairs_min = 0;  // (tile pairs at every list size: profiles/r05ar/)
+    bool opt_i8_pairs = true;    // WLD_OPT_I8_PAIRS: the i8 screen on tile pairs (pre-multiplied images)
     int opt_fp6 = 1;             // WLD_OPT_SCREEN_FP6: 0 off, 1 auto, 2 whenever it applies, 3 auto without the sample run
     bool opt_ref_sums = true;  // WLD_OPT_REF_SUMS: lib.rs's own f32 summation order (default)
     uint64_t opt_staging_rows = 1ull << 25, opt_host_batch_pairs = 1ull << 31;
@@ -149,6 +150,11 @@ struct wld_ctx {
     // the fp6 screen (fp6_prepare): weight codes, packed operands, constants
     DevBuf w6, f6a, f6b;
     Fp6Screen f6{};
+    // the i8 one-plane screen's pre-multiplied images (i8img_prepare, at the
+    // first pass that screens on i8 with them)
+    DevBuf i8a, i8b;
+    I8Screen i8s{};
+    bool i8img_ok = false;
     bool fp6_tried = false;   // fp6_prepare ran for this load
     bool fp6_sampled = false; // this pass's screen was chosen by a sample run (fp6_sample)
     bool fp6_ok = false;      // operands built for this load (the weights allow it)
@@ -208,7 +214,7 @@ struct wld_ctx {
         // work queued on a borrowed stream (wld_set_stream) may still use the
         // buffers: it completes before they are freed
         if (stream && stream != own_stream) (void)hipStreamSynchronize(stream);
-        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &rcodes, &rw, &w6, &f6a, &f6b, &tiles, &cand, &f6_pairs, &fp6_probe_buf,
+        DevBuf *all[] = {&keep, &htab, &htab_kept, &site_index, &raw, &wraw, &codes, &w_pad, &wstats, &site_ok, &site_map, &planes, &frag, &rcodes, &rw, &w6, &f6a, &f6b, &i8a, &i8b, &tiles, &cand, &f6_pairs, &fp6_probe_buf,
                          &seg_cnt, &seg_off, &chunk_total, &chunk_base, &counters, &chunk_left, &prog_n, &st_a, &st_b, &st_d,
                          &st_dp, &st_r2, &out_a, &out_b, &out_d, &out_dp, &out_r2};
         for (DevBuf *b : all) release(*b);
@@ -342,6 +348,24 @@ int fp6_prepare(wld_ctx *c) {
     return WLD_OK;
 }
 
+// The i8 screen's pre-multiplied operand images of this load (pair_mfma.hip
+// pair_i8_screen2w_kernel): the top nonzero digit plane times the site
+// indicators, and the codes, 3 bytes per site and sequence; built on the
+// context's stream at the first pass that screens on i8 with them.
+int i8img_prepare(wld_ctx *c) {
+    uint32_t top = 0;
+    for (uint32_t p = 0; p < 4; ++p)
+        if (c->plane_mask >> p & 1) top = p;
+    WLD_TRY(ensure(c->i8a, i8_a_bytes(c->LP, c->NP)));
+    WLD_TRY(ensure(c->i8b, i8_b_bytes(c->LP, c->NP)));
+    launch_i8img(ptr<uint8_t>(c->codes), ptr<int8_t>(c->planes) + (size_t)top * c->NP, c->LP, c->NP,
+                 ptr<uint8_t>(c->i8a), ptr<uint8_t>(c->i8b), c->stream);
+    HIP_TRY(hipGetLastError());
+    c->i8s = I8Screen{ptr<uint8_t>(c->i8a), ptr<uint8_t>(c->i8b), top};
+    c->i8img_ok = true;
+    return WLD_OK;
+}
+
 int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le);
 int ensure_ref_layout(wld_ctx *c);
 uint32_t chunks_of(size_t L);
@@ -444,6 +468,7 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     c->plane_mask = c->kernel == WLD_KERNEL_MFMA && !c->opt_all_planes ? c->wst.plane_mask : all_planes;
     c->stats.load_ms = event_ms(c->ev[0], c->ev[1]);
     c->fp6_ok = c->fp6_better = c->fp6_tried = false;  // (fp6_prepare: at the first run that may use it)
+    c->i8img_ok = false;  // (i8img_prepare: at the first pass that screens on i8)
     c->stats.mfma_planes = c->kernel == WLD_KERNEL_MFMA ? __builtin_popcount(c->plane_mask) : 0;
     c->stats.kernel = c->kernel;
     c->stats.weight_shift = c->shift;
@@ -546,7 +571,7 @@ int build_tiles(wld_ctx *c, uint32_t lb, uint32_t le) {
     std::vector<uint32_t> pl;
     if (T_used <= 0x7FFF && (int64_t)t.size() >= c->opt_fp6_pairs_min) {
         pl = tile_order::fp6_pair_list(t);
-        if (!c->opt_tile_rows && pl.size() >= 2048) pl = xcd_order(pl, kS, ~0x8000u);
+        if (!c->opt_tile_rows && pl.size() >= 2048) pl = xcd_order(pl, kS, ~tile_order::kSingleEntry);
     }
     // only with many rounds of resident tiles: whole super-blocks per XCD
     // leave up to one super-block of imbalance (C2's 528 tiles: +14%)
@@ -697,6 +722,13 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         m.fp6_bail = fp6_auto && !c->prog_pass && !c->pend.count_out ? std::max<uint32_t>(c->n_tiles / 16, 1) : 0;
         m.f6_pairs = c->f6_n_pairs ? ptr<uint32_t>(c->f6_pairs) : nullptr;
         m.f6_n_pairs = c->f6_n_pairs;
+        // the i8 one-plane screen on tile pairs (WLD_OPT_I8_PAIRS): its images
+        // built at the first pass that needs them
+        if (!dense && m.prefilter && m.screen && !m.screen2 && !m.fp6 && c->opt_i8_pairs && c->f6_n_pairs &&
+            c->use_frag && c->wst.nonneg && c->NP <= 16384) {
+            if (!c->i8img_ok) WLD_TRY(i8img_prepare(c));
+            m.i8img = &c->i8s;
+        }
         for (int p = 0; p < 4; ++p) m.dsum[p] = c->wst.dsum[p];
         m.cand_list = ptr<uint32_t>(c->cand);
         // this pass's candidate set (the scan zeroes the other one, enqueue_pass)
@@ -856,6 +888,7 @@ int wld_set_option(wld_ctx *c, int option, int64_t value) {
             c->opt_host_batch_pairs = (uint64_t)value;
             break;
         case WLD_OPT_FUSED_SCAN: c->opt_fused_scan = value != 0; break;
+        case WLD_OPT_I8_PAIRS: c->opt_i8_pairs = value != 0; break;
         case WLD_OPT_TEST_GUARD: c->opt_test_guard = value != 0; break;
         case WLD_OPT_FP6_PAIRS_MIN_TILES:
             if (value < 0) return fail(WLD_E_ARG, "WLD_OPT_FP6_PAIRS_MIN_TILES must be >= 0");
@@ -889,6 +922,7 @@ int wld_get_option(wld_ctx *c, int option, int64_t *value) {
         case WLD_OPT_TEST_GUARD: *value = c->opt_test_guard; break;
         case WLD_OPT_FP6_PAIRS_MIN_TILES: *value = c->opt_fp6_pairs_min; break;
         case WLD_OPT_SCREEN_FP6: *value = c->opt_fp6; break;
+        case WLD_OPT_I8_PAIRS: *value = c->opt_i8_pairs; break;
         default: return fail(WLD_E_ARG, "unknown option %d", option);
     }
     return WLD_OK;

@@ -221,6 +221,19 @@ size_t fp6_b_bytes(size_t LP, size_t NP);
 void launch_frag6(const uint8_t *codes, const uint8_t *w6, size_t LP, size_t NP, uint8_t *a6, uint8_t *b6,
                   hipStream_t s);
 
+// The i8 one-plane screen's pre-multiplied operand images (pair_mfma.hip
+// pair_i8_screen2w_kernel; capi.hip i8img_prepare): A = the top weight digit
+// times in / major, B = the codes, per 64-site tile and 64-sequence block.
+struct I8Screen {
+    const uint8_t *a8, *b8;
+    uint32_t digit_plane;  // the digit plane the images hold
+};
+size_t i8_a_bytes(size_t LP, size_t NP);
+size_t i8_b_bytes(size_t LP, size_t NP);
+// digit: NP int8 digits of the plane (planes + plane * NP)
+void launch_i8img(const uint8_t *codes, const int8_t *digit, size_t LP, size_t NP, uint8_t *a8, uint8_t *b8,
+                  hipStream_t s);
+
 struct MfmaLaunch {
     const uint8_t *codes;   // site-major codes (used when frag is null)
     const uint8_t *frag;    // fragment-major selector-coded copy (LDS kernel), or null
@@ -263,6 +276,9 @@ struct MfmaLaunch {
     // ... its tile-pair list (pair_fp6_screen2w_kernel; XCD-ordered, kNoTile padded)
     const uint32_t *f6_pairs;
     uint32_t f6_n_pairs;
+    // the i8 one-plane screen on the tile-pair list with pre-multiplied
+    // operands (null: the per-tile LDS kernel)
+    const I8Screen *i8img = nullptr;
 };
 // The fp6 screen's sample run over every stride-th entry of its list: probe[0]
 // = the sampled tiles holding a pair its bound cannot reject, probe[1] = the

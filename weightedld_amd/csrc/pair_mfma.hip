@@ -937,8 +937,14 @@ __device__ __forceinline__ v8i f6_ldb(const uint8_t *p, uint32_t lane) {
 }
 // one B block's four MFMAs against the wave's A channels (in: ai, major: am):
 // acc[channel_a][0 / 1] = X / Y (B raw: minor + 2 major, B's minor bit)
+// Zero scale operands: the compiler selects the unscaled
+// v_mfma_f32_16x16x128_f8f6f4 (no per-block scales), whose sums equal the
+// unit-scaled (E8M0 0x7F) v_mfma_scale form's bit for bit and which issues
+// faster: 17.5 / 16.7 / 16.5 against 19.5 / 17.3 / 17.0 cycles per
+// instruction at 1 / 2 / 3 waves per SIMD (tools/probes/fp6_unscaled_probe.hip);
+// screen C4 -4.1%, 1/8 shard -4.8% (profiles/r06c/).
 __device__ __forceinline__ void f6_block_mfma(v4f (&acc)[2][2], const v8i &ai, const v8i &am, const v8i &b) {
-    constexpr int kOne = 0x7F7F7F7F;    // unit E8M0 block scales
+    constexpr int kOne = 0;
     constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
     const v8i bmin = {b[0] & kMinor, b[1] & kMinor, b[2] & kMinor, b[3] & kMinor, 0, 0, 0, 0};
     acc[0][0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(ai, b, acc[0][0], 2, 4, 0, kOne, 0, kOne);
@@ -1098,28 +1104,29 @@ __global__ __launch_bounds__(256, 4) void pair_fp6_screen_kernel(const uint8_t *
     }
 }
 
-constexpr uint32_t kF6Single = 0x8000u;
-constexpr int kF6PStage = kF6AStage + 2 * kF6BStage;
+constexpr uint32_t kF6Single = 0x8000u;  // (= tile_order::kSingleEntry)
 
 // Tile pairs: one 4-wave workgroup per entry of the pair list, tiles (ta, tb)
 // and (ta, tb + 1) (kF6Single: tile (ta, tb) alone), three workgroups per CU.
 // Both tiles' rows are the same 64 sites, so one A image per stage serves
 // both: per 128 sequences the workgroup LDS-DMAs A (12 KB) and the two B
-// images (2 x 4 KB) into one of two 20-KB stage buffers.  Wide waves: wave w
-// computes rows 32 (w & 1) .. + 31 (two 16-row blocks) x 64 columns of tile
+// images (2 x 4 KB) into one of two 20-KB stage buffers, each wave five 1-KB
+// pieces from bases set once (round 6: C4 -5%, C5 -3%, 1/8 shard -6% against
+// selecting each piece's source per stage, profiles/r06b/).  Wide waves: wave
+// w computes rows 32 (w & 1) .. + 31 (two 16-row blocks) x 64 columns of tile
 // tb + (w >> 1), so each B block is read and masked once for two A row blocks
 // (per MFMA 0.31 KB of LDS reads); 128 accumulator registers per lane.  Each
 // half decides its own tile; a single entry's second half computes on the
 // first B image and decides nothing (it keeps the workgroup's barriers).
-// (Round 5 measured and removed the alternatives: eight waves of 16 x 64,
-// three stage buffers, a producer/consumer split, register-staged operands;
-// DESIGN.md Appendix A.)
-__global__ __launch_bounds__(256, 3) void pair_fp6_screen2w_kernel(const uint8_t *__restrict__ a6,
-                                                                  const uint8_t *__restrict__ b6,
-                                                                  const uint64_t *__restrict__ ok_bits,
-                                                                  const uint32_t *__restrict__ pairs, uint32_t n_pairs,
-                                                                  uint32_t NK, uint32_t L, uint32_t n_chunk_rows,
-                                                                  float thr, OrderArgs o, ScreenArgs sc) {
+// (Measured and removed: eight waves of 16 x 64, three stage buffers, a
+// producer/consumer split, register-staged operands (round 5); tile triples
+// on six waves, two workgroups per CU (+43%), and the full-tile bound on
+// packed f32 (+1%) (round 6); DESIGN.md Appendix A.)
+constexpr int kF6PStage = kF6AStage + 2 * kF6BStage;
+__global__ __launch_bounds__(256, 3) void pair_fp6_screen2w_kernel(
+    const uint8_t *__restrict__ a6, const uint8_t *__restrict__ b6, const uint64_t *__restrict__ ok_bits,
+    const uint32_t *__restrict__ pairs, uint32_t n_pairs, uint32_t NK, uint32_t L, uint32_t n_chunk_rows, float thr,
+    OrderArgs o, ScreenArgs sc) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kF6PStage];
     __shared__ unsigned long long sMask[2];
     __shared__ uint32_t sBail, sCand[2];
@@ -1133,21 +1140,23 @@ __global__ __launch_bounds__(256, 3) void pair_fp6_screen2w_kernel(const uint8_t
     const uint32_t ta = entry >> 16, tb0 = entry & 0x7FFFu;
     const bool single = (entry & kF6Single) != 0, idle = single && half;  // (uniform per wave)
     const uint32_t tb = tb0 + (idle ? 0u : half);
-    const uint8_t *sA = a6 + (size_t)ta * NK * kF6AStage, *sB0 = b6 + (size_t)tb0 * NK * kF6BStage;
-    const uint8_t *sB1 = single ? sB0 : sB0 + (size_t)NK * kF6BStage;
-    // a stage's 1-KB pieces (A image, B image of tb, B image of tb + 1): wave w copies w, w + 4, ...
+    // a stage's twenty 1-KB pieces (A image 0-11, B image of tb 12-15, of tb
+    // + 1 16-19): wave w copies w, w + 4, w + 8 of A and piece w of each B
+    // image (a single entry's second image is the first's, which its idle
+    // half reads)
+    static_assert(kF6AStage == 3 * 4096 && kF6BStage == 4096, "five pieces per wave and stage");
+    const uint8_t *pA = a6 + (size_t)ta * NK * kF6AStage + wave * 1024;
+    const uint8_t *pB0 = b6 + (size_t)tb0 * NK * kF6BStage + wave * 1024;
+    const uint8_t *pB1 = single ? pB0 : pB0 + (size_t)NK * kF6BStage;
     auto issue = [&](uint32_t kb, uint32_t buf) {
-        const uint32_t gb = lds + buf * kF6PStage;
-        const uint8_t *a = sA + (size_t)kb * kF6AStage, *b0 = sB0 + (size_t)kb * kF6BStage,
-                      *b1 = sB1 + (size_t)kb * kF6BStage;
-#pragma unroll
-        for (uint32_t p = wave; p < kF6PStage / 1024; p += 4) {
-            const uint32_t off = p * 1024;
-            glds16_s(off < kF6AStage ? a + off
-                                     : off < kF6AStage + kF6BStage ? b0 + (off - kF6AStage)
-                                                                      : b1 + (off - kF6AStage - kF6BStage),
-                     lane16, gb + off);
-        }
+        const uint32_t gb = lds + buf * kF6PStage + wave * 1024;
+        const uint8_t *a = pA + (size_t)kb * kF6AStage;
+        const size_t bo = (size_t)kb * kF6BStage;
+        glds16_s(a, lane16, gb);
+        glds16_s(a + 4096, lane16, gb + 4096);
+        glds16_s(a + 8192, lane16, gb + 8192);
+        glds16_s(pB0 + bo, lane16, gb + kF6AStage);
+        glds16_s(pB1 + bo, lane16, gb + kF6AStage + kF6BStage);
     };
     issue(0, 0);
     if (tid == 0) {  // the give-up test (as the single-tile kernel)
@@ -1213,6 +1222,174 @@ __global__ __launch_bounds__(256, 3) void pair_fp6_screen2w_kernel(const uint8_t
     }
     if (mine && !idle) {
         const unsigned mk = ep0.blocks(acc[0]) | ep1.blocks(acc[1]);
+        if (mk) atomicOr(&sMask[half], (unsigned long long)mk);
+    }
+    __syncthreads();
+    if (!idle) screen_verdict(mine ? (uint32_t)sMask[half] : 0u, ta, tb, ltid, n_chunk_rows, o, sc);
+}
+
+// ---- i8 screen on tile pairs with wide waves (round 6) ----------------------
+//
+// The one-plane i8 screen (the top weight digit d = d_top)
+// where the fp6 rounding is too coarse for the data (linkage blocks, wide
+// weight ranges): the tile-pair, wide-wave structure of
+// pair_fp6_screen2w_kernel on v_mfma_i32_16x16x64_i8, with the operands
+// pre-multiplied once per load (i8_images_build) instead of formed per stage
+// by v_perm: per 64-site tile and 64-sequence block kb one stage image
+//   A [tile][kb][16-site block][in, major][1 KB]: lane l = site l & 15,
+//      byte j = d(k) x in (resp. major) of sequence k = 64 kb + 16 (l >> 4) + j
+//      (int8: a digit in [-128, 127] times 0 or 1)                      (8 KB)
+//   B [tile][kb][16-site block][1 KB]: the same lanes, byte j = the b code
+//      0 (neither), 1 (minor), 2 (major) = minor + 2 major              (4 KB)
+// so X = S(A B) and Y = S(A (B & 0x01010101)) are the X / Y sums of the fp6
+// screen (X0 = T + SB, Y0 = T - SB, X1 = SA + SAB, Y1 = SA - SAB in
+// top-digit units): exact integers below 2^23, so exact in f32, and the same
+// epilogue (F6Epi, r2_screen_terms_xy2) decides each tile with R2 = 2R on
+// the integer grid.  Per stage (64 sequences) a workgroup LDS-DMAs A (8 KB)
+// and two B images (4 KB each); wave w copies four 1-KB pieces and computes
+// rows 32 (w & 1) .. + 31 x 64 columns of tile tb + (w >> 1): 32 MFMAs per
+// stage, 8 KB of LDS reads, 16 mask instructions.
+constexpr int kI8ABytes = 2048;                 // per 16-site block: in, major channels
+constexpr int kI8AStage = 4 * kI8ABytes;        // a tile's A image per 64 sequences
+constexpr int kI8BStage = 4 * 1024;             // ... and B image
+constexpr int kI8PStage = kI8AStage + 2 * kI8BStage;
+size_t i8_a_bytes(size_t LP, size_t NP) { return LP / 64 * (NP / 64) * kI8AStage; }
+size_t i8_b_bytes(size_t LP, size_t NP) { return LP / 64 * (NP / 64) * kI8BStage; }
+
+// one thread per (64-site tile, 64-sequence block, 16-site block, lane)
+__global__ __launch_bounds__(256) void i8img_kernel(const uint8_t *__restrict__ codes, const int8_t *__restrict__ digit,
+                                                     uint32_t LP, uint32_t NP, uint8_t *__restrict__ a8,
+                                                     uint8_t *__restrict__ b8) {
+    const uint32_t NK = NP / 64;
+    const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (size_t)LP / 16 * NK * 64) return;
+    const uint32_t lane = idx & 63, blk = (idx >> 6) & 3;
+    const size_t tk = idx >> 8, tile = tk / NK;  // tk = tile * NK + kb
+    const uint32_t kb = (uint32_t)(tk % NK);
+    const uint32_t k0 = 64 * kb + 16 * (lane >> 4);
+    const uint4 c4 = *reinterpret_cast<const uint4 *>(codes + (tile * 64 + blk * 16 + (lane & 15)) * (size_t)NP + k0);
+    const uint4 d4 = *reinterpret_cast<const uint4 *>(digit + k0);
+    const uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w}, d[4] = {d4.x, d4.y, d4.z, d4.w};
+    uint32_t ai[4], am[4], b[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t vi = 0, vm = 0, vb = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t cc = (c[q] >> (8 * j)) & 0xFFu, dd = (d[q] >> (8 * j)) & 0xFFu;
+            vi |= ((cc & kCodeIn) ? dd : 0u) << (8 * j);
+            vm |= ((cc & kCodeMaj) ? dd : 0u) << (8 * j);
+            vb |= ((cc & kCodeIn) ? ((cc & kCodeMaj) ? 2u : 1u) : 0u) << (8 * j);
+        }
+        ai[q] = vi, am[q] = vm, b[q] = vb;
+    }
+    uint8_t *pa = a8 + tk * kI8AStage + blk * kI8ABytes;
+    *reinterpret_cast<uint4 *>(pa + 16 * lane) = make_uint4(ai[0], ai[1], ai[2], ai[3]);
+    *reinterpret_cast<uint4 *>(pa + 1024 + 16 * lane) = make_uint4(am[0], am[1], am[2], am[3]);
+    *reinterpret_cast<uint4 *>(b8 + tk * kI8BStage + blk * 1024 + 16 * lane) = make_uint4(b[0], b[1], b[2], b[3]);
+}
+
+void launch_i8img(const uint8_t *codes, const int8_t *digit, size_t LP, size_t NP, uint8_t *a8, uint8_t *b8,
+                  hipStream_t s) {
+    const size_t n = LP / 16 * (NP / 64) * 64;
+    hipLaunchKernelGGL(i8img_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, codes, digit, (uint32_t)LP,
+                       (uint32_t)NP, a8, b8);
+}
+
+__global__ __launch_bounds__(256, 3) void pair_i8_screen2w_kernel(
+    const uint8_t *__restrict__ a8, const uint8_t *__restrict__ b8, const uint64_t *__restrict__ ok_bits,
+    const uint32_t *__restrict__ pairs, uint32_t n_pairs, uint32_t NK, uint32_t L, uint32_t n_chunk_rows, float thr,
+    OrderArgs o, ScreenArgs sc) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kI8PStage];
+    __shared__ unsigned long long sMask[2];
+    __shared__ uint32_t sCand[2];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *sc.cand_work = 0u;  // for the launch after it
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t half = wave >> 1, rp = wave & 1, ltid = tid & 127;
+    const uint32_t lds = lds_addr(smem), lane16 = lane * 16;
+    const uint32_t entry = blockIdx.x < n_pairs ? pairs[blockIdx.x] : kNoTile;
+    if (entry == kNoTile) return;  // (uniform: the whole workgroup)
+    const uint32_t ta = entry >> 16, tb0 = entry & 0x7FFFu;
+    const bool single = (entry & kF6Single) != 0, idle = single && half;  // (uniform per wave)
+    const uint32_t tb = tb0 + (idle ? 0u : half);
+    // a stage's sixteen 1-KB pieces (A image 0-7, B image of tb 8-11, of tb + 1
+    // 12-15): wave w copies w and w + 4 of A and piece w of each B image
+    static_assert(kI8AStage == 2 * 4096 && kI8BStage == 4096, "four pieces per wave and stage");
+    const uint8_t *pA = a8 + (size_t)ta * NK * kI8AStage + wave * 1024;
+    const uint8_t *pB0 = b8 + (size_t)tb0 * NK * kI8BStage + wave * 1024;
+    const uint8_t *pB1 = single ? pB0 : pB0 + (size_t)NK * kI8BStage;
+    auto issue = [&](uint32_t kb, uint32_t buf) {
+        const uint32_t gb = lds + buf * kI8PStage + wave * 1024;
+        const uint8_t *a = pA + (size_t)kb * kI8AStage;
+        const size_t bo = (size_t)kb * kI8BStage;
+        glds16_s(a, lane16, gb);
+        glds16_s(a + 4096, lane16, gb + 4096);
+        glds16_s(pB0 + bo, lane16, gb + kI8AStage);
+        glds16_s(pB1 + bo, lane16, gb + kI8AStage + kI8BStage);
+    };
+    issue(0, 0);
+    if (tid < 2) sCand[tid] = 0u, sMask[tid] = 0ull;
+    const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
+    v4i acc[2][4][2][2];  // [row block 2 rp + j][b block n][channel_a][X, Y]
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y) acc[j][n][x][y] = v4i{0, 0, 0, 0};
+    const uint32_t boff = kI8AStage + (idle ? 0u : half) * kI8BStage;  // this half's B image in a stage
+    const uint32_t aoff = 2 * rp * kI8ABytes;                             // this wave's two A row blocks
+    uint32_t buf = 0;
+    for (uint32_t kb = 0; kb < NK; ++kb) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of the stage landed
+        __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
+        asm volatile("" ::: "memory");
+        if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
+        const uint8_t *g = smem + buf * kI8PStage;
+        v4i av[2][2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+                av[j][x] = *reinterpret_cast<const v4i *>(g + aoff + j * kI8ABytes + x * 1024 + 16 * lane);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const v4i b = *reinterpret_cast<const v4i *>(g + boff + n * 1024 + 16 * lane);
+            constexpr int kOnes = 0x01010101;  // the minor bit of each code byte
+            const v4i bmin = {b[0] & kOnes, b[1] & kOnes, b[2] & kOnes, b[3] & kOnes};
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {
+                    acc[j][n][x][0] = mfma_i8_16(av[j][x], b, acc[j][n][x][0]);
+                    acc[j][n][x][1] = mfma_i8_16(av[j][x], bmin, acc[j][n][x][1]);
+                }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
+        buf ^= 1;
+    }
+    // the integer sums as f32 (exact: |X|, |Y| < 2^23), then the fp6 screen's epilogue
+    v4f accf[2][4][2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) accf[j][n][x][y][e] = (float)acc[j][n][x][y][e];
+    const F6Epi ep0{ta, tb, 2 * rp, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
+    const F6Epi ep1{ta, tb, 2 * rp + 1, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
+    const bool cand = !idle && (ep0.any(accf[0]) || ep1.any(accf[1]));
+    if (cand) sCand[half] = 1u;  // (benign race: every writer stores 1)
+    __syncthreads();
+    const bool mine = sCand[half] != 0;  // (uniform per half)
+    if (mine && !idle) {
+        const unsigned mk = ep0.blocks(accf[0]) | ep1.blocks(accf[1]);
         if (mk) atomicOr(&sMask[half], (unsigned long long)mk);
     }
     __syncthreads();
@@ -1379,7 +1556,7 @@ void fp6_screen_args(const MfmaLaunch &m, ScreenArgs &sc) {
 void launch_fp6_screen(const MfmaLaunch &m, const uint64_t *ok_bits, const OrderArgs &o, const ScreenArgs &sc,
                        uint32_t stride, hipStream_t s) {
     if (m.f6_pairs) {
-        // (a tile pair per workgroup, the XCD-ordered pair list)
+        // (a tile group per workgroup, the XCD-ordered group list)
         hipLaunchKernelGGL(pair_fp6_screen2w_kernel, dim3((m.f6_n_pairs + stride - 1) / stride), dim3(256), 0, s,
                            m.fp6->a6, m.fp6->b6, ok_bits, m.f6_pairs, m.f6_n_pairs, m.fp6->NK, m.L, m.n_chunk_rows,
                            m.thr, o, sc);
@@ -1518,6 +1695,18 @@ bool launch_pair_mfma(const MfmaLaunch &m, const OrderArgs &o, const DenseArgs *
     if ((double)sc.Rf < sc.R) sc.Rf = nextafterf(sc.Rf, INFINITY);
     // 2: doubled sums (NP <= 16384), 1: halved sums with f64 fallback, 0: f64
     sc.f32 = m.nonneg ? (m.NP <= kScrF32MaxNP ? 2 : m.NP <= kScreenF32MaxNP ? 1 : 0) : 0;
+    if (sc.f32 == 2 && m.i8img && m.f6_pairs && m.i8img->digit_plane == top) {
+        // tile pairs, wide waves, pre-multiplied operands: the xy2 epilogue on
+        // exact marginals needs R2 = 2 R on the integer grid (rounded up: a
+        // larger residual bound is still one)
+        sc.Rf = (float)(std::ceil(2.0 * sc.R) / 2.0);
+        screen_consts((float)(2 * m.dsum[top]), 2.0f * sc.Rf, sc.E, sc.mloc);
+        hipLaunchKernelGGL(pair_i8_screen2w_kernel, dim3(m.f6_n_pairs), dim3(256), 0, s, m.i8img->a8, m.i8img->b8,
+                           ok_bits, m.f6_pairs, m.f6_n_pairs, (uint32_t)(m.NP / 64), m.L, m.n_chunk_rows, m.thr, o, sc);
+        if (screen_done) (void)hipEventRecord(screen_done, s);
+        launch_candidates(m, n, idx, ok_bits, o, dn, sc, s);
+        return true;
+    }
     // every doubled one-plane T <= 2 sum_k |d_top,k| <= 256 NP <= 2^22 (exact in f32)
     if (sc.f32 == 2) screen_consts((float)(2 * m.dsum[top]), 2.0f * sc.Rf, sc.E, sc.mloc);
     launch_lds<kModeScreen, 1>(m, ok_bits, m.tiles, m.n_tiles, nullptr, m.n_tiles, top, o, dn, sc, s);
