@@ -434,6 +434,12 @@ def main():
                     help="nccl (default): RCCL over xGMI, one GPU per rank; gloo: counts and rows exchanged as host "
                          "tensors, ranks may share a GPU (rank r on device r mod the visible count: the multi-rank "
                          "test of the launcher on a one-GPU box, never a headline line)")
+    ap.add_argument("--counts", default="auto", choices=["auto", "shm", "collective"],
+                    help="N>1 step path: how the ranks exchange each step's row counts.  shm: through host shared "
+                         "memory once each rank's pass has completed (weightedld_amd.dist.HostCountExchange; ranks "
+                         "on one host); collective: an all_gather queued behind the pass on the device (RCCL, or "
+                         "gloo with --collectives gloo); auto (default): shm when every rank is on this host.  "
+                         "The rows always travel by the collective backend")
     ap.add_argument("--check-steps", type=int, default=0, metavar="K",
                     help="after the timed region, K more steps whose gathered rows rank 0 compares with the "
                          "oracle's (every row and bit, in reference order)")
@@ -569,6 +575,16 @@ def main():
         if serialize == "stream":  # every context on the first one's stream (wld_set_stream)
             for c in ctxs1[1:]:
                 c.set_stream(ctx)
+    xchg = None  # N>1: the row counts through host shared memory (--counts)
+    if dist_on and args.counts != "collective":
+        hosts = [None] * world
+        if world > 1:
+            dist.all_gather_object(hosts, socket.gethostname())
+        one_host = world == 1 or len(set(hosts)) == 1
+        if args.counts == "shm" and not one_host:
+            raise SystemExit("bench.py: --counts shm needs every rank on one host")
+        if one_host:
+            xchg = wdist.HostCountExchange(rank, world)
     if dist_on and pipelined:
         pipe = wdist.PipelinedShardStep([ctx] + [new_ctx() for _ in range(max(2, depth) - 1)], rank, world,
                                         device,
@@ -579,12 +595,13 @@ def main():
                                         # (wld_run_after); 1: for step i-1's whole run (archive/profiles_r01_r03/r02pc/,
                                         # archive/profiles_r01_r03/r03i/)
                                         serialize_kernels={"0": False, "1": True}.get(serialize, "pair"),
-                                        host_collectives=host_coll)
+                                        host_collectives=host_coll, counts=xchg)
     if dist_on:
         # single steps on ctx (stats sampling, unscreened and checked steps) go
         # through the pipeline's own step object for ctx: one stream per context
         shard_step = pipe.steps[0] if pipe is not None else wdist.ShardStep(ctx, rank, world, device,
-                                                                              host_collectives=host_coll)
+                                                                              host_collectives=host_coll,
+                                                                              counts=xchg)
 
     def nrows(res):
         return int(res[1].shape[1]) if res is not None and res[1] is not None else 0
@@ -739,6 +756,8 @@ def main():
             shard_step.close()
         for c in reversed(created):
             c.close()
+        if xchg is not None:
+            xchg.close()
 
     if dist_on:
         # no collective after this: the other ranks leave, so that rank 0's
@@ -901,8 +920,10 @@ def main():
                    # (the launcher's multi-rank test): count the devices used
                    "devices": min(world, n_dev) if host_coll else world,
                    "parallelism": "chunk-range shard x%d%s%s" % (
-                       world, ((" + gloo host-tensor gather" if host_coll else " + RCCL count all_gather, exact-size "
-                                "send/recv to rank 0") if dist_on else ""),
+                       world, (((" + row counts through host shared memory" if xchg is not None else
+                                 " + gloo host-tensor count all_gather" if host_coll else " + RCCL count all_gather") +
+                                (", gloo host-tensor row gather" if host_coll else ", exact-size RCCL send/recv of the "
+                                 "rows to rank 0")) if dist_on else ""),
                        (", pipelined steps (%d contexts, %s)" % (
                            depth, {"0": "screens may overlap", "1": "serialized on the whole step",
                                    "stream": "one stream"}.get(

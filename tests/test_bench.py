@@ -108,7 +108,8 @@ def test_launcher_two_ranks_rows_equal_oracle_every_step():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--collectives", "gloo", "--config", "c2",
                         "--steps", "5", "--warmup", "2", "--settle-s", "0", "--check-steps", "4",
-                        "--cpu-seconds", "2"], cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+                        "--cpu-seconds", "2", "--counts", "collective"], cwd=REPO, env=env, capture_output=True,
+                       text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]
@@ -134,7 +135,8 @@ def test_launcher_eight_ranks_rows_equal_oracle_every_step():
     performance line); BASELINE config 2 at threshold 0, each rank's 1/8
     chunk range, the pipelined N>1 step loop; both checked steps' gathered
     rows equal the oracle's bit for bit in reference order, and the line says
-    n_gpus 8."""
+    n_gpus 8.  The row counts go through host shared memory (--counts auto on
+    one host; the two-rank test above keeps the collective count exchange)."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--collectives", "gloo", "--config", "c2",
                         "--steps", "3", "--warmup", "1", "--settle-s", "0", "--check-steps", "2",
@@ -144,6 +146,7 @@ def test_launcher_eight_ranks_rows_equal_oracle_every_step():
     assert len(lines) == 1, r.stdout[-3000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 8 and out["config"]["launch"] == "bench.py spawned 8 ranks"
+    assert "host shared memory" in out["config"]["parallelism"], out["config"]
     sc = out["steps_check"]
     assert sc["steps"] == 2 and sc["equal_to_oracle"] == 2 and sc["rows_per_step"] > 1_900_000
     print("eight ranks: %.3f ms/step (one shared GPU), steps_check %s" % (out["ms_per_step"], sc))

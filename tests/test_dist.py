@@ -127,7 +127,7 @@ def ld_region_data(L, N, seed):
     return buf, rng.random(N).astype(np.float32) + 0.2
 
 
-def _step_worker(rank, world, port, L, N, thrs, pipelined, q):
+def _step_worker(rank, world, port, L, N, thrs, pipelined, q, counts="collective"):
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import torch.distributed as dist
@@ -141,10 +141,11 @@ def _step_worker(rank, world, port, L, N, thrs, pipelined, q):
         buf, w = ld_region_data(L, N, 5)
         lo, hi = wdist.shard_chunks(L, world, rank)
         results = []
+        xchg = wdist.HostCountExchange(rank, world) if counts == "shm" else None
         if pipelined:
             depth, mode = int(str(pipelined)[0]), ("pair" if str(pipelined).endswith("pair") else False)
             pipe = wdist.PipelinedShardStep([OracleShardContext(buf, w) for _ in range(depth)], rank, world,
-                                            "cpu", serialize_kernels=mode)
+                                            "cpu", serialize_kernels=mode, counts=xchg)
             for t in thrs:
                 r = pipe.submit(t, lo, hi)
                 if r is not None:
@@ -152,11 +153,13 @@ def _step_worker(rank, world, port, L, N, thrs, pipelined, q):
             results += pipe.drain_all()
             assert pipe.drain() is None
         else:
-            step = wdist.ShardStep(OracleShardContext(buf, w), rank, world, "cpu")
+            step = wdist.ShardStep(OracleShardContext(buf, w), rank, world, "cpu", counts=xchg)
             results = [step(t, lo, hi) for t in thrs]
         mine = [int(n) for n, _ in results]
         counts = [None] * world
         dist.all_gather_object(counts, mine)
+        if xchg is not None:
+            xchg.close()
         if rank == 0:
             ok = []
             for i, t in enumerate(thrs):
@@ -170,21 +173,25 @@ def _step_worker(rank, world, port, L, N, thrs, pipelined, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("counts", ["collective", "shm"])
 @pytest.mark.parametrize("pipelined", [0, 2, 3, "3pair"], ids=["step", "pipelined2", "pipelined3", "pipelined3pair"])
 @pytest.mark.parametrize("world", [2, 3, 4])
-def test_gloo_shard_steps_match_unsharded(world, pipelined):
+def test_gloo_shard_steps_match_unsharded(world, pipelined, counts):
     """ShardStep / PipelinedShardStep (the bench's N>1 step path) at world
     2-4 under gloo: per step, the count exchange, the row gather issued only
     when some rank has rows, and (pipelined) step i-1's gather issued after
     step i's count exchange; depth 3: two steps in flight) — every step's gathered rows equal the unsharded
     oracle's, in reference order, with threshold sequences where no rank,
-    one rank or every rank has rows, and nothing deadlocks."""
+    one rank or every rank has rows, and nothing deadlocks; the row counts
+    exchanged by a collective or through host shared memory
+    (HostCountExchange)."""
     L, N = 1200, 200
     thrs = [0.0, 2.0, 0.5, 2.0, 0.0, 0.5, 0.5]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_step_worker, args=(r, world, port, L, N, thrs, pipelined, q)) for r in range(world)]
+    procs = [ctx.Process(target=_step_worker, args=(r, world, port, L, N, thrs, pipelined, q, counts))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -299,7 +306,7 @@ class PlantedRowsContext(OracleShardContext):
             ctypes.c_int64.from_address(d_count_ptr).value = len(self.rows["r2"])
 
 
-def _world8_worker(rank, world, port, kind, pipelined, thrs, q):
+def _world8_worker(rank, world, port, kind, pipelined, thrs, q, counts="collective"):
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import torch.distributed as dist
@@ -319,8 +326,9 @@ def _world8_worker(rank, world, port, kind, pipelined, thrs, q):
             L = PlantedRowsContext.L
             make = PlantedRowsContext
         lo, hi = wdist.shard_chunks(L, world, rank)
+        xchg = wdist.HostCountExchange(rank, world) if counts == "shm" else None
         if pipelined:
-            pipe = wdist.PipelinedShardStep([make() for _ in range(pipelined)], rank, world, "cpu")
+            pipe = wdist.PipelinedShardStep([make() for _ in range(pipelined)], rank, world, "cpu", counts=xchg)
             results = []
             for t in thrs:
                 r = pipe.submit(t, lo, hi)
@@ -328,11 +336,13 @@ def _world8_worker(rank, world, port, kind, pipelined, thrs, q):
                     results.append(r)
             results += pipe.drain_all()
         else:
-            step = wdist.ShardStep(make(), rank, world, "cpu")
+            step = wdist.ShardStep(make(), rank, world, "cpu", counts=xchg)
             results = [step(t, lo, hi) for t in thrs]
         mine = [int(n) for n, _ in results]
         counts = [None] * world
         dist.all_gather_object(counts, mine)
+        if xchg is not None:
+            xchg.close()
         if rank == 0:
             if kind == "c4":
                 base = O.all_pairs(buf, w, np.float32(min(thrs)), n_threads=8)
@@ -350,9 +360,10 @@ def _world8_worker(rank, world, port, kind, pipelined, thrs, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("counts", ["collective", "shm"])
 @pytest.mark.parametrize("kind", ["c4", "c5"])
 @pytest.mark.parametrize("pipelined", [0, 3], ids=["step", "pipelined3"])
-def test_gloo_world8_steps(kind, pipelined):
+def test_gloo_world8_steps(kind, pipelined, counts):
     """The driver's N=8 path before its SCALE run: eight gloo ranks, each
     with its chunk range of BASELINE config 4 (3,160 chunks; oracle-backed
     contexts, N = 32) or config 5 (19,306 chunks; closed-form rows), through
@@ -364,7 +375,8 @@ def test_gloo_world8_steps(kind, pipelined):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_world8_worker, args=(r, 8, port, kind, pipelined, thrs, q)) for r in range(8)]
+    procs = [ctx.Process(target=_world8_worker, args=(r, 8, port, kind, pipelined, thrs, q, counts))
+             for r in range(8)]
     for p in procs:
         p.start()
     for p in procs:

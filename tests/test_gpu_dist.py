@@ -25,7 +25,7 @@ from test_dist import _free_port, ld_region_data
 pytestmark = pytest.mark.gpu
 
 
-def _gpu_step_worker(rank, world, port, L, N, thrs, mode, q):
+def _gpu_step_worker(rank, world, port, L, N, thrs, mode, q, counts="collective"):
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import torch
@@ -47,12 +47,14 @@ def _gpu_step_worker(rank, world, port, L, N, thrs, mode, q):
         for c in ctxs:
             c.load(buf, w)
         results = []
+        xchg = wdist.HostCountExchange(rank, world) if counts == "shm" else None
         if mode == "step":
-            step = wdist.ShardStep(ctxs[0], rank, world, dev, host_collectives=True)
+            step = wdist.ShardStep(ctxs[0], rank, world, dev, host_collectives=True, counts=xchg)
             results = [step(t, lo, hi) for t in thrs]
         else:
             pipe = wdist.PipelinedShardStep(ctxs, rank, world, dev, host_collectives=True,
-                                            serialize_kernels="pair" if mode.endswith("pair") else False)
+                                            serialize_kernels="pair" if mode.endswith("pair") else False,
+                                            counts=xchg)
             for t in thrs:
                 r = pipe.submit(t, lo, hi)
                 if r is not None:
@@ -76,19 +78,23 @@ def _gpu_step_worker(rank, world, port, L, N, thrs, mode, q):
             assert all(r[1] is None for r in results)
         for c in ctxs:
             c.close()
+        if xchg is not None:
+            xchg.close()
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("counts", ["collective", "shm"])
 @pytest.mark.parametrize("mode", ["step", "2pair", "3pair", "2"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_gpu_shard_steps_multi_rank(world, mode):
+def test_gpu_shard_steps_multi_rank(world, mode, counts):
     L, N = 1200, 200
     thrs = [0.0, 2.0, 0.5, 2.0, 0.0, 0.5, 0.5]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gpu_step_worker, args=(r, world, port, L, N, thrs, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gpu_step_worker, args=(r, world, port, L, N, thrs, mode, q, counts))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

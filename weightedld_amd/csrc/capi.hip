@@ -198,6 +198,12 @@ struct wld_ctx {
     int ev_end = 4;            // the event that ends a pass's scan: 4, or 3 when the scan ran inside the pair launch
     uint64_t gather_cap = 0;
     wld_run_stats stats{};
+    // the last pass's phase times, read from its events only when the stats
+    // are asked for (materialize_times; ~3 hipEventElapsedTime calls the N>1
+    // step loop, which never reads them, does not pay)
+    bool times_pending = false;
+    bool times_screened = false;
+    int times_order_end = 4;
     // per-chunk progress (wld_run_host with a callback): the run's chunk
     // countdowns and log slot counter on the device, the log in mapped pinned
     // host memory (one u64 pair count per completed chunk, ~0 until written)
@@ -248,6 +254,15 @@ float event_ms(hipEvent_t a, hipEvent_t b) {
         return -1.0f;
     }
     return ms;
+}
+
+// the last completed pass's phase times from its events (run_complete defers them)
+void materialize_times(wld_ctx *c) {
+    if (!c->times_pending) return;
+    c->times_pending = false;
+    c->stats.pair_kernel_ms = event_ms(c->ev[2], c->ev[3]);
+    c->stats.order_ms = event_ms(c->ev[3], c->ev[c->times_order_end]);
+    c->stats.screen_ms = c->times_screened ? event_ms(c->ev[2], c->ev[6]) : 0.0;
 }
 
 // fixed-point exponent for the MFMA weight planes: max|w| * 2^shift must fit
@@ -1156,6 +1171,10 @@ int grow_staging(wld_ctx *c, uint64_t cap) {
 // the caller's device word, if given).
 int enqueue_pass(wld_ctx *c) {
     const RunPending &r = c->pend;
+    if (c->times_pending) {  // the last pass's times were never asked for: its events are re-recorded now
+        c->times_pending = false;
+        c->stats.pair_kernel_ms = c->stats.order_ms = c->stats.screen_ms = -1.0;
+    }
     const uint32_t lin_count = r.lin_end - r.lin_begin;
     // The chunk scan of every completed run leaves the cursor and its chunk
     // totals at 0, and every computed tile writes all of its segment counts,
@@ -1456,8 +1475,8 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     c->stats.kernel = c->kernel;
     c->stats.pairs = r.pairs;
     c->stats.rows = rows;
-    c->stats.pair_kernel_ms = event_ms(c->ev[2], c->ev[3]);
-    c->stats.order_ms = event_ms(c->ev[3], c->ev[order_end]);
+    c->times_pending = true;  // (pair_kernel_ms, order_ms, screen_ms: materialize_times)
+    c->times_order_end = order_end;
     // (exact candidate pairs: the i8 pass, ref_sums_kernel, ref_compact_kernel)
     c->stats.pair_kernel_launches = c->n_tiles ? (c->ref_pairs_pass ? 3 : c->screened ? 2 : 1) : 0;
     c->stats.tiles = c->n_tiles;
@@ -1489,7 +1508,7 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     // million at C4 size): past a tenth of all pairs the full f32 kernel
     // (27.8 ms for every tile at C4) is cheaper
     if (c->ref_pairs_pass && h[0] * 10 > r.pairs) c->ref_pairs_bad_thr = std::max(c->ref_pairs_bad_thr, r.thr);
-    c->stats.screen_ms = c->screened ? event_ms(c->ev[2], c->ev[6]) : 0.0;
+    c->times_screened = c->screened;
     c->stats.candidate_tiles = c->screened ? h[2] : c->n_tiles;
     c->stats.candidate_blocks = c->screened && !c->ref_pairs_pass ? h[3] : 16 * (uint64_t)c->n_tiles;
     if (n_rows) *n_rows = rows;
@@ -1636,6 +1655,10 @@ int wld_dense(wld_ctx *c, float *d, float *d_prime, float *r2, uint8_t *valid) {
 
 int wld_last_stats(wld_ctx *c, wld_run_stats *out) {
     if (!c || !out) return fail(WLD_E_ARG, "null argument");
+    if (c->members.empty()) {
+        (void)hipSetDevice(c->device);
+        materialize_times(c);
+    }
     *out = c->stats;
     return WLD_OK;
 }
@@ -1800,6 +1823,10 @@ int run_host_group(wld_ctx *g, float thr, const std::function<void(uint64_t)> *o
         wld_pairs_free(out);
     }
     for (auto &p : part) wld_pairs_free(&p);
+    for (wld_ctx *m : g->members) {
+        (void)hipSetDevice(m->device);
+        materialize_times(m);
+    }
     g->stats = g->members[0]->stats;
     g->stats.progress_filled = 0;
     for (wld_ctx *m : g->members) g->stats.progress_filled += m->stats.progress_filled;

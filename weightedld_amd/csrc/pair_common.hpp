@@ -260,19 +260,7 @@ __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst) {
 
 // The same copy addressed as SGPR base + per-lane 32-bit VGPR offset (no
 // 64-bit per-lane address arithmetic).
-#ifndef WLD_GLDS_M0_CLOBBER
-#define WLD_GLDS_M0_CLOBBER 0
-#endif
 __device__ __forceinline__ void glds16_s(const void *sbase, uint32_t voff, uint32_t lds_dst) {
-#if WLD_GLDS_M0_CLOBBER  // (A/B) m0 declared clobbered instead of saved and restored
-    asm volatile(
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %0, %1"
-        :
-        : "v"(voff), "s"(sbase), "s"(lds_dst)
-        : "memory", "m0");
-#else
     uint32_t keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
@@ -283,7 +271,6 @@ __device__ __forceinline__ void glds16_s(const void *sbase, uint32_t voff, uint3
         : "=&s"(keep)
         : "v"(voff), "s"(sbase), "s"(lds_dst)
         : "memory");
-#endif
 }
 
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {

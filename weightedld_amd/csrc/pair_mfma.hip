@@ -1137,95 +1137,109 @@ __global__ __launch_bounds__(256, 3) void pair_fp6_screen2w_kernel(
     const uint32_t ei = sc.probe ? blockIdx.x * sc.probe_stride + blockIdx.x % sc.probe_stride : blockIdx.x;
     const uint32_t entry = ei < n_pairs ? pairs[ei] : kNoTile;
     if (entry == kNoTile) return;  // (uniform: the whole workgroup)
-    const uint32_t ta = entry >> 16, tb0 = entry & 0x7FFFu;
-    const bool single = (entry & kF6Single) != 0, idle = single && half;  // (uniform per wave)
-    const uint32_t tb = tb0 + (idle ? 0u : half);
     // a stage's twenty 1-KB pieces (A image 0-11, B image of tb 12-15, of tb
     // + 1 16-19): wave w copies w, w + 4, w + 8 of A and piece w of each B
     // image (a single entry's second image is the first's, which its idle
     // half reads)
     static_assert(kF6AStage == 3 * 4096 && kF6BStage == 4096, "five pieces per wave and stage");
-    const uint8_t *pA = a6 + (size_t)ta * NK * kF6AStage + wave * 1024;
-    const uint8_t *pB0 = b6 + (size_t)tb0 * NK * kF6BStage + wave * 1024;
-    const uint8_t *pB1 = single ? pB0 : pB0 + (size_t)NK * kF6BStage;
-    auto issue = [&](uint32_t kb, uint32_t buf) {
+    struct Src {
+        const uint8_t *pA, *pB0, *pB1;
+    };
+    auto src_of = [&](uint32_t e) {
+        const uint32_t ta_ = e >> 16, tb0_ = e & 0x7FFFu;
+        Src r;
+        r.pA = a6 + (size_t)ta_ * NK * kF6AStage + wave * 1024;
+        r.pB0 = b6 + (size_t)tb0_ * NK * kF6BStage + wave * 1024;
+        r.pB1 = (e & kF6Single) ? r.pB0 : r.pB0 + (size_t)NK * kF6BStage;
+        return r;
+    };
+    auto issue = [&](const Src &sr, uint32_t kb, uint32_t buf) {
         const uint32_t gb = lds + buf * kF6PStage + wave * 1024;
-        const uint8_t *a = pA + (size_t)kb * kF6AStage;
+        const uint8_t *a = sr.pA + (size_t)kb * kF6AStage;
         const size_t bo = (size_t)kb * kF6BStage;
         glds16_s(a, lane16, gb);
         glds16_s(a + 4096, lane16, gb + 4096);
         glds16_s(a + 8192, lane16, gb + 8192);
-        glds16_s(pB0 + bo, lane16, gb + kF6AStage);
-        glds16_s(pB1 + bo, lane16, gb + kF6AStage + kF6BStage);
+        glds16_s(sr.pB0 + bo, lane16, gb + kF6AStage);
+        glds16_s(sr.pB1 + bo, lane16, gb + kF6AStage + kF6BStage);
     };
-    issue(0, 0);
-    if (tid == 0) {  // the give-up test (as the single-tile kernel)
-        uint32_t v = 0;
-        if (sc.bail) {
-            const unsigned cc = __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v = cc > sc.bail ? ((cc & kAbandonBit) ? 2u : 1u) : 0u;
-        }
-        sBail = v;
-    }
-    if (tid < 2) sCand[tid] = 0u, sMask[tid] = 0ull;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
-    v4f acc[2][4][2][2];  // [row block 2 rp + j][b block n][channel_a][X, Y]
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-            for (int x = 0; x < 2; ++x)
-#pragma unroll
-                for (int y = 0; y < 2; ++y) acc[j][n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-    const uint32_t boff = kF6AStage + (idle ? 0u : half) * kF6BStage;  // this half's B image in a stage
-    const uint32_t aoff = 2 * rp * kF6ABytes;                             // this wave's two A row blocks
+    const Src cur = src_of(entry);
+    issue(cur, 0, 0);
     uint32_t buf = 0;
-    for (uint32_t kb = 0; kb < NK; ++kb) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of the stage landed
-        __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
-        asm volatile("" ::: "memory");
-        if (kb == 0 && sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
-            if (tid == 0 && sBail == 1) {
-                atomicOr(sc.cand_count, kAbandonBit);
-                atomicOr(sc.cand_buckets, kAbandonBit);
+    {
+        const uint32_t ta = entry >> 16, tb0 = entry & 0x7FFFu;
+        const bool single = (entry & kF6Single) != 0, idle = single && half;  // (uniform per wave)
+        const uint32_t tb = tb0 + (idle ? 0u : half);
+        if (tid == 0) {  // the give-up test (as the single-tile kernel)
+            uint32_t v = 0;
+            if (sc.bail) {
+                const unsigned cc = __hip_atomic_load(sc.cand_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v = cc > sc.bail ? ((cc & kAbandonBit) ? 2u : 1u) : 0u;
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            sBail = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint64_t okA = ok_bits[ta], okB = ok_bits[tb];
+        v4f acc[2][4][2][2];  // [row block 2 rp + j][b block n][channel_a][X, Y]
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int x = 0; x < 2; ++x)
+#pragma unroll
+                    for (int y = 0; y < 2; ++y) acc[j][n][x][y] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+        const uint32_t boff = kF6AStage + (idle ? 0u : half) * kF6BStage;  // this half's B image in a stage
+        const uint32_t aoff = 2 * rp * kF6ABytes;                             // this wave's two A row blocks
+        for (uint32_t kb = 0; kb < NK; ++kb) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of the stage landed
+            __builtin_amdgcn_s_barrier();                     // ... and every other wave's; the other buffer is free
+            asm volatile("" ::: "memory");
+            if (kb == 0) {
+                if (sBail) {  // (uniform) give the pass up: drain this wave's copies, leave
+                    if (tid == 0 && sBail == 1) {
+                        atomicOr(sc.cand_count, kAbandonBit);
+                        atomicOr(sc.cand_buckets, kAbandonBit);
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    return;
+                }
+                // (every wave has left the previous entry's epilogue)
+                if (tid < 2) sCand[tid] = 0u, sMask[tid] = 0ull;
+            }
+            if (kb + 1 < NK) issue(cur, kb + 1, buf ^ 1);
+            const uint8_t *g = smem + buf * kF6PStage;
+            const v8i ai0 = f6_ld24(g + aoff, lane), am0 = f6_ld24(g + aoff + 1536, lane);
+            const v8i ai1 = f6_ld24(g + aoff + kF6ABytes, lane), am1 = f6_ld24(g + aoff + kF6ABytes + 1536, lane);
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const v8i b = f6_ldb(g + boff + n * kF6BBytes, lane);
+                f6_block_mfma(acc[0][n], ai0, am0, b);
+                f6_block_mfma(acc[1][n], ai1, am1, b);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
+            buf ^= 1;
+        }
+        const F6Epi ep0{ta, tb, 2 * rp, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
+        const F6Epi ep1{ta, tb, 2 * rp + 1, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
+        const bool cand = !idle && (ep0.any(acc[0]) || ep1.any(acc[1]));
+        if (cand) sCand[half] = 1u;  // (benign race: every writer stores 1)
+        __syncthreads();
+        const bool mine = sCand[half] != 0;  // (uniform per half)
+        if (sc.probe) {  // the sample run: count, decide nothing
+            if (ltid == 0 && !idle) {
+                if (mine) atomicAdd(sc.probe, 1u);
+                atomicAdd(sc.probe + 1, 1u);
+            }
             return;
         }
-        if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
-        const uint8_t *g = smem + buf * kF6PStage;
-        const v8i ai0 = f6_ld24(g + aoff, lane), am0 = f6_ld24(g + aoff + 1536, lane);
-        const v8i ai1 = f6_ld24(g + aoff + kF6ABytes, lane), am1 = f6_ld24(g + aoff + kF6ABytes + 1536, lane);
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const v8i b = f6_ldb(g + boff + n * kF6BBytes, lane);
-            f6_block_mfma(acc[0][n], ai0, am0, b);
-            f6_block_mfma(acc[1][n], ai1, am1, b);
+        if (mine && !idle) {
+            const unsigned mk = ep0.blocks(acc[0]) | ep1.blocks(acc[1]);
+            if (mk) atomicOr(&sMask[half], (unsigned long long)mk);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
-        buf ^= 1;
+        __syncthreads();
+        if (!idle) screen_verdict(mine ? (uint32_t)sMask[half] : 0u, ta, tb, ltid, n_chunk_rows, o, sc);
     }
-    const F6Epi ep0{ta, tb, 2 * rp, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
-    const F6Epi ep1{ta, tb, 2 * rp + 1, lane, okA, okB, 2.0f * sc.Rf, thr * (1.0f - 0x1p-7f), sc.E, sc.mloc};
-    const bool cand = !idle && (ep0.any(acc[0]) || ep1.any(acc[1]));
-    if (cand) sCand[half] = 1u;  // (benign race: every writer stores 1)
-    __syncthreads();
-    const bool mine = sCand[half] != 0;  // (uniform per half)
-    if (sc.probe) {  // the sample run: count, decide nothing
-        if (ltid == 0 && !idle) {
-            if (mine) atomicAdd(sc.probe, 1u);
-            atomicAdd(sc.probe + 1, 1u);
-        }
-        return;
-    }
-    if (mine && !idle) {
-        const unsigned mk = ep0.blocks(acc[0]) | ep1.blocks(acc[1]);
-        if (mk) atomicOr(&sMask[half], (unsigned long long)mk);
-    }
-    __syncthreads();
-    if (!idle) screen_verdict(mine ? (uint32_t)sMask[half] : 0u, ta, tb, ltid, n_chunk_rows, o, sc);
 }
 
 // ---- i8 screen on tile pairs with wide waves (round 6) ----------------------

@@ -113,6 +113,60 @@ class RowGather:
         return torch.cat([parts[r] for r in reversed(range(self.world)) if r in parts], dim=1)
 
 
+class HostCountExchange:
+    """The per-step row-count exchange of ranks on one host through a block
+    of host shared memory instead of a collective: each rank publishes its
+    step's row count (known on the host once its own pass has completed,
+    wld_run_wait) and reads every rank's.  One exchange costs a few
+    microseconds of host time where the RCCL count all_gather, its stream
+    scope, event and pinned copy cost ~30; the rows themselves
+    still travel by the collective backend (RowGather).  Slots are
+    double-buffered by step parity: a rank can publish step k + 2 only after
+    every rank has published step k + 1, i.e. after every rank has read step
+    k.  Within a slot the count is stored before the step number and read
+    after it (x86-64: stores and loads are not reordered among themselves).
+    Built collectively (rank 0 creates the block and broadcasts its name);
+    all ranks must share the host."""
+
+    def __init__(self, rank, world, group=None):
+        import torch.distributed as dist
+        from multiprocessing import resource_tracker, shared_memory
+
+        self.rank, self.world, self.seq = rank, world, 0
+        name = [None]
+        if rank == 0:
+            self.shm = shared_memory.SharedMemory(create=True, size=2 * 2 * 8 * world)
+            np.ndarray((2, world, 2), dtype=np.int64, buffer=self.shm.buf)[:] = -1
+            name[0] = self.shm.name
+        if world > 1:
+            dist.broadcast_object_list(name, src=0, group=group)
+        if rank != 0:
+            self.shm = shared_memory.SharedMemory(name=name[0])
+            # (the creator owns the block: no second tracker unlinks it at exit)
+            resource_tracker.unregister(self.shm._name, "shared_memory")
+        self.slots = np.ndarray((2, world, 2), dtype=np.int64, buffer=self.shm.buf)  # [parity][rank][count, step]
+        if world > 1:
+            dist.barrier(group=group)  # every rank attached before the creator may unlink at close
+
+    def __call__(self, count):
+        self.seq += 1
+        s = self.slots[self.seq & 1]
+        s[self.rank, 0] = count
+        s[self.rank, 1] = self.seq
+        steps = s[:, 1]
+        while steps.min() < self.seq:
+            pass
+        return s[:, 0].tolist()
+
+    def close(self):
+        if self.shm is not None:
+            self.slots = None
+            self.shm.close()
+            if self.rank == 0:
+                self.shm.unlink()
+            self.shm = None
+
+
 class _HostStream:
     """Stand-in for the context's stream when the step runs on the CPU (the
     gloo rehearsal of the N>1 path in tests/test_dist.py): ordering is program
@@ -149,10 +203,13 @@ class ShardStep:
     ranks on one GPU, where RCCL refuses a duplicate device (the multi-rank
     GPU test); the count then reaches the host before its all_gather."""
 
-    def __init__(self, ctx, rank, world, device, group=None, host_collectives=False):
+    def __init__(self, ctx, rank, world, device, group=None, host_collectives=False, counts=None):
         import torch
 
         self.ctx = ctx
+        # counts: a HostCountExchange (ranks on one host): the row counts are
+        # exchanged through host shared memory after the pass, no count collective
+        self.xchg = counts
         device = torch.device(device)
         self.host = host_collectives and device.type == "cuda"
         self.gather = RowGather(rank, world, torch.device("cpu") if self.host else device, group)
@@ -185,7 +242,7 @@ class ShardStep:
         # behind the all_gather; finish() waits on its event and reads them (no
         # synchronous device-to-host read per step: the host's share of a short
         # step, e.g. one of eight shards of config 4)
-        self.pinned = device.type == "cuda" and not self.host
+        self.pinned = device.type == "cuda" and not self.host and counts is None
         if self.pinned:
             self.cnts_host = torch.empty(world, dtype=torch.int64, pin_memory=True)
             self.cnts_evt = torch.cuda.Event()
@@ -198,6 +255,11 @@ class ShardStep:
         import torch.distributed as dist
 
         g = self.gather
+        if self.xchg is not None:  # the pass alone: its count is read on the host in finish()
+            self.ctx.run_chunks_async(thr, chunk_begin, chunk_end)
+            if kernel_done is not None:
+                kernel_done.record(self.stream)
+            return
         with _stream_scope(self.stream):
             self.ctx.run_chunks_async(thr, chunk_begin, chunk_end, (self.cnt_dev if self.host else g.cnt).data_ptr())
             if kernel_done is not None:
@@ -214,6 +276,18 @@ class ShardStep:
         import torch.distributed as dist
 
         g = self.gather
+        if self.xchg is not None:
+            n = self.ctx.run_wait()  # this rank's pass completed; its row count on the host
+            counts = self.xchg(n)
+            self.rows_seen = max(counts) > 0
+            if not self.rows_seen:
+                if self._no_rows is None:
+                    self._no_rows = g.cnt.new_zeros((5, 0), dtype=torch.int32)
+                return n, (self._no_rows if g.rank == 0 else None)
+            packed = pack_rows_device(self.ctx, n, self.device)
+            if self.host:
+                packed = packed.cpu()
+            return n, (packed if g.world == 1 else g(packed, counts))
         if self.host:
             with _stream_scope(self.stream):
                 g.cnt.fill_(int(self.cnt_dev.item()))  # host wait for this step's count
@@ -267,11 +341,12 @@ class PipelinedShardStep:
     on every rank (count all_gathers in submit order, a step's row gather when
     it completes), so the sequence is the same everywhere."""
 
-    def __init__(self, ctxs, rank, world, device, group=None, serialize_kernels=False, host_collectives=False):
+    def __init__(self, ctxs, rank, world, device, group=None, serialize_kernels=False, host_collectives=False,
+                 counts=None):
         import torch
 
         assert len(ctxs) >= 2
-        self.steps = [ShardStep(c, rank, world, device, group, host_collectives) for c in ctxs]
+        self.steps = [ShardStep(c, rank, world, device, group, host_collectives, counts) for c in ctxs]
         self.done = ([torch.cuda.Event() for _ in ctxs] if torch.device(device).type == "cuda"
                      else [_HostEvent() for _ in ctxs])
         self.serialize = serialize_kernels  # False: step i's kernel may start in step i-1's tail
