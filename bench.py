@@ -799,6 +799,10 @@ def main():
                      else "pair_fp6_screen_kernel<fp6 x fp4 16x16x128>")
         elif screen_kind == 4:
             kname = "pair_mfma_kernel<candidate pairs, %d planes>" % min(planes, 2)
+        elif screened and screen_kind == 1 and ctx.get_option("i8_pairs") and NP <= 16384 and \
+                bool(np.all(weights >= 0)) and (L + 63) // 64 <= 0x7FFF:
+            # the i8 one-plane screen on the tile-pair list (WLD_OPT_I8_PAIRS)
+            kname = "pair_i8_screen2w_kernel<tile pairs, 32x64 per wave, i8 16x16x64, pre-multiplied operands>"
         elif screened:
             kname = "pair_mfma_kernel<screen,%d plane%s>" % ((2, "s") if screen_kind == 3 else (1, ""))
         else:
@@ -858,7 +862,10 @@ def main():
                           "unscreened_frac": alg_ops / (unscreened_ms * 1e-3) / 1e12 / roof["peak"]}
     # PMC traffic (profiles/traffic.json) was measured on the default C4 line's
     # dominant kernel (the one-plane i8 screen); other lines report null
-    tr = load_traffic(args.config + ("-unweighted" if args.unweighted else ""), "fp6" if fp6 else kern_name)
+    # (keyed by the data set too: the same kernel moves different bytes on linkage blocks)
+    tr = load_traffic(args.config + ("-unweighted" if args.unweighted else "") +
+                      ("-ldblocks" if args.data == "ldblocks" else ""),
+                      "fp6" if fp6 else "i8pairs" if roof.get("kernel", "").startswith("pair_i8_screen2w") else kern_name)
     same_kernel = (screen_kind == 1 and args.thr is None and not args.wide_weights
                    and not (args.rehearse_dist and args.rehearse_shard > 1))
     # ... and only for the kernel those counters were collected on

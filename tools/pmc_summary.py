@@ -9,7 +9,7 @@ import sys
 for f in sorted(glob.glob(sys.argv[1] + "/**/*_counter_collection.csv", recursive=True)):
   by_kernel = collections.defaultdict(lambda: (collections.defaultdict(list), {}))
   for r in csv.DictReader(open(f)):
-    if not any(k in r["Kernel_Name"] for k in ("pair_mfma", "pair_valu", "pair_fp6", "ref_item")):
+    if not any(k in r["Kernel_Name"] for k in ("pair_mfma", "pair_valu", "pair_fp6", "pair_i8", "ref_item")):
         continue
     agg, dur = by_kernel[r["Kernel_Name"].split("(")[0]]
     agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -27,7 +27,7 @@ for f in sorted(glob.glob(sys.argv[1] + "/**/*_counter_collection.csv", recursiv
             for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
                 if k in m:
                     out[k] = round(m[k] / m["SQ_WAVE_CYCLES"], 3)
-        for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_MISC", "FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"):
+        for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_MISC", "SQ_ACTIVE_INST_VALU", "SQ_LDS_BANK_CONFLICT", "FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"):
             if k in m:
                 out[k] = m[k]
         print(out)
