@@ -201,7 +201,6 @@ struct wld_ctx {
     // the last pass's phase times, read from its events only when the stats
     // are asked for (materialize_times; ~3 hipEventElapsedTime calls the N>1
     // step loop, which never reads them, does not pay)
-    uint32_t cand_grid_hint = 0;  // the next candidate launch's grid (last screened pass's sub-blocks)
     bool times_pending = false;
     bool times_screened = false;
     int times_order_end = 4;
@@ -484,7 +483,6 @@ int common_load(wld_ctx *c, const uint8_t *d_sites, const float *d_w, const uint
     c->plane_mask = c->kernel == WLD_KERNEL_MFMA && !c->opt_all_planes ? c->wst.plane_mask : all_planes;
     c->stats.load_ms = event_ms(c->ev[0], c->ev[1]);
     c->fp6_ok = c->fp6_better = c->fp6_tried = false;  // (fp6_prepare: at the first run that may use it)
-    c->cand_grid_hint = 0;
     c->i8img_ok = false;  // (i8img_prepare: at the first pass that screens on i8)
     c->stats.mfma_planes = c->kernel == WLD_KERNEL_MFMA ? __builtin_popcount(c->plane_mask) : 0;
     c->stats.kernel = c->kernel;
@@ -754,7 +752,6 @@ int launch_pairs(wld_ctx *c, float thr, const OrderArgs &o, const DenseArgs *den
         m.cand_work = reinterpret_cast<unsigned *>(ptr<unsigned long long>(c->counters) + 2) + 1;  // beside the ticket
         m.cand_buckets = reinterpret_cast<unsigned *>(set + 1);
         m.test_guard = c->opt_test_guard;
-        m.cand_grid_hint = c->cand_grid_hint;
         if (scan && !dense) m.scan = *scan;
         RefRowsLaunch rr{};
         if (ref_screen) {
@@ -1512,10 +1509,6 @@ int run_complete(wld_ctx *c, uint64_t *n_rows) {
     // (27.8 ms for every tile at C4) is cheaper
     if (c->ref_pairs_pass && h[0] * 10 > r.pairs) c->ref_pairs_bad_thr = std::max(c->ref_pairs_bad_thr, r.thr);
     c->times_screened = c->screened;
-    // the next candidate launch: a workgroup per candidate sub-block of this
-    // pass, 64 to kRefItemGrid (items hold up to four)
-    c->cand_grid_hint = c->screened && !c->ref_pairs_pass
-                            ? (uint32_t)std::min<uint64_t>(kRefItemGrid, std::max<uint64_t>(64, h[3])) : 0;
     c->stats.candidate_tiles = c->screened ? h[2] : c->n_tiles;
     c->stats.candidate_blocks = c->screened && !c->ref_pairs_pass ? h[3] : 16 * (uint64_t)c->n_tiles;
     if (n_rows) *n_rows = rows;

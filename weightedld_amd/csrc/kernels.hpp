@@ -150,11 +150,6 @@ struct ValuLaunch {
     // tile_count launches: the list's entries are 16-row blocks of candidate
     // tiles (pair_mfma.hip ScreenArgs::rb_items), counted by the buckets
     bool rb_items;
-    // the item launch's grid (0: kRefItemGrid), sized from the context's last
-    // screened pass (its items loop over the list from a work counter, so any
-    // grid computes every item; an empty launch of 64 workgroups dispatches
-    // faster than one of 1,024)
-    uint32_t grid_hint = 0;
 };
 // returns true when the run's chunk scan ran in the launch (v.scan given, the
 // item kernel of a full run); else the caller launches it
@@ -284,7 +279,6 @@ struct MfmaLaunch {
     // the i8 one-plane screen on the tile-pair list with pre-multiplied
     // operands (null: the per-tile LDS kernel)
     const I8Screen *i8img = nullptr;
-    uint32_t cand_grid_hint = 0;  // ValuLaunch::grid_hint of the candidate launch
 };
 // The fp6 screen's sample run over every stride-th entry of its list: probe[0]
 // = the sampled tiles holding a pair its bound cannot reject, probe[1] = the

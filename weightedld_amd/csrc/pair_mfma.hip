@@ -1545,7 +1545,6 @@ void launch_candidates(const MfmaLaunch &m, uint32_t n, uint32_t idx, const uint
         v.tile_buckets = sc.cand_buckets;
         v.bucket_cap = sc.cand_cap;
         v.rb_items = sc.rb_items != 0;
-        v.grid_hint = m.cand_grid_hint;
         v.scan = sc.scan;
         launch_pair_valu(v, o, nullptr, s);
         return;

@@ -1142,8 +1142,7 @@ bool launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
         } else if (v.tile_count) {
             if (v.safe) launch_v<false, true, false, true, true>(v, grid, flush, cs, o, dn, s);
             else if (v.rb_items)  // items of <= 4 sub-blocks, one per wave, no LDS staging
-                hipLaunchKernelGGL(ref_item_kernel<true>,
-                                   dim3(std::min<uint32_t>(4 * v.n_tiles, v.grid_hint ? v.grid_hint : kRefItemGrid)),
+                hipLaunchKernelGGL(ref_item_kernel<true>, dim3(std::min<uint32_t>(4 * v.n_tiles, kRefItemGrid)),
                                    dim3(256), 0, s, v.codes, v.w, v.site_ok, v.tiles, v.n_tiles, v.tile_bits,
                                    v.tile_work, v.tile_buckets, v.bucket_cap, v.L, v.NP, cs, v.ref_tail_n,
                                    v.n_chunk_rows, v.thr, o, v.scan);
