@@ -568,7 +568,13 @@ def main():
     # queued back to back with wld_run_after (WLD_PIPE_SERIALIZE / --pipe-depth
     # select the others)
     depth = args.pipe_depth or (3 if dist_on else 2)
-    serialize = os.environ.get("WLD_PIPE_SERIALIZE", "0" if dist_on else "pair")
+    # N=1 "auto" (default): both orders are timed on the warm contexts after
+    # the clock settle, interleaved, and the faster one runs the timed steps
+    # (profiles/r06i/: free screens C4 0.543 against 0.558 ms/step and C2
+    # 0.101 against 0.122, but LD blocks 1.220 against 1.186, where two
+    # contexts' i8 operand images, 2 x 160 MB, exceed the Infinity Cache)
+    serialize = os.environ.get("WLD_PIPE_SERIALIZE", "0" if dist_on else "auto")
+    serialize_trials = None  # N=1 auto: {mode: [ms/step of each trial]}
     ctxs1 = None  # N=1: the contexts of the pipelined loop
     if not dist_on and pipelined:
         ctxs1 = [ctx] + [new_ctx() for _ in range(max(2, depth) - 1)]
@@ -665,6 +671,21 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             settle_steps = int(t.item())
         run_steps(settle_steps)
+    if serialize == "auto":
+        serialize = "pair"
+        if ctxs1 is not None:
+            # a trial = about settle_s / 6 of steps (at least 4) in one order
+            n_trial = max(4, settle_steps // 6)
+            serialize_trials = {"pair": [], "0": []}
+            for _ in range(2):
+                for m in ("pair", "0"):
+                    serialize = m
+                    torch.cuda.synchronize()
+                    t1 = time.perf_counter()
+                    run_steps(n_trial)
+                    torch.cuda.synchronize()
+                    serialize_trials[m].append((time.perf_counter() - t1) * 1e3 / n_trial)
+            serialize = min(serialize_trials, key=lambda m: sum(serialize_trials[m]))
     run_steps(args.warmup)
     if dist_on:
         dist.barrier()
@@ -934,9 +955,13 @@ def main():
                        (", pipelined steps (%d contexts, %s)" % (
                            depth, {"0": "screens may overlap", "1": "serialized on the whole step",
                                    "stream": "one stream"}.get(
-                               serialize, "pair kernels queued back to back"))
+                               serialize, "pair kernels queued back to back") +
+                           (" (auto: the faster of two interleaved trials of each order)"
+                            if serialize_trials else ""))
                         if (pipe is not None or ctxs1 is not None) else ""))},
         "roofline": roof,
+        # N=1 "auto": ms/step of each trial of the two step orders (the timed steps ran the faster)
+        "pipe_order_trials_ms": serialize_trials,
         # SURVEY 8(d)'s no-reuse byte MODEL (2N bytes per pair as if every pair
         # re-read both site columns from HBM) — not a roofline: the kernel
         # stages columns through LDS/L2 and reads each far fewer times

@@ -148,14 +148,22 @@ class HostCountExchange:
         if world > 1:
             dist.barrier(group=group)  # every rank attached before the creator may unlink at close
 
-    def __call__(self, count):
+    def __call__(self, count, timeout_s=300.0):
         self.seq += 1
         s = self.slots[self.seq & 1]
         s[self.rank, 0] = count
         s[self.rank, 1] = self.seq
         steps = s[:, 1]
+        spins = 0
         while steps.min() < self.seq:
-            pass
+            spins += 1
+            if spins & 0xFFFF == 0:  # (a rank that died never publishes: fail instead of spinning forever)
+                import time
+                if spins == 0x10000:
+                    self._t0 = time.monotonic()
+                elif time.monotonic() - self._t0 > timeout_s:
+                    raise RuntimeError("HostCountExchange: step %d: ranks %s did not publish within %.0f s" % (
+                        self.seq, np.nonzero(steps < self.seq)[0].tolist(), timeout_s))
         return s[:, 0].tolist()
 
     def close(self):
