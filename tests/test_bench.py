@@ -72,6 +72,11 @@ def test_bench_json_line():
     cb = out["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["value"] > 0 and cb["cores"] >= 1
     assert out["config"]["workload"]
+    # N=1 auto step order: two trials of each order, the timed steps in the faster
+    tr = out["pipe_order_trials_ms"]
+    assert set(tr) == {"pair", "0"} and all(len(v) == 2 and min(v) > 0 for v in tr.values())
+    chosen = "screens may overlap" if sum(tr["0"]) < sum(tr["pair"]) else "pair kernels queued back to back"
+    assert chosen in out["config"]["parallelism"], out["config"]["parallelism"]
 
 
 def test_launcher_starts_n_ranks_before_the_gpu():
