@@ -943,6 +943,9 @@ __device__ __forceinline__ v8i f6_ldb(const uint8_t *p, uint32_t lane) {
 // faster: 17.5 / 16.7 / 16.5 against 19.5 / 17.3 / 17.0 cycles per
 // instruction at 1 / 2 / 3 waves per SIMD (tools/probes/fp6_unscaled_probe.hip);
 // screen C4 -4.1%, 1/8 shard -4.8% (profiles/r06c/).
+__device__ __forceinline__ v4f f6_mfma(const v8i &a, const v8i &b, const v4f &c) {
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 2, 4, 0, 0, 0, 0);
+}
 __device__ __forceinline__ void f6_block_mfma(v4f (&acc)[2][2], const v8i &ai, const v8i &am, const v8i &b) {
     constexpr int kOne = 0;
     constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
@@ -1209,13 +1212,35 @@ __global__ __launch_bounds__(256, 3) void pair_fp6_screen2w_kernel(
             }
             if (kb + 1 < NK) issue(cur, kb + 1, buf ^ 1);
             const uint8_t *g = smem + buf * kF6PStage;
+            // Two B slots rolled through the stage: block n's raw MFMAs, its
+            // minor mask in place, its masked MFMAs, then block n + 2's read
+            // into the same slot, in flight under block n + 1's eight MFMAs
+            // (round 6: C4 screen -1.6%, LD blocks -2% with the same order in
+            // the i8 screen, against reading blocks 2-3 only after blocks
+            // 0-1's MFMAs, where the compiler's one register set for them
+            // left the read's latency exposed; profiles/r06k/.  Reading row
+            // block 0's A and B block 0 first, or the next stage's copies
+            // issued after the reads, measured no better: profiles/r06l/)
             const v8i ai0 = f6_ld24(g + aoff, lane), am0 = f6_ld24(g + aoff + 1536, lane);
             const v8i ai1 = f6_ld24(g + aoff + kF6ABytes, lane), am1 = f6_ld24(g + aoff + kF6ABytes + 1536, lane);
+            v8i bs[2] = {f6_ldb(g + boff, lane), f6_ldb(g + boff + kF6BBytes, lane)};
 #pragma unroll
             for (int n = 0; n < 4; ++n) {
-                const v8i b = f6_ldb(g + boff + n * kF6BBytes, lane);
-                f6_block_mfma(acc[0][n], ai0, am0, b);
-                f6_block_mfma(acc[1][n], ai1, am1, b);
+                v8i &b = bs[n & 1];
+                constexpr int kMinor = 0x22222222;  // fp4 1.0 (minor) nibbles; 2.0 (major) is 0x4
+                acc[0][n][0][0] = f6_mfma(ai0, b, acc[0][n][0][0]);
+                acc[0][n][1][0] = f6_mfma(am0, b, acc[0][n][1][0]);
+                acc[1][n][0][0] = f6_mfma(ai1, b, acc[1][n][0][0]);
+                acc[1][n][1][0] = f6_mfma(am1, b, acc[1][n][1][0]);
+                __builtin_amdgcn_sched_barrier(0);
+                b = v8i{b[0] & kMinor, b[1] & kMinor, b[2] & kMinor, b[3] & kMinor, 0, 0, 0, 0};
+                acc[0][n][0][1] = f6_mfma(ai0, b, acc[0][n][0][1]);
+                acc[0][n][1][1] = f6_mfma(am0, b, acc[0][n][1][1]);
+                acc[1][n][0][1] = f6_mfma(ai1, b, acc[1][n][0][1]);
+                acc[1][n][1][1] = f6_mfma(am1, b, acc[1][n][1][1]);
+                __builtin_amdgcn_sched_barrier(0);
+                if (n + 2 < 4) b = f6_ldb(g + boff + (n + 2) * kF6BBytes, lane);
+                __builtin_amdgcn_sched_barrier(0);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
             buf ^= 1;
@@ -1363,23 +1388,32 @@ __global__ __launch_bounds__(256, 3) void pair_i8_screen2w_kernel(
         if (kb + 1 < NK) issue(kb + 1, buf ^ 1);
         const uint8_t *g = smem + buf * kI8PStage;
         v4i av[2][2];
+        auto ldb = [&](int n) { return *reinterpret_cast<const v4i *>(g + boff + n * 1024 + 16 * lane); };
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int x = 0; x < 2; ++x)
                 av[j][x] = *reinterpret_cast<const v4i *>(g + aoff + j * kI8ABytes + x * 1024 + 16 * lane);
+        // two B slots rolled through the stage, as the fp6 screen (round 6:
+        // LD-block screen -2%, profiles/r06k/)
+        v4i bs[2] = {ldb(0), ldb(1)};
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
-            const v4i b = *reinterpret_cast<const v4i *>(g + boff + n * 1024 + 16 * lane);
+            v4i &b = bs[n & 1];
             constexpr int kOnes = 0x01010101;  // the minor bit of each code byte
-            const v4i bmin = {b[0] & kOnes, b[1] & kOnes, b[2] & kOnes, b[3] & kOnes};
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int x = 0; x < 2; ++x) {
-                    acc[j][n][x][0] = mfma_i8_16(av[j][x], b, acc[j][n][x][0]);
-                    acc[j][n][x][1] = mfma_i8_16(av[j][x], bmin, acc[j][n][x][1]);
-                }
+                for (int x = 0; x < 2; ++x) acc[j][n][x][0] = mfma_i8_16(av[j][x], b, acc[j][n][x][0]);
+            __builtin_amdgcn_sched_barrier(0);
+            b = v4i{b[0] & kOnes, b[1] & kOnes, b[2] & kOnes, b[3] & kOnes};
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int x = 0; x < 2; ++x) acc[j][n][x][1] = mfma_i8_16(av[j][x], b, acc[j][n][x][1]);
+            __builtin_amdgcn_sched_barrier(0);
+            if (n + 2 < 4) b = ldb(n + 2);
+            __builtin_amdgcn_sched_barrier(0);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of this buffer done before the next barrier
         buf ^= 1;
