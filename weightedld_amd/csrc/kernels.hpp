@@ -201,7 +201,9 @@ constexpr uint32_t kCandidateGrid = 2048;
 // workgroups (three per CU, 256 CUs); extra workgroups would only queue (and
 // cost dispatch time when there is no candidate at all)
 constexpr uint32_t kRefCandidateGrid = 768;
-// ... and of its items (ref_item_kernel<LOOP>, one sub-block per wave: four per CU)
+// ... and of its items (ref_item_kernel<LOOP>, one sub-block per wave, five
+// workgroups per CU): 1,024 (4 per CU) measured faster than 768, 896 or
+// every slot (1,280) on LD blocks (profiles/r06t/, r06u/)
 constexpr uint32_t kRefItemGrid = 1024;
 // ... and of ref_sums_kernel / ref_compact_kernel (low-register: eight per CU)
 constexpr uint32_t kRefRowsGrid = 2048;

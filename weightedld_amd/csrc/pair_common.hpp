@@ -273,6 +273,20 @@ __device__ __forceinline__ void glds16_s(const void *sbase, uint32_t voff, uint3
         : "memory");
 }
 
+// ... and one dword per lane (64 lanes: 256 bytes to lds_dst + 4*lane)
+__device__ __forceinline__ void glds4_s(const void *sbase, uint32_t voff, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dword %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(sbase), "s"(lds_dst)
+        : "memory");
+}
+
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
 }

@@ -585,14 +585,12 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t x, int e) {
 #define WLD_REF_ITEM_WG 6  // workgroups per CU, full runs (<= 85 VGPRs: 72 with the shared A operands)
 #endif
 #ifndef WLD_REF_ITEML_WG
-#define WLD_REF_ITEML_WG 4  // ... the candidate loop (its loop state: <= 128 VGPRs)
+#define WLD_REF_ITEML_WG 5  // ... the candidate loop (<= 102 VGPRs: 75 with the LDS-staged operands)
 #endif
 // Full runs (not LOOP) load each stage's operands at its top instead of one
 // stage ahead: 70 instead of 96 VGPRs, six workgroups per CU instead of five,
 // and the co-resident waves cover the latency (C2 -2.5%, profiles/r05v/; the
-// matrix pipe fills only with many waves in their sums).  The
-// candidate loop keeps the prefetch (four workgroups per CU either way).
-constexpr bool kItemNoPrefetch = true;
+// matrix pipe fills only with many waves in their sums).
 // kItemAShare (full runs): the four waves of an item share its 16 rows,
 // so each forms the A operands (w x in, w x major) of one 16-position group of
 // a stage and writes them to LDS, and every wave reads all four: a quarter of
@@ -602,6 +600,16 @@ constexpr bool kItemNoPrefetch = true;
 // eight waves per SIMD), so vector instructions cost MFMA throughput directly.
 // C2 0.1184 -> 0.1114 ms (profiles/r05ad/; rows bit-identical, 191 tests).
 constexpr bool kItemAShare = true;
+// kItemStage (the candidate loop): each wave's stage operands — its 16 a rows'
+// and 16 b rows' 64 code bytes and the 64 weights — copied into a per-wave
+// three-slot LDS ring by LDS-DMA in whole 16-byte pieces (three copies per
+// stage), then read as the MFMA operands, instead of twelve fragment-shaped
+// global loads per stage (16 rows x 4 bytes per instruction) one stage
+// ahead.  LD blocks: the candidate launch 0.331 -> 0.314 ms at five
+// workgroups per CU (profiles/r06s/, r06t/, r06u/; four per CU: 0.318), PMC
+// MFMA busy 0.551 -> 0.573 (the guide's rule for fragment-shaped operand loads)
+constexpr bool kItemStage = true;
+constexpr uint32_t kItemSlot = 2048 + 256;  // A 1 KB | B 1 KB | weights 256 B
 template <bool LOOP>
 __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) void ref_item_kernel(
     const uint8_t *__restrict__ rcodes, const float *__restrict__ rw, const uint8_t *__restrict__ site_ok,
@@ -615,6 +623,8 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
     constexpr bool kAShare = kItemAShare && !LOOP;
     // (kAShare) two stages of A operands: [stage & 1][group][element][lane] (u, v)
     __shared__ float2 sAop[kAShare ? 2 * 16 * 64 : 1];
+    constexpr bool kStage = kItemStage && LOOP;
+    __shared__ __attribute__((aligned(16))) uint8_t sRing[kStage ? 4 * 3 * kItemSlot : 16];
     const uint32_t tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
@@ -646,17 +656,9 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
             const uint32_t cls = 64 * ref_cs, n_st = 8 * ref_cs;
             uint32_t ca[4], cb[4];
             float4 cw[4];
-            auto fetch = [&](uint32_t k0) {
-#pragma unroll
-                for (int grp = 0; grp < 4; ++grp) {
-                    ca[grp] = *reinterpret_cast<const uint32_t *>(rowA + k0 + 16 * grp);
-                    cb[grp] = *reinterpret_cast<const uint32_t *>(rowB + k0 + 16 * grp);
-                    cw[grp] = *reinterpret_cast<const float4 *>(wg + k0 + 16 * grp);
-                }
-            };
             // the scalar tail's codes and weights (positions 8 cls .. 8 cls + 7),
             // all loaded at once after the last stage (one round trip, not one
-            // per position), into the stage prefetch registers: ca[e] / cb[e] =
+            // per position): ca[e] / cb[e] =
             // a row e's bytes 0-3 / 4-7, cw[0], cw[1] = the weights, cw[2].x /
             // .y = the b row's bytes
             auto fetch_tail = [&] {
@@ -673,7 +675,6 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                 cw[2].x = __uint_as_float(b8.x);
                 cw[2].y = __uint_as_float(b8.y);
             };
-            constexpr bool kNoPrefetch = kItemNoPrefetch && !LOOP;
             if constexpr (kAShare) {
                 // this wave's share: group `wave` of each stage (rows of the item's
                 // row block, lane (r, g) its row r, elements 4 e + g)
@@ -732,48 +733,77 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                             for (int q = 0; q < 4; ++q) tot[e][q] += acc[q][e];
                     }
                 }
-            } else {
-            if (n_st && !kNoPrefetch) fetch(0);
-            v4f acc[4];
-            uint32_t in_cls = 0;  // this stage's index in its class (no modulo in the loop)
-            for (uint32_t st = 0; st < n_st; ++st) {
-                if (in_cls == 0)
+            } else if constexpr (kStage) {
+                // slot s of this wave's ring: A image (lane l's 16 bytes at 16 l:
+                // a row l / 4, piece (l & 3) ^ ((l >> 4) & 3) of the stage's 64
+                // bytes, so the reads below hit distinct banks), B image the
+                // same, then the 64 weights
+                const uint32_t ring = lds_addr(sRing) + wave * 3 * kItemSlot;
+                const uint8_t *baseA = rcodes + (size_t)(a0 + 16 * ui) * NPr;
+                const uint8_t *baseB = rcodes + (size_t)(b0 + 16 * un) * NPr;
+                const uint32_t voff = (lane >> 2) * NPr + 16 * ((lane & 3) ^ ((lane >> 4) & 3));
+                auto issue = [&](uint32_t st, uint32_t slot) {
+                    const uint32_t d = ring + slot * kItemSlot, k0 = 64 * st;
+                    glds16_s(baseA + k0, voff, d);
+                    glds16_s(baseB + k0, voff, d + 1024);
+                    glds4_s(rw + k0, 4 * lane, d + 2048);
+                };
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (only the ring's copies counted below)
+                if (n_st) issue(0, 0);
+                if (n_st > 1) issue(1, 1);
+                v4f acc[4];
+                uint32_t in_cls = 0, slot = 0;
+                for (uint32_t st = 0; st < n_st; ++st) {
+                    if (in_cls == 0)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) acc[q] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-                uint32_t A[4], B[4];
-                float4 Wt[4];
-                if constexpr (kNoPrefetch) fetch(64 * st);  // this stage's operands, at its top
+                        for (int q = 0; q < 4; ++q) acc[q] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+                    // stage st + 2 into the slot stage st - 1 was read from (its
+                    // reads done), then wait for stage st's three copies
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (st + 2 < n_st) {
+                        issue(st + 2, slot == 0 ? 2u : slot - 1u);
+                        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                    } else if (st + 1 < n_st) {
+                        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+                    } else {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                    const uint8_t *p = sRing + (wave * 3 + slot) * kItemSlot;
+                    uint32_t A[4], B[4];
+                    float4 Wt[4];
 #pragma unroll
-                for (int grp = 0; grp < 4; ++grp) A[grp] = ca[grp], B[grp] = cb[grp], Wt[grp] = cw[grp];
-                if (!kNoPrefetch && st + 1 < n_st) fetch(64 * (st + 1));  // (classes are consecutive: stage st at 64 st)
+                    for (int grp = 0; grp < 4; ++grp) {
+                        const uint32_t pos = 16 * (4 * r + (grp ^ ((r >> 2) & 3))) + 4 * g;
+                        A[grp] = *reinterpret_cast<const uint32_t *>(p + pos);
+                        B[grp] = *reinterpret_cast<const uint32_t *>(p + 1024 + pos);
+                        Wt[grp] = *reinterpret_cast<const float4 *>(p + 2048 + 4 * (16 * grp + 4 * g));
+                    }
 #pragma unroll
-                for (int grp = 0; grp < 4; ++grp) {
-                    const float we[4] = {Wt[grp].x, Wt[grp].y, Wt[grp].z, Wt[grp].w};
-                    // the four elements' in / major bits as bytes 0/1 (one mask
-                    // per dword), each turned into 0.0/1.0 by a byte convert
-                    const uint32_t ai = A[grp] & 0x01010101u, am = (A[grp] >> 1) & 0x01010101u;
-                    const uint32_t bi = B[grp] & 0x01010101u, bm = (B[grp] >> 1) & 0x01010101u;
+                    for (int grp = 0; grp < 4; ++grp) {
+                        const float we[4] = {Wt[grp].x, Wt[grp].y, Wt[grp].z, Wt[grp].w};
+                        const uint32_t ai = A[grp] & 0x01010101u, am = (A[grp] >> 1) & 0x01010101u;
+                        const uint32_t bi = B[grp] & 0x01010101u, bm = (B[grp] >> 1) & 0x01010101u;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        // w x 1.0 or w x 0.0: exact; a -0.0 term (negative w
-                        // masked) adds nothing to a chain that starts at +0.0
-                        const float u = we[e] * cvt_ubyte<0>(ai, e), v = we[e] * cvt_ubyte<0>(am, e);
-                        const float fi = cvt_ubyte<1>(bi, e), fm = cvt_ubyte<1>(bm, e);
-                        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fi, acc[0], 0, 0, 0);
-                        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fi, acc[1], 0, 0, 0);
-                        acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fm, acc[2], 0, 0, 0);
-                        acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fm, acc[3], 0, 0, 0);
+                        for (int e = 0; e < 4; ++e) {
+                            // w x 1.0 or w x 0.0: exact; a -0.0 term (negative w
+                            // masked) adds nothing to a chain that starts at +0.0
+                            const float u = we[e] * cvt_ubyte<0>(ai, e), v = we[e] * cvt_ubyte<0>(am, e);
+                            const float fi = cvt_ubyte<1>(bi, e), fm = cvt_ubyte<1>(bm, e);
+                            acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fi, acc[0], 0, 0, 0);
+                            acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fi, acc[1], 0, 0, 0);
+                            acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(u, fm, acc[2], 0, 0, 0);
+                            acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, fm, acc[3], 0, 0, 0);
+                        }
+                    }
+                    slot = slot == 2 ? 0u : slot + 1u;
+                    if (++in_cls == ref_cs) {
+                        in_cls = 0;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) tot[e][q] += acc[q][e];
                     }
                 }
-                // end of a class: its chain joins the ordered horizontal sum
-                if (++in_cls == ref_cs) {
-                    in_cls = 0;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) tot[e][q] += acc[q][e];
-                }
-            }
             }
             // the scalar tail (lib.rs:461-480), onto the horizontal sums in order
             // (ref_tail_n <= 7, uniform)
