@@ -625,6 +625,10 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
     __shared__ float2 sAop[kAShare ? 2 * 16 * 64 : 1];
     constexpr bool kStage = kItemStage && LOOP;
     __shared__ __attribute__((aligned(16))) uint8_t sRing[kStage ? 4 * 3 * kItemSlot : 16];
+    // (full runs, kAShare: each wave's B rows staged by LDS-DMA in a two-slot
+    // ring instead of four fragment-shaped loads per stage; C2's launch
+    // 0.111 -> 0.104 ms, profiles/r06aj/)
+    __shared__ __attribute__((aligned(16))) uint8_t sBRing[kAShare ? 4 * 2 * 1024 : 16];
     const uint32_t tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
@@ -651,7 +655,6 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
         if (has || kAShare) {
             const uint32_t urow = kAShare ? (uint32_t)__builtin_ctz(owned) : ui;
             const uint8_t *rowA = rcodes + (size_t)(a0 + 16 * urow + r) * NPr + 4 * g;
-            const uint8_t *rowB = rcodes + (size_t)(b0 + 16 * un + r) * NPr + 4 * g;
             const float *wg = rw + 4 * g;
             const uint32_t cls = 64 * ref_cs, n_st = 8 * ref_cs;
             uint32_t ca[4], cb[4];
@@ -680,17 +683,20 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                 // row block, lane (r, g) its row r, elements 4 e + g)
                 const uint8_t *rowAs = rowA + 16 * wave;
                 const float *wgs = wg + 16 * wave;
-                uint32_t sa_c = 0, nb[4];
+                uint32_t sa_c = 0;
                 float4 sa_w = make_float4(0.f, 0.f, 0.f, 0.f);
                 auto fetch2 = [&](uint32_t k0) {
                     sa_c = *reinterpret_cast<const uint32_t *>(rowAs + k0);
                     sa_w = *reinterpret_cast<const float4 *>(wgs + k0);
-                    if (has)
-#pragma unroll
-                        for (int grp = 0; grp < 4; ++grp)
-                            nb[grp] = *reinterpret_cast<const uint32_t *>(rowB + k0 + 16 * grp);
                 };
+                // this wave's 16 b rows' 64 bytes of stage st in ring slot st & 1
+                // (lane l's 16 bytes at 16 l: row l / 4, piece (l & 3) ^ ((l >> 4) & 3))
+                const uint32_t bring = lds_addr(sBRing) + wave * 2 * 1024;
+                const uint8_t *baseB = rcodes + (size_t)(b0 + 16 * un) * NPr;
+                const uint32_t bvoff = (lane >> 2) * NPr + 16 * ((lane & 3) ^ ((lane >> 4) & 3));
+                auto issueB = [&](uint32_t st) { glds16_s(baseB + 64 * st, bvoff, bring + (st & 1u) * 1024); };
                 if (n_st) fetch2(0);
+                if (has && n_st) issueB(0);
                 v4f acc[4];
                 uint32_t in_cls = 0;
                 for (uint32_t st = 0; st < n_st; ++st) {
@@ -706,10 +712,21 @@ __global__ __launch_bounds__(256, LOOP ? WLD_REF_ITEML_WG : WLD_REF_ITEM_WG) voi
                             dst[64 * e] = make_float2(we[e] * cvt_ubyte<0>(ai, e), we[e] * cvt_ubyte<0>(am, e));
                     }
                     uint32_t B[4];
-#pragma unroll
-                    for (int grp = 0; grp < 4; ++grp) B[grp] = nb[grp];
+                    if (has) {  // (uniform per wave)
+                        // stage st + 1's B into the slot this wave read stage st - 1
+                        // from; stage st's copy (the only load outstanding here) is
+                        // waited for first — the compiler waits before the asm anyway
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (st + 1 < n_st) issueB(st + 1);
+                    }
                     if (st + 1 < n_st) fetch2(64 * (st + 1));
                     __syncthreads();  // the stage's four groups written (and the buffer's last readers done)
+                    if (has) {
+                        const uint8_t *pb = sBRing + (wave * 2 + (st & 1u)) * 1024;
+#pragma unroll
+                        for (int grp = 0; grp < 4; ++grp)
+                            B[grp] = *reinterpret_cast<const uint32_t *>(pb + 16 * (4 * r + (grp ^ ((r >> 2) & 3))) + 4 * g);
+                    }
                     const float2 *src = sAop + (st & 1) * 1024 + lane;
                     if (has)  // (uniform per wave)
 #pragma unroll
