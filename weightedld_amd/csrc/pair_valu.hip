@@ -538,16 +538,18 @@ __global__ __launch_bounds__(256) void ref_layout_kernel(const uint8_t *__restri
     if (s == 0) rw[p] = seq < N ? w[seq] : 0.0f;
 }
 
-// Work items of lib.rs's order on f32 MFMA with no LDS staging: an item is
-// up to four 16x16 sub-blocks of one 64x64 tile (`bits`), one per wave (the
-// u-th computed sub-block in column-major order goes to wave u), owning the
-// 16-row blocks `owned` of the tile's segments.  Each wave reads its own
-// operands straight from the lane-class layout (L2-resident): per 64-position
-// stage, lane (r, g) loads the dword of its a row and of its b row at 16 grp
-// + 4 g (elements 16 grp + 4 e + g, e = 0..3, of the four 16-element groups
-// grp) and the four weights beside them, one stage ahead of the MFMAs; the
-// waves never wait for each other before the epilogue.  Same sums, same
-// order, same epilogue as pair_valu_kernel<MF, REF> (bit-identical rows).
+// Work items of lib.rs's order on f32 MFMA: an item is up to four 16x16
+// sub-blocks of one 64x64 tile (`bits`), one per wave (the u-th computed
+// sub-block in column-major order goes to wave u), owning the 16-row blocks
+// `owned` of the tile's segments.  Per 64-position stage, lane (r, g) needs
+// the dword of its a row and of its b row at 16 grp + 4 g (elements 16 grp +
+// 4 e + g, e = 0..3, of the four 16-element groups grp) and the four weights
+// beside them.  The candidate loop copies each wave's stage operands into a
+// per-wave LDS ring by LDS-DMA (kItemStage: no barriers, the waves never wait
+// for each other before the epilogue); full runs share each stage's A
+// operands through LDS (kItemAShare, a barrier per stage) and copy each
+// wave's B rows into a per-wave ring the same way.  Same sums, same order,
+// same epilogue as pair_valu_kernel<MF, REF> (bit-identical rows).
 // LOOP: the candidate launch over the screen's item list (buckets, work
 // counter, fused chunk scan); else the full run's tiles in four 16-row items
 // each (workgroup 4t + q: tile t's row block q).
@@ -1188,7 +1190,7 @@ bool launch_pair_valu(const ValuLaunch &v, const OrderArgs &o, const DenseArgs *
             else launch_v<true, false, true, true, false>(v, grid, flush, cs, o, dn, s);
         } else if (v.tile_count) {
             if (v.safe) launch_v<false, true, false, true, true>(v, grid, flush, cs, o, dn, s);
-            else if (v.rb_items)  // items of <= 4 sub-blocks, one per wave, no LDS staging
+            else if (v.rb_items)  // items of <= 4 sub-blocks, one per wave
                 hipLaunchKernelGGL(ref_item_kernel<true>, dim3(std::min<uint32_t>(4 * v.n_tiles, kRefItemGrid)),
                                    dim3(256), 0, s, v.codes, v.w, v.site_ok, v.tiles, v.n_tiles, v.tile_bits,
                                    v.tile_work, v.tile_buckets, v.bucket_cap, v.L, v.NP, cs, v.ref_tail_n,
